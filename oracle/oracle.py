@@ -1,0 +1,282 @@
+"""ctypes wrapper over the C parity oracle (oracle/ckks_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, never by the product (fhe-spear_amd/).  See ckks_oracle.h for what each
+function restates and which reference file:line it follows.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "_build" / "libckks_oracle.so"
+
+_u64p = C.POINTER(C.c_uint64)
+_dblp = C.POINTER(C.c_double)
+
+
+def build(quiet: bool = True) -> Path:
+    """Compile the oracle with gcc (Makefile next to this file)."""
+    out = subprocess.run(["make", "-C", str(HERE)], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        L.ock_ctx_create.restype = C.c_void_p
+        L.ock_ctx_create.argtypes = [C.c_uint64, _u64p, C.c_int, C.c_int]
+        L.ock_ctx_destroy.argtypes = [C.c_void_p]
+        L.ock_create_coeff_modulus.argtypes = [C.c_uint64, C.POINTER(C.c_int), C.c_int, _u64p]
+        L.ock_galois_elt_from_step.restype = C.c_uint64
+        L.ock_galois_elt_from_step.argtypes = [C.c_int, C.c_uint64]
+        for name in ("ock_splitmix64",):
+            getattr(L, name).restype = C.c_uint64
+            getattr(L, name).argtypes = [C.c_uint64]
+        L.ock_stream_key.restype = C.c_uint64
+        L.ock_stream_key.argtypes = [C.c_uint64, C.c_uint64]
+        L.ock_rnd.restype = C.c_uint64
+        L.ock_rnd.argtypes = [C.c_uint64, C.c_uint64]
+        vp = C.c_void_p
+        L.ock_ntt_fwd.argtypes = [vp, _u64p, C.c_int]
+        L.ock_ntt_inv.argtypes = [vp, _u64p, C.c_int]
+        L.ock_apply_galois_ntt.argtypes = [vp, _u64p, _u64p, C.c_uint64]
+        for name in ("ock_add", "ock_sub", "ock_multiply_plain", "ock_add_plain"):
+            getattr(L, name).argtypes = [vp, _u64p, _u64p, _u64p, C.c_int, C.c_int]
+        L.ock_negate.argtypes = [vp, _u64p, _u64p, C.c_int, C.c_int]
+        L.ock_multiply.argtypes = [vp, _u64p, _u64p, _u64p, C.c_int]
+        L.ock_rescale_to_next.argtypes = [vp, _u64p, _u64p, C.c_int, C.c_int]
+        L.ock_keyswitch.argtypes = [vp, _u64p, _u64p, C.c_int, _u64p, _u64p]
+        L.ock_rotate.argtypes = [vp, _u64p, _u64p, C.c_uint64, C.c_int, _u64p]
+        L.ock_relinearize.argtypes = [vp, _u64p, _u64p, C.c_int, _u64p]
+        L.ock_bsgs_loop.argtypes = [vp, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p),
+                                    C.c_int, C.c_int, C.c_int, C.c_int, _u64p]
+        L.ock_gen_secret.argtypes = [vp, C.c_uint64, _u64p]
+        L.ock_gen_switch_key.argtypes = [vp, C.c_uint64, C.c_uint64, _u64p, _u64p, _u64p]
+        L.ock_gen_galois_key.argtypes = [vp, C.c_uint64, _u64p, C.c_uint64, _u64p]
+        L.ock_gen_relin_key.argtypes = [vp, C.c_uint64, _u64p, _u64p]
+        L.ock_gen_public_key.argtypes = [vp, C.c_uint64, _u64p, _u64p]
+        L.ock_encrypt_symmetric.argtypes = [vp, C.c_uint64, C.c_uint64, _u64p, _u64p, C.c_int, _u64p]
+        L.ock_encrypt_asymmetric.argtypes = [vp, C.c_uint64, C.c_uint64, _u64p, _u64p, C.c_int, _u64p]
+        L.ock_decrypt.argtypes = [vp, _u64p, _u64p, C.c_int, C.c_int, _u64p]
+        L.ock_encode_complex.argtypes = [vp, _dblp, C.c_size_t, C.c_double, C.c_int, _u64p]
+        L.ock_decode_complex.argtypes = [vp, _u64p, C.c_int, C.c_double, _dblp]
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_u64p)
+
+
+def create_coeff_modulus(N: int, bits) -> list[int]:
+    bits = list(bits)
+    arr = (C.c_int * len(bits))(*bits)
+    out = np.zeros(len(bits), dtype=np.uint64)
+    rc = lib().ock_create_coeff_modulus(N, arr, len(bits), _p(out))
+    if rc != 0:
+        raise ValueError(f"create_coeff_modulus failed rc={rc}")
+    return [int(x) for x in out]
+
+
+def galois_elt(step: int, N: int) -> int:
+    return int(lib().ock_galois_elt_from_step(step, N))
+
+
+class Oracle:
+    """Parameter set + tables.  primes: key-level list (L0 data primes, then P special)."""
+
+    def __init__(self, N: int, primes, special: int):
+        self.N = N
+        self.primes = [int(q) for q in primes]
+        self.P = special
+        self.L0 = len(self.primes) - special
+        self.K = len(self.primes)
+        arr = np.array(self.primes, dtype=np.uint64)
+        self._h = lib().ock_ctx_create(N, _p(arr), len(self.primes), special)
+        if not self._h:
+            raise ValueError("bad oracle parameters")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ock_ctx_destroy(h)
+            self._h = None
+
+    @property
+    def dnum(self):
+        return (self.L0 + self.P - 1) // self.P
+
+    # --- transforms
+    def ntt(self, limb: np.ndarray, prime_idx: int) -> np.ndarray:
+        a = np.ascontiguousarray(limb, dtype=np.uint64).copy()
+        lib().ock_ntt_fwd(self._h, _p(a), prime_idx)
+        return a
+
+    def intt(self, limb: np.ndarray, prime_idx: int) -> np.ndarray:
+        a = np.ascontiguousarray(limb, dtype=np.uint64).copy()
+        lib().ock_ntt_inv(self._h, _p(a), prime_idx)
+        return a
+
+    def galois_ntt(self, limb: np.ndarray, elt: int) -> np.ndarray:
+        a = np.ascontiguousarray(limb, dtype=np.uint64)
+        out = np.empty_like(a)
+        lib().ock_apply_galois_ntt(self._h, _p(a), _p(out), elt)
+        return out
+
+    # --- ciphertext ops; ct arrays are (ncomp, l, N) uint64
+    def _bin(self, fn, a, b, ncomp, l, out_shape=None):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        b = np.ascontiguousarray(b, dtype=np.uint64)
+        out = np.empty(out_shape or a.shape, dtype=np.uint64)
+        fn(self._h, _p(a), _p(b), _p(out), ncomp, l)
+        return out
+
+    def add(self, a, b):
+        return self._bin(lib().ock_add, a, b, a.shape[0], a.shape[1])
+
+    def sub(self, a, b):
+        return self._bin(lib().ock_sub, a, b, a.shape[0], a.shape[1])
+
+    def negate(self, a):
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        out = np.empty_like(a)
+        lib().ock_negate(self._h, _p(a), _p(out), a.shape[0], a.shape[1])
+        return out
+
+    def multiply_plain(self, ct, pt):
+        return self._bin(lib().ock_multiply_plain, ct, pt, ct.shape[0], ct.shape[1])
+
+    def add_plain(self, ct, pt):
+        return self._bin(lib().ock_add_plain, ct, pt, ct.shape[0], ct.shape[1])
+
+    def multiply(self, a, b):
+        l = a.shape[1]
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        b = np.ascontiguousarray(b, dtype=np.uint64)
+        out = np.empty((3, l, self.N), dtype=np.uint64)
+        lib().ock_multiply(self._h, _p(a), _p(b), _p(out), l)
+        return out
+
+    def rescale(self, ct):
+        ncomp, l, N = ct.shape
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.empty((ncomp, l - 1, N), dtype=np.uint64)
+        lib().ock_rescale_to_next(self._h, _p(ct), _p(out), ncomp, l)
+        return out
+
+    def keyswitch(self, a, key):
+        l = a.shape[0]
+        a = np.ascontiguousarray(a, dtype=np.uint64)
+        key = np.ascontiguousarray(key, dtype=np.uint64)
+        o0 = np.empty((l, self.N), dtype=np.uint64)
+        o1 = np.empty_like(o0)
+        lib().ock_keyswitch(self._h, _p(a), _p(key), l, _p(o0), _p(o1))
+        return o0, o1
+
+    def rotate(self, ct, gkey, step: int):
+        l = ct.shape[1]
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.empty_like(ct)
+        lib().ock_rotate(self._h, _p(ct), _p(np.ascontiguousarray(gkey)), galois_elt(step, self.N), l, _p(out))
+        return out
+
+    def rotate_elt(self, ct, gkey, elt: int):
+        l = ct.shape[1]
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.empty_like(ct)
+        lib().ock_rotate(self._h, _p(ct), _p(np.ascontiguousarray(gkey)), elt, l, _p(out))
+        return out
+
+    def relinearize(self, ct3, rlk):
+        l = ct3.shape[1]
+        ct3 = np.ascontiguousarray(ct3, dtype=np.uint64)
+        out = np.empty((2, l, self.N), dtype=np.uint64)
+        lib().ock_relinearize(self._h, _p(ct3), _p(np.ascontiguousarray(rlk)), l, _p(out))
+        return out
+
+    def bsgs_loop(self, baby, pts, gkeys_by_giant, G, B, D):
+        """bg:464-485 restated.  gkeys_by_giant[g] is the key for step g*G (entry 0 unused)."""
+        l = baby[0].shape[1]
+        baby = [np.ascontiguousarray(b, dtype=np.uint64) for b in baby]
+        pts = [np.ascontiguousarray(p, dtype=np.uint64) for p in pts]
+        keys = [np.ascontiguousarray(k, dtype=np.uint64) if k is not None else baby[0] for k in gkeys_by_giant]
+        BA = (_u64p * len(baby))(*[_p(b) for b in baby])
+        PA = (_u64p * len(pts))(*[_p(p) for p in pts])
+        KA = (_u64p * len(keys))(*[_p(k) for k in keys])
+        out = np.empty((2, l - 1, self.N), dtype=np.uint64)
+        lib().ock_bsgs_loop(self._h, BA, PA, KA, G, B, D, l, _p(out))
+        return out
+
+    # --- keys / encryption
+    def gen_secret(self, seed: int):
+        s = np.empty((self.K, self.N), dtype=np.uint64)
+        lib().ock_gen_secret(self._h, seed, _p(s))
+        return s
+
+    def key_shape(self):
+        return (self.dnum, 2, self.K, self.N)
+
+    def gen_galois_key(self, seed: int, s, elt: int):
+        k = np.empty(self.key_shape(), dtype=np.uint64)
+        lib().ock_gen_galois_key(self._h, seed, _p(s), elt, _p(k))
+        return k
+
+    def gen_relin_key(self, seed: int, s):
+        k = np.empty(self.key_shape(), dtype=np.uint64)
+        lib().ock_gen_relin_key(self._h, seed, _p(s), _p(k))
+        return k
+
+    def gen_public_key(self, seed: int, s):
+        pk = np.empty((2, self.L0, self.N), dtype=np.uint64)
+        lib().ock_gen_public_key(self._h, seed, _p(s), _p(pk))
+        return pk
+
+    def encrypt_symmetric(self, seed: int, counter: int, s, pt):
+        l = pt.shape[0]
+        ct = np.empty((2, l, self.N), dtype=np.uint64)
+        lib().ock_encrypt_symmetric(self._h, seed, counter, _p(s), _p(np.ascontiguousarray(pt)), l, _p(ct))
+        return ct
+
+    def encrypt_asymmetric(self, seed: int, counter: int, pk, pt):
+        l = pt.shape[0]
+        ct = np.empty((2, l, self.N), dtype=np.uint64)
+        lib().ock_encrypt_asymmetric(self._h, seed, counter, _p(np.ascontiguousarray(pk)),
+                                     _p(np.ascontiguousarray(pt)), l, _p(ct))
+        return ct
+
+    def decrypt(self, s, ct):
+        ncomp, l, N = ct.shape
+        pt = np.empty((l, N), dtype=np.uint64)
+        lib().ock_decrypt(self._h, _p(s), _p(np.ascontiguousarray(ct)), ncomp, l, _p(pt))
+        return pt
+
+    def encode(self, values, scale: float, l: int):
+        z = np.asarray(values)
+        zc = np.zeros((len(z), 2), dtype=np.float64)
+        zc[:, 0] = np.real(z)
+        zc[:, 1] = np.imag(z) if np.iscomplexobj(z) else 0.0
+        zc = np.ascontiguousarray(zc)
+        pt = np.empty((l, self.N), dtype=np.uint64)
+        lib().ock_encode_complex(self._h, zc.ctypes.data_as(_dblp), len(z), scale, l, _p(pt))
+        return pt
+
+    def decode(self, pt, scale: float):
+        l = pt.shape[0]
+        z = np.empty((self.N // 2, 2), dtype=np.float64)
+        lib().ock_decode_complex(self._h, _p(np.ascontiguousarray(pt)), l, scale, z.ctypes.data_as(_dblp))
+        return z[:, 0] + 1j * z[:, 1]
