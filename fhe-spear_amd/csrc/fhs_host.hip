@@ -1,0 +1,1474 @@
+// fhs_host.hip -- host side of libfhespear_hip.so: parameter tables, object lifetime, key
+// generation, CKKS encode/decode, and every extern "C" entry point of include/fhespear.h.
+//
+// Runtime model (MI355X-first):
+//  - one context = one device + one HIP stream; all device memory comes from the stream-ordered
+//    pool (hipMallocAsync / hipFreeAsync), so a free never synchronises the host;
+//  - calls on a context are serialised by a mutex (ctypes drops the GIL; bg:223-249 may call
+//    from a thread pool);
+//  - rotations are DEFERRED and batched: fhs_rotate allocates the output and queues the
+//    key-switch; the queue is flushed as one batched key-switch by the next operation that is
+//    not a rotation at the same level.  The reference's baby-step loop (bg:215-220) issues G-1
+//    independent rotations back to back; batching turns 39 workgroups per rotation into
+//    39 (G-1) workgroups per launch.  Each rotation is computed exactly as it would be alone.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fhespear.h"
+#include "fhs_kernels.h"
+#include "fhs_modarith.h"
+
+using fhs::DevTables;
+using fhs::KsItem;
+typedef unsigned __int128 hu128;
+
+// ============================================================================ errors
+static thread_local std::string g_err;
+static fhs_status fail(fhs_status code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+static fhs_status hip_fail(hipError_t e, const char* where) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+        return fail(FHS_ERR_OOM, std::string("HIP out of memory in ") + where);
+    return fail(FHS_ERR_HIP, std::string("HIP error in ") + where + ": " + hipGetErrorString(e));
+}
+#define HIPCHK(expr, where)                                  \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return hip_fail(_e, where);    \
+    } while (0)
+
+extern "C" const char* fhs_last_error(void) { return g_err.c_str(); }
+extern "C" const char* fhs_version(void) { return "fhespear-mi355x 0.1 (gfx950)"; }
+extern "C" int fhs_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+// ============================================================================ host number theory
+static inline uint64_t h_mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)(((hu128)a * b) % q); }
+static uint64_t h_pow(uint64_t b, uint64_t e, uint64_t q) {
+    uint64_t r = 1 % q;
+    b %= q;
+    while (e) {
+        if (e & 1) r = h_mulmod(r, b, q);
+        b = h_mulmod(b, b, q);
+        e >>= 1;
+    }
+    return r;
+}
+static uint64_t h_inv(uint64_t a, uint64_t q) { return h_pow(a % q, q - 2, q); }
+static uint64_t h_shoup(uint64_t w, uint64_t q) { return (uint64_t)(((hu128)w << 64) / q); }
+static bool h_is_prime(uint64_t n) {
+    if (n < 2) return false;
+    const uint64_t bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
+    for (uint64_t p : bases) {
+        if (n == p) return true;
+        if (n % p == 0) return false;
+    }
+    uint64_t d = n - 1;
+    int s = 0;
+    while (!(d & 1)) { d >>= 1; ++s; }
+    for (uint64_t a : bases) {
+        uint64_t x = h_pow(a, d, n);
+        if (x == 1 || x == n - 1) continue;
+        bool comp = true;
+        for (int r = 1; r < s && comp; ++r) {
+            x = h_mulmod(x, x, n);
+            if (x == n - 1) comp = false;
+        }
+        if (comp) return false;
+    }
+    return true;
+}
+static uint32_t h_bitrev(uint32_t x, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; ++i) { r = (r << 1) | (x & 1); x >>= 1; }
+    return r;
+}
+// minimal primitive 2N-th root of unity mod q (SEAL / Phantom convention)
+static uint64_t h_min_root(uint64_t q, uint64_t N) {
+    const uint64_t cof = (q - 1) / (2 * N);
+    uint64_t g = 0;
+    for (uint64_t c = 2;; ++c) {
+        g = h_pow(c, cof, q);
+        if (h_pow(g, N, q) == q - 1) break;
+    }
+    const uint64_t g2 = h_mulmod(g, g, q);
+    uint64_t best = g, cur = g;
+    for (uint64_t k = 1; k < N; ++k) {
+        cur = h_mulmod(cur, g2, q);
+        if (cur < best) best = cur;
+    }
+    return best;
+}
+
+extern "C" fhs_status fhs_create_coeff_modulus(uint64_t N, const int* bits, int n, uint64_t* out) {
+    if (!bits || !out || n <= 0 || N < 2 || (N & (N - 1))) return fail(FHS_ERR_INVALID, "create_coeff_modulus: bad args");
+    const uint64_t fac = 2 * N;
+    std::map<int, std::vector<uint64_t>> pool;
+    std::map<int, int> need, used;
+    for (int i = 0; i < n; ++i) {
+        if (bits[i] < 2 || bits[i] > 61) return fail(FHS_ERR_INVALID, "create_coeff_modulus: bit size must be in [2, 61]");
+        need[bits[i]]++;
+    }
+    for (auto& kv : need) {
+        const int b = kv.first;
+        uint64_t v = ((uint64_t)1 << b) - fac + 1;
+        const uint64_t lo = (uint64_t)1 << (b - 1);
+        while ((int)pool[b].size() < kv.second && v > lo) {
+            if (h_is_prime(v)) pool[b].push_back(v);
+            v -= fac;
+        }
+        if ((int)pool[b].size() < kv.second) return fail(FHS_ERR_INVALID, "create_coeff_modulus: not enough primes");
+    }
+    for (int i = 0; i < n; ++i) out[i] = pool[bits[i]][used[bits[i]]++];
+    return FHS_OK;
+}
+
+extern "C" uint64_t fhs_galois_elt_from_step(int step, uint64_t N) {
+    const uint64_t m = 2 * N;
+    if (step == 0) return m - 1;
+    const uint64_t slots = N / 2;
+    uint64_t s = step > 0 ? (uint64_t)step : slots - (uint64_t)(-(int64_t)step);
+    s %= slots;
+    uint64_t e = 1;
+    for (uint64_t i = 0; i < s; ++i) e = (e * 5) & (m - 1);
+    return e;
+}
+
+// ============================================================================ objects
+struct PendingRot {
+    KsItem item;
+    fhs_ciphertext* out;
+    const fhs_ciphertext* in;
+};
+
+struct fhs_context {
+    int device = 0;
+    hipStream_t st = nullptr;
+    std::recursive_mutex mu;
+    uint64_t N = 0;
+    int logN = 0, L0 = 0, P = 0, K = 0, dnum = 0;
+    std::vector<uint64_t> q;
+    std::vector<uint64_t> elts;
+    DevTables T{};
+    std::vector<void*> tables;     // device allocations owned by the context
+    void* items_dev = nullptr;     // KsItem[kMaxItems]
+    void* ptrs_dev = nullptr;      // pointer arrays for BSGS (2 x kMaxPtrs)
+    std::vector<PendingRot> pending;
+    int pending_l = -1;
+    std::set<const void*> pending_refs;
+    std::vector<std::complex<double>> fft_w;   // exp(2 pi i k / N), k < N
+    std::vector<uint64_t> slot_index;          // (5^j mod 2N - 1)/2, j < N/2
+    std::atomic<uint64_t> bytes_live{0};
+    // kernel timer (bench): events around the timed kernel launches
+    int timer_kernel = -1;   // 0 = k_bsgs_inner, 1 = k_modup_ip
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timer_pairs;
+    static constexpr int kMaxItems = 512;
+    static constexpr int kMaxPtrs = 1 << 16;
+};
+
+struct fhs_ciphertext {
+    fhs_context* ctx;
+    uint64_t* d;
+    int ncomp, ci, l;
+    double scale;
+};
+struct fhs_plaintext {
+    fhs_context* ctx;
+    uint64_t* d;
+    int ci, l;
+    double scale;
+};
+struct fhs_secret_key {
+    fhs_context* ctx;
+    uint64_t* s;   // K limbs, NTT
+    uint64_t seed;
+    uint64_t ctr;
+};
+struct fhs_public_key {
+    fhs_context* ctx;
+    uint64_t* pk;  // 2 x L0
+    uint64_t seed;
+    uint64_t ctr;
+};
+struct fhs_relin_key {
+    fhs_context* ctx;
+    uint64_t* key;
+};
+struct fhs_galois_keys {
+    fhs_context* ctx;
+    std::map<uint64_t, uint64_t*> keys;
+};
+
+static size_t key_words(const fhs_context* c) { return (size_t)c->dnum * 2 * c->K * c->N; }
+
+static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
+    void* v = nullptr;
+    hipError_t e = hipMallocAsync(&v, bytes ? bytes : 8, c->st);
+    if (e == hipSuccess) {
+        *p = (uint64_t*)v;
+        c->bytes_live += bytes;
+    }
+    return e;
+}
+static void dfree(fhs_context* c, void* p, size_t bytes) {
+    if (!p) return;
+    (void)hipFreeAsync(p, c->st);
+    c->bytes_live -= bytes;
+}
+
+static fhs_status new_ct(fhs_context* c, int ncomp, int ci, double scale, fhs_ciphertext** out) {
+    const int l = c->L0 + 1 - ci;
+    if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
+    auto* ct = new fhs_ciphertext{c, nullptr, ncomp, ci, l, scale};
+    hipError_t e = dalloc(c, &ct->d, 8ull * ncomp * l * c->N);
+    if (e != hipSuccess) {
+        delete ct;
+        return hip_fail(e, "ciphertext allocation");
+    }
+    *out = ct;
+    return FHS_OK;
+}
+static fhs_status new_pt(fhs_context* c, int ci, double scale, fhs_plaintext** out) {
+    const int l = c->L0 + 1 - ci;
+    if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
+    auto* pt = new fhs_plaintext{c, nullptr, ci, l, scale};
+    hipError_t e = dalloc(c, &pt->d, 8ull * l * c->N);
+    if (e != hipSuccess) {
+        delete pt;
+        return hip_fail(e, "plaintext allocation");
+    }
+    *out = pt;
+    return FHS_OK;
+}
+static size_t ct_bytes(const fhs_ciphertext* ct) { return 8ull * ct->ncomp * ct->l * ct->ctx->N; }
+static size_t pt_bytes(const fhs_plaintext* pt) { return 8ull * pt->l * pt->ctx->N; }
+
+// ---------------------------------------------------------------- deferred rotations
+static fhs_status flush(fhs_context* c) {
+    if (c->pending.empty()) return FHS_OK;
+    const int R = (int)c->pending.size(), l = c->pending_l;
+    std::vector<KsItem> items(R);
+    for (int r = 0; r < R; ++r) items[r] = c->pending[r].item;
+    const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, l);
+    uint64_t* ws = nullptr;
+    hipError_t e = dalloc(c, &ws, wsb);
+    if (e != hipSuccess) return hip_fail(e, "key-switch workspace");
+    hipEvent_t tev[2] = {nullptr, nullptr};
+    const bool timed = c->timer_kernel == 1;
+    if (timed) {
+        hipEventCreate(&tev[0]);
+        hipEventCreate(&tev[1]);
+    }
+    e = fhs::launch_keyswitch(c->T, items.data(), R, l, ws, wsb, c->items_dev, c->st, timed ? tev : nullptr);
+    dfree(c, ws, wsb);
+    if (timed) c->timer_pairs.push_back({tev[0], tev[1]});
+    c->pending.clear();
+    c->pending_refs.clear();
+    c->pending_l = -1;
+    // the items buffer is reused by the next launch: keep host/device ordered
+    if (e != hipSuccess) return hip_fail(e, "key-switch launch");
+    return FHS_OK;
+}
+
+struct Guard {
+    fhs_context* c;
+    std::lock_guard<std::recursive_mutex> lk;
+    explicit Guard(fhs_context* c_) : c(c_), lk(c_->mu) {}
+};
+#define ENTER(ctx)                                                           \
+    if (!(ctx)) return fail(FHS_ERR_INVALID, "null context");               \
+    Guard _g(ctx);                                                           \
+    do {                                                                     \
+        fhs_status _s = flush(ctx);                                          \
+        if (_s != FHS_OK) return _s;                                         \
+    } while (0)
+
+// ============================================================================ context
+extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int nprimes, int special,
+                                         const uint64_t* galois_elts, int n_elts, int device, fhs_context** out) {
+    if (!primes || !out) return fail(FHS_ERR_INVALID, "context_create: null argument");
+    if (N < 256 || N > 16384 || (N & (N - 1)))
+        return fail(FHS_ERR_INVALID, "context_create: poly_modulus_degree must be a power of two in [256, 16384]");
+    if (special < 1 || special >= nprimes) return fail(FHS_ERR_INVALID, "context_create: bad special modulus size");
+    const int L0 = nprimes - special;
+    if (L0 % special != 0)
+        return fail(FHS_ERR_INVALID,
+                    "context_create: data primes (L0) must be a multiple of special_modulus_size (README.md:59)");
+    if (special > 8) return fail(FHS_ERR_INVALID, "context_create: special_modulus_size > 8 unsupported");
+    for (int i = 0; i < nprimes; ++i) {
+        if (primes[i] >= (1ull << 61) || (primes[i] - 1) % (2 * N) != 0 || !h_is_prime(primes[i]))
+            return fail(FHS_ERR_INVALID, "context_create: every modulus must be a prime < 2^61, = 1 mod 2N");
+        for (int j = 0; j < i; ++j)
+            if (primes[j] == primes[i]) return fail(FHS_ERR_INVALID, "context_create: duplicate modulus");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(FHS_ERR_NODEVICE, "no HIP device: libfhespear_hip needs an MI355X (gfx950)");
+    if (device < 0 || device >= ndev) return fail(FHS_ERR_INVALID, "context_create: bad device index");
+    HIPCHK(hipSetDevice(device), "hipSetDevice");
+
+    auto c = std::make_unique<fhs_context>();
+    c->device = device;
+    c->N = N;
+    while ((1ull << c->logN) < N) c->logN++;
+    c->K = nprimes;
+    c->P = special;
+    c->L0 = L0;
+    c->dnum = (L0 + special - 1) / special;
+    c->q.assign(primes, primes + nprimes);
+    HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "hipStreamCreate");
+    {
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+            uint64_t thr = ~0ull;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        }
+    }
+    if (galois_elts && n_elts > 0) {
+        c->elts.assign(galois_elts, galois_elts + n_elts);
+    } else {   // default: +-2^k steps and conjugation (SEAL/Phantom create_galois_keys default)
+        std::set<uint64_t> s;
+        for (uint64_t k = 1; k < N / 2; k <<= 1) {
+            s.insert(fhs_galois_elt_from_step((int)k, N));
+            s.insert(fhs_galois_elt_from_step(-(int)k, N));
+        }
+        s.insert(2 * N - 1);
+        c->elts.assign(s.begin(), s.end());
+    }
+    for (uint64_t e : c->elts)
+        if ((e & 1) == 0 || e >= 2 * N) return fail(FHS_ERR_INVALID, "context_create: invalid galois element");
+
+    const int K = nprimes, P = special, dnum = c->dnum;
+    // ---- per-prime constants and twiddles
+    std::vector<PrimeK> pk(K);
+    std::vector<uint64_t> twf((size_t)K * N * 2), twi((size_t)K * N * 2);
+    for (int i = 0; i < K; ++i) {
+        const uint64_t q = primes[i];
+        const hu128 r = (~(hu128)0) / q;
+        const uint64_t psi = h_min_root(q, N), ipsi = h_inv(psi, q);
+        uint64_t pw = 1, ipw = 1;
+        for (uint64_t k = 0; k < N; ++k) {
+            const uint32_t rv = h_bitrev((uint32_t)k, c->logN);
+            twf[((size_t)i * N + rv) * 2] = pw;
+            twi[((size_t)i * N + rv) * 2] = ipw;
+            pw = h_mulmod(pw, psi, q);
+            ipw = h_mulmod(ipw, ipsi, q);
+        }
+        for (uint64_t k = 0; k < N; ++k) {
+            twf[((size_t)i * N + k) * 2 + 1] = h_shoup(twf[((size_t)i * N + k) * 2], q);
+            twi[((size_t)i * N + k) * 2 + 1] = h_shoup(twi[((size_t)i * N + k) * 2], q);
+        }
+        const uint64_t ninv = h_inv(N % q, q);
+        const uint64_t w1n = h_mulmod(twi[((size_t)i * N + 1) * 2], ninv, q);
+        pk[i] = PrimeK{q, (uint64_t)r, (uint64_t)(r >> 64), ninv, h_shoup(ninv, q), w1n, h_shoup(w1n, q), 0};
+    }
+    // ---- ModUp tables per level l: digit j covers [jP, min(jP+P, l))
+    std::vector<uint64_t> mu_intt((size_t)(L0 + 1) * L0 * 4, 0), mu_hat((size_t)(L0 + 1) * dnum * P * K, 0);
+    for (int l = 1; l <= L0; ++l) {
+        const int dn = (l + P - 1) / P;
+        for (int j = 0; j < dn; ++j) {
+            const int s0 = j * P, s1 = std::min(s0 + P, l), ns = s1 - s0;
+            for (int u = 0; u < ns; ++u) {
+                const int i = s0 + u;
+                const uint64_t q = primes[i];
+                uint64_t hat = 1;
+                for (int v = 0; v < ns; ++v)
+                    if (v != u) hat = h_mulmod(hat, primes[s0 + v] % q, q);
+                const uint64_t ih = h_inv(hat, q);
+                const uint64_t a = h_mulmod(pk[i].ninv, ih, q), b = h_mulmod(pk[i].w1ninv, ih, q);
+                uint64_t* d = &mu_intt[((size_t)l * L0 + i) * 4];
+                d[0] = a; d[1] = h_shoup(a, q); d[2] = b; d[3] = h_shoup(b, q);
+                for (int t = 0; t < K; ++t) {
+                    const uint64_t m = primes[t];
+                    uint64_t h = 1;
+                    for (int v = 0; v < ns; ++v)
+                        if (v != u) h = h_mulmod(h, primes[s0 + v] % m, m);
+                    mu_hat[(((size_t)l * dnum + j) * P + u) * K + t] = h;
+                }
+            }
+        }
+    }
+    // ---- ModDown tables
+    std::vector<uint64_t> md_intt((size_t)P * 4), md_hat((size_t)P * L0), md_pinv((size_t)3 * L0);
+    for (int k = 0; k < P; ++k) {
+        const int pi = L0 + k;
+        const uint64_t p = primes[pi];
+        uint64_t hat = 1;
+        for (int v = 0; v < P; ++v)
+            if (v != k) hat = h_mulmod(hat, primes[L0 + v] % p, p);
+        const uint64_t ih = h_inv(hat, p);
+        const uint64_t a = h_mulmod(pk[pi].ninv, ih, p), b = h_mulmod(pk[pi].w1ninv, ih, p);
+        md_intt[k * 4 + 0] = a; md_intt[k * 4 + 1] = h_shoup(a, p);
+        md_intt[k * 4 + 2] = b; md_intt[k * 4 + 3] = h_shoup(b, p);
+        for (int i = 0; i < L0; ++i) {
+            const uint64_t q = primes[i];
+            uint64_t h = 1;
+            for (int v = 0; v < P; ++v)
+                if (v != k) h = h_mulmod(h, primes[L0 + v] % q, q);
+            md_hat[(size_t)k * L0 + i] = h;
+        }
+    }
+    for (int i = 0; i < L0; ++i) {
+        const uint64_t q = primes[i];
+        uint64_t pm = 1;
+        for (int k = 0; k < P; ++k) pm = h_mulmod(pm, primes[L0 + k] % q, q);
+        const uint64_t pinv = h_inv(pm, q);
+        md_pinv[2 * i] = pinv;
+        md_pinv[2 * i + 1] = h_shoup(pinv, q);
+        md_pinv[2 * L0 + i] = pm;
+    }
+    // ---- rescale tables: level l (limbs) drops q_{l-1}
+    std::vector<uint64_t> rs((size_t)(L0 + 1) * L0 * 4, 0);
+    for (int l = 2; l <= L0; ++l) {
+        const uint64_t ql = primes[l - 1], half = ql >> 1;
+        for (int i = 0; i < l - 1; ++i) {
+            const uint64_t q = primes[i];
+            const uint64_t inv = h_inv(ql % q, q);
+            uint64_t* d = &rs[((size_t)l * L0 + i) * 4];
+            d[0] = inv; d[1] = h_shoup(inv, q); d[2] = half % q; d[3] = half;
+        }
+    }
+    // ---- 2^e mod q for exact double reduction
+    std::vector<uint64_t> pow2((size_t)K * 1088);
+    for (int i = 0; i < K; ++i) {
+        uint64_t v = 1 % primes[i];
+        for (int e = 0; e < 1088; ++e) {
+            pow2[(size_t)i * 1088 + e] = v;
+            v = h_mulmod(v, 2, primes[i]);
+        }
+    }
+    auto up = [&](const void* src, size_t bytes, const void** dst) -> hipError_t {
+        void* d = nullptr;
+        hipError_t e = hipMalloc(&d, bytes);
+        if (e != hipSuccess) return e;
+        c->tables.push_back(d);
+        e = hipMemcpy(d, src, bytes, hipMemcpyHostToDevice);
+        *dst = d;
+        return e;
+    };
+    DevTables& T = c->T;
+    T.N = (int)N; T.logN = c->logN; T.L0 = L0; T.P = P; T.K = K; T.dnum = dnum;
+    HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");
+    HIPCHK(up(twf.data(), 8 * twf.size(), (const void**)&T.tw_fwd), "tables");
+    HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");
+    HIPCHK(up(mu_intt.data(), 8 * mu_intt.size(), (const void**)&T.modup_intt), "tables");
+    HIPCHK(up(mu_hat.data(), 8 * mu_hat.size(), (const void**)&T.modup_hat), "tables");
+    HIPCHK(up(md_intt.data(), 8 * md_intt.size(), (const void**)&T.md_intt), "tables");
+    HIPCHK(up(md_hat.data(), 8 * md_hat.size(), (const void**)&T.md_hat), "tables");
+    HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
+    HIPCHK(up(rs.data(), 8 * rs.size(), (const void**)&T.rescale), "tables");
+    HIPCHK(up(pow2.data(), 8 * pow2.size(), (const void**)&T.pow2), "tables");
+    HIPCHK(hipMalloc(&c->items_dev, sizeof(KsItem) * fhs_context::kMaxItems), "items buffer");
+    c->tables.push_back(c->items_dev);
+    HIPCHK(hipMalloc(&c->ptrs_dev, sizeof(void*) * 2 * fhs_context::kMaxPtrs), "pointer buffer");
+    c->tables.push_back(c->ptrs_dev);
+    // encoder tables
+    c->fft_w.resize(N);
+    for (uint64_t k = 0; k < N; ++k) c->fft_w[k] = std::polar(1.0, 2.0 * M_PI * (double)k / (double)N);
+    c->slot_index.resize(N / 2);
+    uint64_t e5 = 1;
+    for (uint64_t j = 0; j < N / 2; ++j) {
+        c->slot_index[j] = (e5 - 1) / 2;
+        e5 = (e5 * 5) & (2 * N - 1);
+    }
+    *out = c.release();
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
+    if (!c) return FHS_OK;
+    {
+        Guard g(c);
+        flush(c);
+        hipStreamSynchronize(c->st);
+        for (void* p : c->tables) hipFree(p);
+        for (auto& pr : c->timer_pairs) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+        hipStreamDestroy(c->st);
+    }
+    delete c;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_context_info(const fhs_context* c, uint64_t* N, int* L0, int* P, int* n_elts) {
+    if (!c) return fail(FHS_ERR_INVALID, "null context");
+    if (N) *N = c->N;
+    if (L0) *L0 = c->L0;
+    if (P) *P = c->P;
+    if (n_elts) *n_elts = (int)c->elts.size();
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_context_galois_elts(const fhs_context* c, uint64_t* out) {
+    if (!c || !out) return fail(FHS_ERR_INVALID, "null argument");
+    std::copy(c->elts.begin(), c->elts.end(), out);
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_synchronize(fhs_context* c) {
+    ENTER(c);
+    HIPCHK(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_memory_in_use(fhs_context* c, uint64_t* bytes) {
+    if (!c || !bytes) return fail(FHS_ERR_INVALID, "null argument");
+    *bytes = c->bytes_live.load();
+    return FHS_OK;
+}
+
+// ============================================================================ sampling helpers
+static uint64_t sm64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+static uint64_t stream_key(uint64_t seed, uint64_t stream) { return sm64(seed ^ sm64(stream)); }
+static uint64_t stream_id(uint64_t kind, uint64_t a, uint64_t b) { return (kind << 56) | (a << 16) | b; }
+enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6 };
+
+// sample a small polynomial (ternary/CBD) over `limbs` primes and NTT it
+static hipError_t sample_small_ntt(fhs_context* c, int mode, uint64_t key, uint64_t* out, int limbs) {
+    hipError_t e = fhs::launch_sample(c->T, mode, key, out, limbs, 0, c->st);
+    if (e != hipSuccess) return e;
+    return fhs::launch_ntt_fwd(c->T, out, limbs, limbs, 1, 0, c->st);
+}
+
+// ============================================================================ keys
+extern "C" fhs_status fhs_secret_key_create(fhs_context* c, uint64_t seed, fhs_secret_key** out) {
+    ENTER(c);
+    if (!out) return fail(FHS_ERR_INVALID, "null out");
+    auto* sk = new fhs_secret_key{c, nullptr, seed, 0};
+    hipError_t e = dalloc(c, &sk->s, 8ull * c->K * c->N);
+    if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key"); }
+    e = sample_small_ntt(c, fhs::SAMPLE_TERNARY, stream_key(seed, stream_id(ST_SECRET, 0, 0)), sk->s, c->K);
+    if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key sampling"); }
+    *out = sk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_secret_key_destroy(fhs_secret_key* sk) {
+    if (!sk) return FHS_OK;
+    { Guard g(sk->ctx); flush(sk->ctx); dfree(sk->ctx, sk->s, 8ull * sk->ctx->K * sk->ctx->N); }
+    delete sk;
+    return FHS_OK;
+}
+
+static fhs_status gen_switch_key(fhs_context* c, uint64_t seed, uint64_t base, const uint64_t* s, const uint64_t* snew,
+                                 uint64_t** key_out) {
+    uint64_t* key = nullptr;
+    hipError_t e = dalloc(c, &key, 8 * key_words(c));
+    if (e != hipSuccess) return hip_fail(e, "switching key");
+    uint64_t* ebuf = nullptr;
+    e = dalloc(c, &ebuf, 8ull * c->K * c->N);
+    if (e != hipSuccess) { dfree(c, key, 8 * key_words(c)); return hip_fail(e, "switching key"); }
+    const size_t S = (size_t)c->K * c->N;
+    for (int j = 0; j < c->dnum && e == hipSuccess; ++j) {
+        const uint64_t ka = stream_key(seed, base | (uint64_t)(2 * j));
+        const uint64_t ke = stream_key(seed, base | (uint64_t)(2 * j + 1));
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, ka, key + ((size_t)j * 2 + 1) * S, c->K, 0, c->st);
+        if (e == hipSuccess) e = sample_small_ntt(c, fhs::SAMPLE_CBD, ke, ebuf, c->K);
+        if (e == hipSuccess) e = fhs::launch_switch_key_assemble(c->T, key, ebuf, s, snew, j, c->st);
+    }
+    dfree(c, ebuf, 8ull * c->K * c->N);
+    if (e != hipSuccess) { dfree(c, key, 8 * key_words(c)); return hip_fail(e, "switching key generation"); }
+    *key_out = key;
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_gen_relin_key(fhs_context* c, fhs_secret_key* sk, fhs_relin_key** out) {
+    ENTER(c);
+    if (!sk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    uint64_t* s2 = nullptr;
+    HIPCHK(dalloc(c, &s2, 8ull * c->K * c->N), "relin key");
+    HIPCHK(fhs::launch_key_prod(c->T, sk->s, sk->s, s2, c->K, c->st), "relin key");
+    auto* rk = new fhs_relin_key{c, nullptr};
+    fhs_status s = gen_switch_key(c, sk->seed, stream_id(ST_RELIN, 0, 0), sk->s, s2, &rk->key);
+    dfree(c, s2, 8ull * c->K * c->N);
+    if (s != FHS_OK) { delete rk; return s; }
+    *out = rk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_relin_key_destroy(fhs_relin_key* rk) {
+    if (!rk) return FHS_OK;
+    { Guard g(rk->ctx); flush(rk->ctx); dfree(rk->ctx, rk->key, 8 * key_words(rk->ctx)); }
+    delete rk;
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_create_galois_keys(fhs_context* c, fhs_secret_key* sk, const uint64_t* elts, int n,
+                                             fhs_galois_keys** out) {
+    ENTER(c);
+    if (!sk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    std::vector<uint64_t> list = (elts && n > 0) ? std::vector<uint64_t>(elts, elts + n) : c->elts;
+    auto* gk = new fhs_galois_keys{c, {}};
+    uint64_t* sn = nullptr;
+    hipError_t e = dalloc(c, &sn, 8ull * c->K * c->N);
+    if (e != hipSuccess) { delete gk; return hip_fail(e, "galois keys"); }
+    for (uint64_t elt : list) {
+        if (gk->keys.count(elt)) continue;
+        if ((elt & 1) == 0 || elt >= 2 * c->N) { e = hipErrorInvalidValue; break; }
+        e = fhs::launch_galois_perm(c->T, sk->s, sn, c->K, elt, c->st);
+        if (e != hipSuccess) break;
+        uint64_t* key = nullptr;
+        fhs_status s = gen_switch_key(c, sk->seed, stream_id(ST_GALOIS, elt, 0), sk->s, sn, &key);
+        if (s != FHS_OK) {
+            dfree(c, sn, 8ull * c->K * c->N);
+            for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
+            delete gk;
+            return s;
+        }
+        gk->keys[elt] = key;
+    }
+    dfree(c, sn, 8ull * c->K * c->N);
+    if (e != hipSuccess) {
+        for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
+        delete gk;
+        return hip_fail(e, "galois key generation");
+    }
+    *out = gk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_galois_keys_destroy(fhs_galois_keys* gk) {
+    if (!gk) return FHS_OK;
+    {
+        Guard g(gk->ctx);
+        flush(gk->ctx);
+        for (auto& kv : gk->keys) dfree(gk->ctx, kv.second, 8 * key_words(gk->ctx));
+    }
+    delete gk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_galois_keys_has(const fhs_galois_keys* gk, uint64_t elt, int* has) {
+    if (!gk || !has) return fail(FHS_ERR_INVALID, "null argument");
+    *has = gk->keys.count(elt) ? 1 : 0;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_galois_keys_bytes(const fhs_galois_keys* gk, uint64_t* bytes) {
+    if (!gk || !bytes) return fail(FHS_ERR_INVALID, "null argument");
+    *bytes = (uint64_t)gk->keys.size() * 8 * key_words(gk->ctx);
+    return FHS_OK;
+}
+
+static fhs_status export_dev(fhs_context* c, const void* d, size_t bytes, void* host) {
+    HIPCHK(hipMemcpyAsync(host, d, bytes, hipMemcpyDeviceToHost, c->st), "export");
+    HIPCHK(hipStreamSynchronize(c->st), "export sync");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_galois_key_export(fhs_context* c, const fhs_galois_keys* gk, uint64_t elt, uint64_t* host) {
+    ENTER(c);
+    if (!gk || !host) return fail(FHS_ERR_INVALID, "null argument");
+    auto it = gk->keys.find(elt);
+    if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "galois key not present");
+    return export_dev(c, it->second, 8 * key_words(c), host);
+}
+extern "C" fhs_status fhs_relin_key_export(fhs_context* c, const fhs_relin_key* rk, uint64_t* host) {
+    ENTER(c);
+    if (!rk || !host) return fail(FHS_ERR_INVALID, "null argument");
+    return export_dev(c, rk->key, 8 * key_words(c), host);
+}
+extern "C" fhs_status fhs_secret_key_export(fhs_context* c, const fhs_secret_key* sk, uint64_t* host) {
+    ENTER(c);
+    if (!sk || !host) return fail(FHS_ERR_INVALID, "null argument");
+    return export_dev(c, sk->s, 8ull * c->K * c->N, host);
+}
+
+extern "C" fhs_status fhs_gen_public_key(fhs_context* c, fhs_secret_key* sk, fhs_public_key** out) {
+    ENTER(c);
+    if (!sk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    auto* pk = new fhs_public_key{c, nullptr, sk->seed, 1ull << 20};
+    const size_t S = (size_t)c->L0 * c->N;
+    hipError_t e = dalloc(c, &pk->pk, 16 * S);
+    if (e != hipSuccess) { delete pk; return hip_fail(e, "public key"); }
+    uint64_t* eb = nullptr;
+    e = dalloc(c, &eb, 8 * S);
+    if (e == hipSuccess)
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(sk->seed, stream_id(ST_PUBKEY, 0, 0)), pk->pk + S,
+                               c->L0, 0, c->st);
+    if (e == hipSuccess)
+        e = sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(sk->seed, stream_id(ST_PUBKEY, 0, 1)), eb, c->L0);
+    if (e == hipSuccess)
+        e = fhs::launch_encrypt_combine(c->T, 0, pk->pk, pk->pk + S, sk->s, nullptr, nullptr, eb, nullptr, nullptr,
+                                        c->L0, c->st);
+    dfree(c, eb, 8 * S);
+    if (e != hipSuccess) { dfree(c, pk->pk, 16 * S); delete pk; return hip_fail(e, "public key generation"); }
+    *out = pk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_public_key_destroy(fhs_public_key* pk) {
+    if (!pk) return FHS_OK;
+    { Guard g(pk->ctx); flush(pk->ctx); dfree(pk->ctx, pk->pk, 16ull * pk->ctx->L0 * pk->ctx->N); }
+    delete pk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_public_key_export(fhs_context* c, const fhs_public_key* pk, uint64_t* host) {
+    ENTER(c);
+    if (!pk || !host) return fail(FHS_ERR_INVALID, "null argument");
+    return export_dev(c, pk->pk, 16ull * c->L0 * c->N, host);
+}
+
+// ============================================================================ object API
+static bool pending_uses(fhs_context* c, const void* p) { return c->pending_refs.count(p) != 0; }
+
+extern "C" fhs_status fhs_ciphertext_destroy(fhs_ciphertext* ct) {
+    if (!ct) return FHS_OK;
+    fhs_context* c = ct->ctx;
+    {
+        Guard g(c);
+        if (pending_uses(c, ct)) flush(c);
+        dfree(c, ct->d, ct_bytes(ct));
+    }
+    delete ct;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_plaintext_destroy(fhs_plaintext* pt) {
+    if (!pt) return FHS_OK;
+    { Guard g(pt->ctx); dfree(pt->ctx, pt->d, pt_bytes(pt)); }
+    delete pt;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_ciphertext_info(const fhs_ciphertext* ct, int* ncomp, int* ci, int* l, double* scale) {
+    if (!ct) return fail(FHS_ERR_INVALID, "null ciphertext");
+    if (ncomp) *ncomp = ct->ncomp;
+    if (ci) *ci = ct->ci;
+    if (l) *l = ct->l;
+    if (scale) *scale = ct->scale;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_ciphertext_set_scale(fhs_ciphertext* ct, double scale) {
+    if (!ct) return fail(FHS_ERR_INVALID, "null ciphertext");
+    ct->scale = scale;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_plaintext_info(const fhs_plaintext* pt, int* ci, int* l, double* scale) {
+    if (!pt) return fail(FHS_ERR_INVALID, "null plaintext");
+    if (ci) *ci = pt->ci;
+    if (l) *l = pt->l;
+    if (scale) *scale = pt->scale;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_ciphertext_export(fhs_context* c, const fhs_ciphertext* ct, uint64_t* host) {
+    ENTER(c);
+    if (!ct || !host) return fail(FHS_ERR_INVALID, "null argument");
+    return export_dev(c, ct->d, ct_bytes(ct), host);
+}
+extern "C" fhs_status fhs_plaintext_export(fhs_context* c, const fhs_plaintext* pt, uint64_t* host) {
+    ENTER(c);
+    if (!pt || !host) return fail(FHS_ERR_INVALID, "null argument");
+    return export_dev(c, pt->d, pt_bytes(pt), host);
+}
+extern "C" fhs_status fhs_ciphertext_import(fhs_context* c, const uint64_t* host, int ncomp, int ci, double scale,
+                                            fhs_ciphertext** out) {
+    ENTER(c);
+    if (!host || !out || ncomp < 2 || ncomp > 3) return fail(FHS_ERR_INVALID, "ciphertext_import: bad args");
+    fhs_ciphertext* ct;
+    fhs_status s = new_ct(c, ncomp, ci, scale, &ct);
+    if (s != FHS_OK) return s;
+    HIPCHK(hipMemcpyAsync(ct->d, host, ct_bytes(ct), hipMemcpyHostToDevice, c->st), "ciphertext_import");
+    HIPCHK(hipStreamSynchronize(c->st), "ciphertext_import");
+    *out = ct;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_plaintext_import(fhs_context* c, const uint64_t* host, int ci, double scale,
+                                           fhs_plaintext** out) {
+    ENTER(c);
+    if (!host || !out) return fail(FHS_ERR_INVALID, "plaintext_import: bad args");
+    fhs_plaintext* pt;
+    fhs_status s = new_pt(c, ci, scale, &pt);
+    if (s != FHS_OK) return s;
+    HIPCHK(hipMemcpyAsync(pt->d, host, pt_bytes(pt), hipMemcpyHostToDevice, c->st), "plaintext_import");
+    HIPCHK(hipStreamSynchronize(c->st), "plaintext_import");
+    *out = pt;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_ciphertext_device_ptr(const fhs_ciphertext* ct, void** dptr, uint64_t* bytes) {
+    if (!ct || !dptr) return fail(FHS_ERR_INVALID, "null argument");
+    fhs_context* c = ct->ctx;
+    Guard g(c);
+    fhs_status s = flush(c);
+    if (s != FHS_OK) return s;
+    *dptr = ct->d;
+    if (bytes) *bytes = ct_bytes(ct);
+    return FHS_OK;
+}
+
+// ============================================================================ encoder
+// slots z_j sit at the evaluation point zeta^(5^j); encode solves m(zeta^(5^j)) = scale z_j with
+// a length-N complex DFT over the odd exponents (pb:141-149).
+static void fft_inplace(std::vector<std::complex<double>>& a, const std::vector<std::complex<double>>& w, int logN,
+                        bool inverse) {
+    const size_t n = a.size();
+    for (size_t i = 0; i < n; ++i) {
+        const size_t r = h_bitrev((uint32_t)i, logN);
+        if (r > i) std::swap(a[i], a[r]);
+    }
+    for (size_t len = 2; len <= n; len <<= 1) {
+        const size_t step = n / len;
+        for (size_t i = 0; i < n; i += len) {
+            for (size_t k = 0; k < len / 2; ++k) {
+                std::complex<double> wk = w[k * step];
+                if (inverse) wk = std::conj(wk);
+                const std::complex<double> u = a[i + k], v = a[i + k + len / 2] * wk;
+                a[i + k] = u + v;
+                a[i + k + len / 2] = u - v;
+            }
+        }
+    }
+}
+
+// values: count vectors of n complex (re,im) (or real when is_real); produces rounded coefficients
+static void encode_coeffs(const fhs_context* c, const double* vals, size_t n, bool is_real, double scale,
+                          double* coef) {
+    const size_t N = c->N, M = 2 * N, slots = N / 2;
+    std::vector<std::complex<double>> v(N, 0.0);
+    for (size_t j = 0; j < slots; ++j) {
+        std::complex<double> z(0.0, 0.0);
+        if (j < n) z = is_real ? std::complex<double>(vals[j], 0.0) : std::complex<double>(vals[2 * j], vals[2 * j + 1]);
+        const size_t t = c->slot_index[j];
+        v[t] = z;
+        v[(M - (2 * t + 1) - 1) / 2] = std::conj(z);
+    }
+    fft_inplace(v, c->fft_w, c->logN, true);    // sum_t v_t w^{-tk}
+    const double invN = 1.0 / (double)N;
+    for (size_t k = 0; k < N; ++k) {
+        const std::complex<double> zk = std::polar(1.0, -M_PI * (double)k / (double)N);
+        const double re = (v[k] * zk).real() * invN;
+        coef[k] = std::round(re * scale);
+    }
+}
+
+static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, size_t n, bool is_real, double scale,
+                              int ci, fhs_plaintext** outs) {
+    if (n > c->N / 2) return fail(FHS_ERR_INVALID, "encode: more values than slots");
+    if (!(scale > 0) || !std::isfinite(scale)) return fail(FHS_ERR_INVALID, "encode: bad scale");
+    const int l = c->L0 + 1 - ci;
+    if (ci < 1 || l < 1) return fail(FHS_ERR_LEVEL, "encode: chain index out of range");
+    const size_t N = c->N, stride = is_real ? n : 2 * n;
+    const size_t chunk = std::min<size_t>(count, 256);
+    std::vector<double> coef(chunk * N);
+    double* dcoef = nullptr;
+    HIPCHK(hipMalloc(&dcoef, 8 * chunk * N), "encode staging");
+    for (size_t base = 0; base < count; base += chunk) {
+        const size_t cnt = std::min(chunk, count - base);
+        const unsigned nth = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 32));
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nth; ++t)
+            th.emplace_back([&, t]() {
+                for (size_t v = t; v < cnt; v += nth)
+                    encode_coeffs(c, vals + (base + v) * stride, n, is_real, scale, coef.data() + v * N);
+            });
+        for (auto& x : th) x.join();
+        hipError_t e = hipMemcpyAsync(dcoef, coef.data(), 8 * cnt * N, hipMemcpyHostToDevice, c->st);
+        for (size_t v = 0; v < cnt && e == hipSuccess; ++v) {
+            fhs_plaintext* pt = nullptr;
+            fhs_status s = new_pt(c, ci, scale, &pt);
+            if (s != FHS_OK) { hipFree(dcoef); return s; }
+            outs[base + v] = pt;
+            e = fhs::launch_encode_reduce(c->T, dcoef + v * N, 1, pt->d, l, c->st);
+            if (e == hipSuccess) e = fhs::launch_ntt_fwd(c->T, pt->d, l, l, 1, 0, c->st);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // staging buffers are reused
+        if (e != hipSuccess) { hipFree(dcoef); return hip_fail(e, "encode"); }
+    }
+    hipFree(dcoef);
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_encode(fhs_context* c, const double* re_im, size_t n, double scale, int ci,
+                                 fhs_plaintext** out) {
+    ENTER(c);
+    if ((!re_im && n) || !out) return fail(FHS_ERR_INVALID, "encode: null argument");
+    return encode_many(c, re_im, 1, n, false, scale, ci, out);
+}
+extern "C" fhs_status fhs_encode_real(fhs_context* c, const double* v, size_t n, double scale, int ci,
+                                      fhs_plaintext** out) {
+    ENTER(c);
+    if ((!v && n) || !out) return fail(FHS_ERR_INVALID, "encode: null argument");
+    return encode_many(c, v, 1, n, true, scale, ci, out);
+}
+extern "C" fhs_status fhs_encode_batch(fhs_context* c, const double* re_im, size_t count, size_t n, double scale,
+                                       int ci, fhs_plaintext** out) {
+    ENTER(c);
+    if (!re_im || !out) return fail(FHS_ERR_INVALID, "encode_batch: null argument");
+    return encode_many(c, re_im, count, n, false, scale, ci, out);
+}
+extern "C" fhs_status fhs_encode_real_batch(fhs_context* c, const double* v, size_t count, size_t n, double scale,
+                                            int ci, fhs_plaintext** out) {
+    ENTER(c);
+    if (!v || !out) return fail(FHS_ERR_INVALID, "encode_batch: null argument");
+    return encode_many(c, v, count, n, true, scale, ci, out);
+}
+
+// CRT-compose l residues of each coefficient to a centred double (multi-precision, host)
+static void crt_compose(const fhs_context* c, const std::vector<uint64_t>& limbs, int l, std::vector<double>& out) {
+    const size_t N = c->N;
+    const int W = l + 1;
+    std::vector<uint64_t> Q(W, 0);
+    Q[0] = 1;
+    for (int i = 0; i < l; ++i) {
+        hu128 carry = 0;
+        for (int w = 0; w < W; ++w) {
+            const hu128 t = (hu128)Q[w] * c->q[i] + carry;
+            Q[w] = (uint64_t)t;
+            carry = t >> 64;
+        }
+    }
+    std::vector<uint64_t> hat((size_t)l * W, 0), ihat(l);
+    for (int i = 0; i < l; ++i) {
+        uint64_t* h = &hat[(size_t)i * W];
+        h[0] = 1;
+        uint64_t hm = 1;
+        for (int k = 0; k < l; ++k) {
+            if (k == i) continue;
+            hu128 carry = 0;
+            for (int w = 0; w < W; ++w) {
+                const hu128 t = (hu128)h[w] * c->q[k] + carry;
+                h[w] = (uint64_t)t;
+                carry = t >> 64;
+            }
+            hm = h_mulmod(hm, c->q[k] % c->q[i], c->q[i]);
+        }
+        ihat[i] = h_inv(hm, c->q[i]);
+    }
+    std::vector<uint64_t> halfQ(W);
+    for (int w = 0; w < W; ++w) halfQ[w] = (Q[w] >> 1) | (w + 1 < W ? Q[w + 1] << 63 : 0);
+    out.assign(N, 0.0);
+    const unsigned nth = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 32));
+    std::vector<std::thread> th;
+    for (unsigned tix = 0; tix < nth; ++tix)
+        th.emplace_back([&, tix]() {
+            std::vector<uint64_t> x(W + 1);
+            for (size_t n = tix; n < N; n += nth) {
+                std::fill(x.begin(), x.end(), 0);
+                for (int i = 0; i < l; ++i) {
+                    const uint64_t y = h_mulmod(limbs[(size_t)i * N + n], ihat[i], c->q[i]);
+                    hu128 carry = 0;
+                    const uint64_t* h = &hat[(size_t)i * W];
+                    for (int w = 0; w < W; ++w) {
+                        const hu128 t = (hu128)h[w] * y + x[w] + carry;
+                        x[w] = (uint64_t)t;
+                        carry = t >> 64;
+                    }
+                    x[W] += (uint64_t)carry;
+                    for (;;) {   // x < 2Q: at most one subtraction
+                        bool ge = x[W] != 0;
+                        if (!ge) {
+                            ge = true;
+                            for (int w = W - 1; w >= 0; --w)
+                                if (x[w] != Q[w]) { ge = x[w] > Q[w]; break; }
+                        }
+                        if (!ge) break;
+                        uint64_t br = 0;
+                        for (int w = 0; w < W; ++w) {
+                            const uint64_t qa = Q[w] + br;
+                            const uint64_t nb = (qa < br) || (x[w] < qa);
+                            x[w] -= qa;
+                            br = nb;
+                        }
+                        x[W] -= br;
+                    }
+                }
+                bool neg = false;
+                for (int w = W - 1; w >= 0; --w)
+                    if (x[w] != halfQ[w]) { neg = x[w] > halfQ[w]; break; }
+                if (neg) {
+                    uint64_t br = 0;
+                    for (int w = 0; w < W; ++w) {
+                        const uint64_t xa = x[w] + br;
+                        const uint64_t nb = (xa < br) || (Q[w] < xa);
+                        x[w] = Q[w] - xa;
+                        br = nb;
+                    }
+                }
+                double v = 0;
+                for (int w = W - 1; w >= 0; --w) v = v * 18446744073709551616.0 + (double)x[w];
+                out[n] = neg ? -v : v;
+            }
+        });
+    for (auto& t : th) t.join();
+}
+
+extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double* re_im) {
+    ENTER(c);
+    if (!pt || !re_im) return fail(FHS_ERR_INVALID, "decode: null argument");
+    const size_t N = c->N;
+    const int l = pt->l;
+    uint64_t* tmp = nullptr;
+    HIPCHK(dalloc(c, &tmp, pt_bytes(pt)), "decode");
+    HIPCHK(hipMemcpyAsync(tmp, pt->d, pt_bytes(pt), hipMemcpyDeviceToDevice, c->st), "decode");
+    HIPCHK(fhs::launch_ntt_inv(c->T, tmp, l, l, 1, 0, c->st), "decode");
+    std::vector<uint64_t> host((size_t)l * N);
+    HIPCHK(hipMemcpyAsync(host.data(), tmp, pt_bytes(pt), hipMemcpyDeviceToHost, c->st), "decode");
+    HIPCHK(hipStreamSynchronize(c->st), "decode");
+    dfree(c, tmp, pt_bytes(pt));
+    std::vector<double> m;
+    crt_compose(c, host, l, m);
+    std::vector<std::complex<double>> v(N);
+    for (size_t k = 0; k < N; ++k) v[k] = std::polar(m[k] / pt->scale, M_PI * (double)k / (double)N);
+    fft_inplace(v, c->fft_w, c->logN, false);
+    for (size_t j = 0; j < N / 2; ++j) {
+        const std::complex<double> z = v[c->slot_index[j]];
+        re_im[2 * j] = z.real();
+        re_im[2 * j + 1] = z.imag();
+    }
+    return FHS_OK;
+}
+
+// ============================================================================ encryption
+extern "C" fhs_status fhs_encrypt_symmetric(fhs_context* c, fhs_secret_key* sk, const fhs_plaintext* pt,
+                                            fhs_ciphertext** out) {
+    ENTER(c);
+    if (!sk || !pt || !out) return fail(FHS_ERR_INVALID, "encrypt: null argument");
+    const uint64_t ctr = sk->ctr++;
+    fhs_ciphertext* ct;
+    fhs_status s = new_ct(c, 2, pt->ci, pt->scale, &ct);
+    if (s != FHS_OK) return s;
+    const int l = pt->l;
+    const size_t S = (size_t)l * c->N;
+    uint64_t* eb = nullptr;
+    HIPCHK(dalloc(c, &eb, 8 * S), "encrypt");
+    HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(sk->seed, stream_id(ST_ENC_SYM, ctr, 0)), ct->d + S,
+                              l, 0, c->st), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(sk->seed, stream_id(ST_ENC_SYM, ctr, 1)), eb, l), "encrypt");
+    HIPCHK(fhs::launch_encrypt_combine(c->T, 0, ct->d, ct->d + S, sk->s, nullptr, nullptr, eb, nullptr, pt->d, l, c->st),
+           "encrypt");
+    dfree(c, eb, 8 * S);
+    *out = ct;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_encrypt_asymmetric(fhs_context* c, fhs_public_key* pk, const fhs_plaintext* pt,
+                                             fhs_ciphertext** out) {
+    ENTER(c);
+    if (!pk || !pt || !out) return fail(FHS_ERR_INVALID, "encrypt: null argument");
+    const uint64_t ctr = pk->ctr++;
+    fhs_ciphertext* ct;
+    fhs_status s = new_ct(c, 2, pt->ci, pt->scale, &ct);
+    if (s != FHS_OK) return s;
+    const int l = pt->l;
+    const size_t S = (size_t)l * c->N, SL = (size_t)c->L0 * c->N;
+    uint64_t* tmp = nullptr;
+    HIPCHK(dalloc(c, &tmp, 24 * S), "encrypt");
+    uint64_t *u = tmp, *e0 = tmp + S, *e1 = tmp + 2 * S;
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_TERNARY, stream_key(pk->seed, stream_id(ST_ENC_ASYM, ctr, 0)), u, l), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(pk->seed, stream_id(ST_ENC_ASYM, ctr, 1)), e0, l), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(pk->seed, stream_id(ST_ENC_ASYM, ctr, 2)), e1, l), "encrypt");
+    HIPCHK(fhs::launch_encrypt_combine(c->T, 1, ct->d, ct->d + S, pk->pk, pk->pk + SL, u, e0, e1, pt->d, l, c->st),
+           "encrypt");
+    dfree(c, tmp, 24 * S);
+    *out = ct;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_decrypt(fhs_context* c, fhs_secret_key* sk, const fhs_ciphertext* ct, fhs_plaintext** out) {
+    ENTER(c);
+    if (!sk || !ct || !out) return fail(FHS_ERR_INVALID, "decrypt: null argument");
+    fhs_plaintext* pt;
+    fhs_status s = new_pt(c, ct->ci, ct->scale, &pt);
+    if (s != FHS_OK) return s;
+    HIPCHK(fhs::launch_decrypt(c->T, ct->d, ct->ncomp, sk->s, pt->d, ct->l, c->st), "decrypt");
+    *out = pt;
+    return FHS_OK;
+}
+
+// ============================================================================ evaluator
+static fhs_status same_level(const fhs_ciphertext* a, const fhs_ciphertext* b) {
+    if (a->ci != b->ci) return fail(FHS_ERR_LEVEL, "operands are at different chain indices");
+    return FHS_OK;
+}
+static bool scales_close(double a, double b) { return std::fabs(a - b) <= 1e-9 * std::max(std::fabs(a), std::fabs(b)); }
+
+static fhs_status binop(fhs_context* c, int op, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out) {
+    if (!a || !b || !out) return fail(FHS_ERR_INVALID, "null argument");
+    fhs_status s = same_level(a, b);
+    if (s != FHS_OK) return s;
+    if (a->ncomp != b->ncomp) return fail(FHS_ERR_INVALID, "ciphertext sizes differ");
+    if (!scales_close(a->scale, b->scale)) return fail(FHS_ERR_SCALE, "scale mismatch");
+    fhs_ciphertext* r;
+    s = new_ct(c, a->ncomp, a->ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    const size_t cs = (size_t)a->l * c->N;
+    HIPCHK(fhs::launch_eltwise(c->T, op, a->d, b->d, r->d, a->ncomp, a->l, cs, cs, c->st), "eltwise");
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_add(fhs_context* c, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out) {
+    ENTER(c);
+    return binop(c, fhs::OP_ADD, a, b, out);
+}
+extern "C" fhs_status fhs_sub(fhs_context* c, const fhs_ciphertext* a, const fhs_ciphertext* b, int negate,
+                              fhs_ciphertext** out) {
+    ENTER(c);
+    return binop(c, negate ? fhs::OP_SUBNEG : fhs::OP_SUB, a, b, out);
+}
+extern "C" fhs_status fhs_negate(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, a->ncomp, a->ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    const size_t cs = (size_t)a->l * c->N;
+    HIPCHK(fhs::launch_eltwise(c->T, fhs::OP_NEG, a->d, nullptr, r->d, a->ncomp, a->l, cs, 0, c->st), "negate");
+    *out = r;
+    return FHS_OK;
+}
+static fhs_status plainop(fhs_context* c, int op, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out) {
+    if (!a || !p || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (a->ci != p->ci) return fail(FHS_ERR_LEVEL, "ciphertext and plaintext are at different chain indices");
+    const double sc = op == fhs::OP_MULP ? a->scale * p->scale : a->scale;
+    if (op != fhs::OP_MULP && !scales_close(a->scale, p->scale)) return fail(FHS_ERR_SCALE, "scale mismatch");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, a->ncomp, a->ci, sc, &r);
+    if (s != FHS_OK) return s;
+    const size_t cs = (size_t)a->l * c->N;
+    HIPCHK(fhs::launch_eltwise(c->T, op, a->d, p->d, r->d, a->ncomp, a->l, cs, 0, c->st), "plain op");
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_add_plain(fhs_context* c, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out) {
+    ENTER(c);
+    return plainop(c, fhs::OP_ADDP, a, p, out);
+}
+extern "C" fhs_status fhs_sub_plain(fhs_context* c, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out) {
+    ENTER(c);
+    return plainop(c, fhs::OP_SUBP, a, p, out);
+}
+extern "C" fhs_status fhs_multiply_plain(fhs_context* c, const fhs_ciphertext* a, const fhs_plaintext* p,
+                                         fhs_ciphertext** out) {
+    ENTER(c);
+    return plainop(c, fhs::OP_MULP, a, p, out);
+}
+extern "C" fhs_status fhs_multiply(fhs_context* c, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !b || !out) return fail(FHS_ERR_INVALID, "null argument");
+    fhs_status s = same_level(a, b);
+    if (s != FHS_OK) return s;
+    if (a->ncomp != 2 || b->ncomp != 2) return fail(FHS_ERR_INVALID, "multiply expects 2-component ciphertexts");
+    fhs_ciphertext* r;
+    s = new_ct(c, 3, a->ci, a->scale * b->scale, &r);
+    if (s != FHS_OK) return s;
+    HIPCHK(fhs::launch_tensor(c->T, a->d, b->d, r->d, a->l, c->st), "multiply");
+    *out = r;
+    return FHS_OK;
+}
+
+static fhs_status run_keyswitch(fhs_context* c, std::vector<KsItem>& items, int l) {
+    const int R = (int)items.size();
+    const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, l);
+    uint64_t* ws = nullptr;
+    HIPCHK(dalloc(c, &ws, wsb), "key-switch workspace");
+    hipError_t e = fhs::launch_keyswitch(c->T, items.data(), R, l, ws, wsb, c->items_dev, c->st, nullptr);
+    dfree(c, ws, wsb);
+    if (e != hipSuccess) return hip_fail(e, "key-switch");
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_relinearize(fhs_context* c, const fhs_ciphertext* a, const fhs_relin_key* rk,
+                                      fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !rk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (a->ncomp != 3) return fail(FHS_ERR_INVALID, "relinearize expects a 3-component ciphertext");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, 2, a->ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    const size_t S = (size_t)a->l * c->N;
+    std::vector<KsItem> it{KsItem{a->d + 2 * S, a->d, a->d + S, rk->key, r->d, r->d + S, 1, 0}};
+    s = run_keyswitch(c, it, a->l);
+    if (s != FHS_OK) return s;
+    *out = r;
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_rescale_to_next(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (a->l < 2) return fail(FHS_ERR_LEVEL, "rescale_to_next: no level left (end of modulus switching chain)");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, a->ncomp, a->ci + 1, a->scale / (double)c->q[a->l - 1], &r);
+    if (s != FHS_OK) return s;
+    uint64_t* scratch = nullptr;
+    HIPCHK(dalloc(c, &scratch, 8ull * a->ncomp * c->N), "rescale");
+    HIPCHK(fhs::launch_rescale(c->T, a->d, r->d, scratch, a->ncomp, a->l, c->st), "rescale");
+    dfree(c, scratch, 8ull * a->ncomp * c->N);
+    *out = r;
+    return FHS_OK;
+}
+
+static fhs_status drop_ct(fhs_context* c, const fhs_ciphertext* a, int ci, fhs_ciphertext** out) {
+    if (ci < a->ci) return fail(FHS_ERR_LEVEL, "mod_switch_to: cannot switch to a higher level");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, a->ncomp, ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    const size_t row = 8ull * r->l * c->N, pitch = 8ull * a->l * c->N;
+    HIPCHK(hipMemcpy2DAsync(r->d, row, a->d, pitch, row, a->ncomp, hipMemcpyDeviceToDevice, c->st), "mod_switch");
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_mod_switch_to_next(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (a->l < 2) return fail(FHS_ERR_LEVEL, "mod_switch_to_next: end of modulus switching chain");
+    return drop_ct(c, a, a->ci + 1, out);
+}
+extern "C" fhs_status fhs_mod_switch_to(fhs_context* c, const fhs_ciphertext* a, int ci, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (ci > c->L0) return fail(FHS_ERR_LEVEL, "mod_switch_to: chain index out of range");
+    return drop_ct(c, a, ci, out);
+}
+static fhs_status drop_pt(fhs_context* c, const fhs_plaintext* a, int ci, fhs_plaintext** out) {
+    if (ci < a->ci || ci > c->L0) return fail(FHS_ERR_LEVEL, "mod_switch_to: bad target chain index");
+    fhs_plaintext* r;
+    fhs_status s = new_pt(c, ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    HIPCHK(hipMemcpyAsync(r->d, a->d, pt_bytes(r), hipMemcpyDeviceToDevice, c->st), "mod_switch");
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_plain_mod_switch_to_next(fhs_context* c, const fhs_plaintext* a, fhs_plaintext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    return drop_pt(c, a, a->ci + 1, out);
+}
+extern "C" fhs_status fhs_plain_mod_switch_to(fhs_context* c, const fhs_plaintext* a, int ci, fhs_plaintext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    return drop_pt(c, a, ci, out);
+}
+
+// rotation: queued, flushed as one batched key-switch (see file header)
+static fhs_status queue_rotation(fhs_context* c, const fhs_ciphertext* a, uint64_t elt, const fhs_galois_keys* gk,
+                                 fhs_ciphertext** out) {
+    if (!a || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (a->ncomp != 2) return fail(FHS_ERR_INVALID, "rotate expects a 2-component ciphertext");
+    auto it = gk->keys.find(elt);
+    if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "galois key for this rotation step is not present");
+    if (!c->pending.empty() && (c->pending_l != a->l || (int)c->pending.size() >= fhs_context::kMaxItems ||
+                                pending_uses(c, a))) {
+        fhs_status s = flush(c);
+        if (s != FHS_OK) return s;
+    }
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, 2, a->ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    const size_t S = (size_t)a->l * c->N;
+    c->pending.push_back(PendingRot{KsItem{a->d + S, a->d, nullptr, it->second, r->d, r->d + S, elt, 0}, r, a});
+    c->pending_l = a->l;
+    c->pending_refs.insert(r);
+    c->pending_refs.insert(a);
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_rotate(fhs_context* c, const fhs_ciphertext* a, int step, const fhs_galois_keys* gk,
+                                 fhs_ciphertext** out) {
+    if (!c) return fail(FHS_ERR_INVALID, "null context");
+    Guard g(c);
+    if (step == 0 || std::abs(step) >= (int)(c->N / 2)) {
+        if (step == 0) return fail(FHS_ERR_INVALID, "rotate: step 0 (use apply_galois for conjugation)");
+        return fail(FHS_ERR_INVALID, "rotate: |step| must be < slot count");
+    }
+    return queue_rotation(c, a, fhs_galois_elt_from_step(step, c->N), gk, out);
+}
+extern "C" fhs_status fhs_apply_galois(fhs_context* c, const fhs_ciphertext* a, uint64_t elt, const fhs_galois_keys* gk,
+                                       fhs_ciphertext** out) {
+    if (!c) return fail(FHS_ERR_INVALID, "null context");
+    Guard g(c);
+    return queue_rotation(c, a, elt, gk, out);
+}
+extern "C" fhs_status fhs_rotate_many(fhs_context* c, const fhs_ciphertext* const* in, const int* steps, int n,
+                                      const fhs_galois_keys* gk, fhs_ciphertext** out) {
+    if (!c) return fail(FHS_ERR_INVALID, "null context");
+    Guard g(c);
+    for (int i = 0; i < n; ++i) {
+        fhs_status s = queue_rotation(c, in[i], fhs_galois_elt_from_step(steps[i], c->N), gk, &out[i]);
+        if (s != FHS_OK) return s;
+    }
+    return flush(c);
+}
+
+// ============================================================================ fused BSGS
+static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, int G, const uint64_t* const* pt_ptrs,
+                            int D, int B, int ci, double pt_scale, const fhs_galois_keys* gk, fhs_ciphertext** out) {
+    if (G < 1 || D < 1 || !baby) return fail(FHS_ERR_INVALID, "bsgs: bad G/D");
+    const int Beff = std::min(B, (D + G - 1) / G);
+    if (Beff < 1) return fail(FHS_ERR_INVALID, "bsgs: no giant groups");
+    if (G > 2048 || (size_t)D + G > (size_t)fhs_context::kMaxPtrs) return fail(FHS_ERR_INVALID, "bsgs: too many diagonals");
+    const int l = baby[0]->l;
+    for (int b = 0; b < G; ++b) {
+        if (!baby[b] || baby[b]->l != l || baby[b]->ncomp != 2 || baby[b]->ci != ci)
+            return fail(FHS_ERR_LEVEL, "bsgs: baby steps and diagonals must share one chain index");
+    }
+    if (l < 2) return fail(FHS_ERR_LEVEL, "bsgs: no level left for the final rescale");
+    std::vector<const uint64_t*> keys(Beff, nullptr);
+    for (int g = 1; g < Beff; ++g) {
+        const uint64_t elt = fhs_galois_elt_from_step(g * G, c->N);
+        auto it = gk->keys.find(elt);
+        if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "bsgs: galois key for a giant step is missing");
+        keys[g] = it->second;
+    }
+    const size_t S = (size_t)l * c->N;
+    // pointer arrays -> device
+    std::vector<const uint64_t*> ptrs(G + D);
+    for (int b = 0; b < G; ++b) ptrs[b] = baby[b]->d;
+    for (int k = 0; k < D; ++k) ptrs[G + k] = pt_ptrs[k];
+    HIPCHK(hipMemcpyAsync(c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D), hipMemcpyHostToDevice, c->st), "bsgs");
+    const uint64_t* const* dbaby = reinterpret_cast<const uint64_t* const*>(c->ptrs_dev);
+    const uint64_t* const* dpts = dbaby + G;
+    uint64_t* inner = nullptr;
+    HIPCHK(dalloc(c, &inner, 8ull * Beff * 2 * S), "bsgs inner products");
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timer_kernel == 0) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, c->st); }
+    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dpts, G, Beff, D, l, inner, c->st), "bsgs inner");
+    if (c->timer_kernel == 0) { hipEventRecord(e1, c->st); c->timer_pairs.push_back({e0, e1}); }
+    const size_t wsb = fhs::bsgs_giant_workspace_bytes(c->T, Beff - 1, l);
+    uint64_t* ws = nullptr;
+    HIPCHK(dalloc(c, &ws, wsb), "bsgs workspace");
+    uint64_t* sum = nullptr;
+    HIPCHK(dalloc(c, &sum, 16 * S), "bsgs sum");
+    hipEvent_t tev[2] = {nullptr, nullptr};
+    if (c->timer_kernel == 1 && Beff > 1) { hipEventCreate(&tev[0]); hipEventCreate(&tev[1]); }
+    HIPCHK(fhs::launch_bsgs_giant(c->T, inner, G, Beff, l, keys.data(), sum, ws, wsb, c->items_dev, c->st,
+                                  tev[0] ? tev : nullptr), "bsgs giant");
+    if (tev[0]) c->timer_pairs.push_back({tev[0], tev[1]});
+    dfree(c, ws, wsb);
+    dfree(c, inner, 8ull * Beff * 2 * S);
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, 2, ci + 1, baby[0]->scale * pt_scale / (double)c->q[l - 1], &r);
+    if (s != FHS_OK) return s;
+    uint64_t* scratch = nullptr;
+    HIPCHK(dalloc(c, &scratch, 16ull * c->N), "bsgs rescale");
+    HIPCHK(fhs::launch_rescale(c->T, sum, r->d, scratch, 2, l, c->st), "bsgs rescale");
+    dfree(c, scratch, 16ull * c->N);
+    dfree(c, sum, 16 * S);
+    *out = r;
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_ciphertext* const* baby, int G,
+                                                   const fhs_plaintext* const* pts, int D, int B,
+                                                   const fhs_galois_keys* gk, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!pts || !gk || !out || !baby) return fail(FHS_ERR_INVALID, "null argument");
+    std::vector<const uint64_t*> p(D);
+    for (int k = 0; k < D; ++k) {
+        if (!pts[k] || pts[k]->ci != baby[0]->ci) return fail(FHS_ERR_LEVEL, "bsgs: diagonal at a different chain index");
+        if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs: diagonal scales differ");
+        p[k] = pts[k]->d;
+    }
+    return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out);
+}
+
+extern "C" fhs_status fhs_host_alloc(uint64_t bytes, void** ptr) {
+    if (!ptr) return fail(FHS_ERR_INVALID, "null argument");
+    HIPCHK(hipHostMalloc(ptr, bytes ? bytes : 8, hipHostMallocDefault), "pinned host allocation");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_host_free(void* ptr) {
+    if (ptr) HIPCHK(hipHostFree(ptr), "pinned host free");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_offload_plaintexts(fhs_context* c, const fhs_plaintext* const* pts, int count, uint64_t* host) {
+    ENTER(c);
+    if (!pts || !host || count < 1) return fail(FHS_ERR_INVALID, "offload: bad args");
+    const size_t b = pt_bytes(pts[0]);
+    for (int k = 0; k < count; ++k) {
+        if (pts[k]->l != pts[0]->l) return fail(FHS_ERR_LEVEL, "offload: plaintexts at different levels");
+        HIPCHK(hipMemcpyAsync((char*)host + (size_t)k * b, pts[k]->d, b, hipMemcpyDeviceToHost, c->st), "offload");
+    }
+    HIPCHK(hipStreamSynchronize(c->st), "offload");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_upload_plaintexts(fhs_context* c, const uint64_t* host, int count, int ci, double scale,
+                                            fhs_plaintext** outs) {
+    ENTER(c);
+    if (!host || !outs || count < 1) return fail(FHS_ERR_INVALID, "upload: bad args");
+    for (int k = 0; k < count; ++k) {
+        fhs_plaintext* pt;
+        fhs_status s = new_pt(c, ci, scale, &pt);
+        if (s != FHS_OK) return s;
+        HIPCHK(hipMemcpyAsync(pt->d, host + (size_t)k * pt->l * c->N, pt_bytes(pt), hipMemcpyHostToDevice, c->st), "upload");
+        outs[k] = pt;
+    }
+    HIPCHK(hipStreamSynchronize(c->st), "upload");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_bsgs_from_cpu(fhs_context* c, const fhs_ciphertext* const* baby, int G, const uint64_t* host,
+                                        int D, int B, int ci, double scale, const fhs_galois_keys* gk,
+                                        fhs_ciphertext** out) {
+    ENTER(c);
+    if (!baby || !host || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (ci != baby[0]->ci) return fail(FHS_ERR_LEVEL, "bsgs_from_cpu: diagonals at a different chain index");
+    const int l = c->L0 + 1 - ci;
+    const size_t bytes = 8ull * D * l * c->N;
+    uint64_t* dev = nullptr;
+    HIPCHK(dalloc(c, &dev, bytes), "bsgs_from_cpu staging");
+    HIPCHK(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, c->st), "bsgs_from_cpu upload");
+    std::vector<const uint64_t*> p(D);
+    for (int k = 0; k < D; ++k) p[k] = dev + (size_t)k * l * c->N;
+    fhs_status s = bsgs_core(c, baby, G, p.data(), D, B, ci, scale, gk, out);
+    dfree(c, dev, bytes);
+    return s;
+}
+
+// ============================================================================ measurement hooks
+extern "C" fhs_status fhs_random_plaintexts(fhs_context* c, uint64_t seed, int count, int ci, double scale,
+                                            fhs_plaintext** outs) {
+    ENTER(c);
+    if (!outs || count < 1) return fail(FHS_ERR_INVALID, "random_plaintexts: bad args");
+    for (int k = 0; k < count; ++k) {
+        fhs_plaintext* pt;
+        fhs_status s = new_pt(c, ci, scale, &pt);
+        if (s != FHS_OK) return s;
+        HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(seed, (7ull << 56) | (uint64_t)k), pt->d, pt->l, 0,
+                                  c->st), "random_plaintexts");
+        outs[k] = pt;
+    }
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_event_record(fhs_context* c, void** ev) {
+    ENTER(c);
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e), "event");
+    HIPCHK(hipEventRecord(e, c->st), "event");
+    *ev = (void*)e;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_event_elapsed(void* a, void* b, float* ms) {
+    HIPCHK(hipEventSynchronize((hipEvent_t)b), "event sync");
+    HIPCHK(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "event elapsed");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_event_destroy(void* e) {
+    if (e) hipEventDestroy((hipEvent_t)e);
+    return FHS_OK;
+}
+// kernel 0 = k_bsgs_inner (Hadamard), kernel 1 = k_modup_ip (every key-switch); -1 = off
+extern "C" fhs_status fhs_kernel_timer(fhs_context* c, int kernel_id, float* ms, int* launches, int reset) {
+    ENTER(c);
+    HIPCHK(hipStreamSynchronize(c->st), "timer sync");
+    float tot = 0.f;
+    int n = 0;
+    for (auto& pr : c->timer_pairs) {
+        float t = 0.f;
+        if (hipEventElapsedTime(&t, pr.first, pr.second) == hipSuccess) { tot += t; ++n; }
+    }
+    if (ms) *ms = tot;
+    if (launches) *launches = n;
+    if (reset) {
+        for (auto& pr : c->timer_pairs) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+        c->timer_pairs.clear();
+    }
+    c->timer_kernel = kernel_id;
+    return FHS_OK;
+}

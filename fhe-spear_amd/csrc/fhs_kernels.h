@@ -1,0 +1,70 @@
+// fhs_kernels.h -- launch wrappers for the gfx950 kernels (fhs_kernels.hip).  Host-side only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fhs {
+
+typedef uint64_t u64;
+
+// Device-resident parameter tables (built once per context, fhs_host.hip).
+struct DevTables {
+    const void* primes;       // PrimeK[K]
+    const u64* tw_fwd;        // [K][N][2]  psi^rev(k), Shoup
+    const u64* tw_inv;        // [K][N][2]  psi^-rev(k), Shoup
+    const u64* modup_intt;    // [L0+1][L0][4]  INTT stage-0 constants with inv_hat folded in
+    const u64* modup_hat;     // [L0+1][dnum][P][K]  (Q_S / q_u) mod prime(t)
+    const u64* md_intt;       // [P][4]  INTT constants with inv(P/p_k) folded in
+    const u64* md_hat;        // [P][L0]  (P / p_k) mod q_i
+    const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup
+    const u64* rescale;       // [L0+1][L0][4]  inv(q_{l-1}) mod q_i (+Shoup), half mod q_i, half
+    const u64* pow2;          // [K][1088] 2^e mod q_i (exact double reduction)
+    int N, logN, L0, P, K, dnum;
+};
+
+// One key-switch input of a batch.
+struct KsItem {
+    const u64* a;        // poly to switch (NTT form, l limbs), read through galois elt `elt`
+    const u64* add0;     // added to output comp 0 (through `elt`), may be null
+    const u64* add1;     // added to output comp 1 (identity), may be null
+    const u64* key;      // [dnum][2][K][N]
+    u64* out0;           // l limbs
+    u64* out1;           // l limbs
+    u64 elt;             // galois element applied to a / add0 (1 = identity)
+    u64 pad;
+};
+
+// all launchers enqueue on `st` and return hipSuccess or the first launch error
+hipError_t launch_ntt_fwd(const DevTables& T, u64* data, int limbs, int l_split, int npoly, size_t poly_stride,
+                          hipStream_t st);
+hipError_t launch_ntt_inv(const DevTables& T, u64* data, int limbs, int l_split, int npoly, size_t poly_stride,
+                          hipStream_t st);
+hipError_t launch_eltwise(const DevTables& T, int op, const u64* a, const u64* b, u64* out, int ncomp, int l,
+                          size_t a_cstride, size_t b_cstride, hipStream_t st);
+hipError_t launch_tensor(const DevTables& T, const u64* a, const u64* b, u64* out3, int l, hipStream_t st);
+hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
+                          hipStream_t st);
+hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, int l, u64* workspace,
+                            size_t ws_bytes, void* items_dev, hipStream_t st, hipEvent_t* timer_ev);
+size_t keyswitch_workspace_bytes(const DevTables& T, int R, int l);
+hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
+                             int D, int l, u64* inner, hipStream_t st);
+// giant-step key-switches of inner[1..B-1] (rotation by g*G), summed with inner[0]; output 2 x l limbs
+hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
+                             u64* out, u64* workspace, size_t ws_bytes, void* items_dev, hipStream_t st,
+                             hipEvent_t* timer_ev);
+size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l);
+hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
+hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,
+                                      const u64* snew_ntt, int digit, hipStream_t st);
+hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int limbs, u64 elt, hipStream_t st);
+hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
+                                  const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st);
+hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);
+hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st);
+hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st);
+
+enum EltOp { OP_ADD = 0, OP_SUB = 1, OP_NEG = 2, OP_MULP = 3, OP_ADDP = 4, OP_SUBP = 5, OP_SUBNEG = 6 };
+enum SampleMode { SAMPLE_UNIFORM = 0, SAMPLE_TERNARY = 1, SAMPLE_CBD = 2 };
+
+}  // namespace fhs

@@ -1,0 +1,731 @@
+// fhs_kernels.hip -- hand-written gfx950 kernels for the CKKS BSGS hot path.
+//
+// Kernel map:
+//   k_ntt_fwd / k_ntt_inv          batched per-limb negacyclic NTT (one limb per workgroup, LDS-resident)
+//   k_eltwise / k_tensor           ct add/sub/negate, ct x pt Hadamard (pb:167, 181), ct x ct tensor (pb:177)
+//   k_rescale_*                    divide-and-round by q_last (pb:185, bg:484)
+//   k_ks_intt / k_modup_ip /       hybrid key-switch: automorphism+INTT, fused ModUp+NTT+key inner product,
+//   k_ks_special_intt / k_moddown  ModDown (pb:203 rotate, pb:183 relinearize)
+//   k_bsgs_inner                   sum_b baby[b] (.) pt[gG+b] for every giant group g (bg:465-476)
+//   k_giant_sum / k_giant_final    giant-step rotations summed exactly in the extended basis (bg:478-483)
+//   k_sample / k_swk / ...         deterministic key generation and encryption helpers
+// Every integer result is reduced to [0, q): limbs are bit-identical to oracle/ckks_oracle.c.
+#include "fhs_kernels.h"
+#include "fhs_ntt.h"
+
+namespace fhs {
+
+#define FHS_DISPATCH_LOGN(logN, ...)                   \
+    switch (logN) {                                    \
+        case 8: { constexpr int LOGN = 8; __VA_ARGS__; } break;   \
+        case 9: { constexpr int LOGN = 9; __VA_ARGS__; } break;   \
+        case 10: { constexpr int LOGN = 10; __VA_ARGS__; } break; \
+        case 11: { constexpr int LOGN = 11; __VA_ARGS__; } break; \
+        case 12: { constexpr int LOGN = 12; __VA_ARGS__; } break; \
+        case 13: { constexpr int LOGN = 13; __VA_ARGS__; } break; \
+        case 14: { constexpr int LOGN = 14; __VA_ARGS__; } break; \
+        default: return hipErrorInvalidValue;          \
+    }
+
+__device__ __forceinline__ const PrimeK& PK(const DevTables& T, int i) {
+    return reinterpret_cast<const PrimeK*>(T.primes)[i];
+}
+__device__ __forceinline__ int limb_prime(int b, int l_split, int L0) { return b < l_split ? b : L0 + (b - l_split); }
+
+// NTT-domain automorphism X -> X^elt: output slot e reads input slot galois_src(e)
+__device__ __forceinline__ int galois_src(int e, u64 elt, int logN) {
+    if (elt == 1) return e;
+    const unsigned r = __brev((unsigned)e) >> (32 - logN);
+    const u64 m = (u64)2 << logN;
+    const u64 e2 = ((2 * (u64)r + 1) * elt) & (m - 1);
+    return (int)(__brev((unsigned)((e2 - 1) >> 1)) >> (32 - logN));
+}
+
+template <int LOGN>
+constexpr size_t lds_bytes() { return (size_t)((1 << LOGN) + (1 << LOGN) / 16) * 8; }
+
+// ============================================================================ plain NTT
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_fwd(DevTables T, u64* data, int limbs, int l_split,
+                                                              size_t poly_stride) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const int pi = limb_prime(b, l_split, T.L0);
+    const u64 q = PK(T, pi).q;
+    u64* p = data + blockIdx.y * poly_stride + (size_t)b * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = p[tid + k * TH];
+    __syncthreads();
+    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)pi * N * 2, q);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        p[e] = csub(csub(lds[lds_pad(e)], 2 * q), q);
+    }
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_inv(DevTables T, u64* data, int limbs, int l_split,
+                                                              size_t poly_stride) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const int pi = limb_prime(b, l_split, T.L0);
+    const PrimeK& P = PK(T, pi);
+    u64* p = data + blockIdx.y * poly_stride + (size_t)b * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = p[tid + c * TH];
+    __syncthreads();
+    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
+}
+
+hipError_t launch_ntt_fwd(const DevTables& T, u64* data, int limbs, int l_split, int npoly, size_t poly_stride,
+                          hipStream_t st) {
+    if (limbs <= 0 || npoly <= 0) return hipSuccess;
+    FHS_DISPATCH_LOGN(T.logN, {
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN>), dim3(limbs, npoly), dim3((1 << LOGN) / 16), 0, st, T,
+                           data, limbs, l_split, poly_stride);
+    });
+    return hipGetLastError();
+}
+hipError_t launch_ntt_inv(const DevTables& T, u64* data, int limbs, int l_split, int npoly, size_t poly_stride,
+                          hipStream_t st) {
+    if (limbs <= 0 || npoly <= 0) return hipSuccess;
+    FHS_DISPATCH_LOGN(T.logN, {
+        hipLaunchKernelGGL((k_ntt_inv<LOGN>), dim3(limbs, npoly), dim3((1 << LOGN) / 16), 0, st, T,
+                           data, limbs, l_split, poly_stride);
+    });
+    return hipGetLastError();
+}
+
+// ============================================================================ element-wise
+// a: ncomp x l x N (component stride a_cs); b: component stride b_cs (0 = plaintext broadcast)
+__global__ void k_eltwise(DevTables T, int op, const u64* __restrict__ a, const u64* __restrict__ b,
+                          u64* __restrict__ out, int ncomp, int l, size_t a_cs, size_t b_cs) {
+    const int N = T.N;
+    const size_t half = (size_t)N / 2;
+    const size_t total = (size_t)ncomp * l * half;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t n2 = idx % half;
+        const size_t li = idx / half;
+        const int i = (int)(li % l), comp = (int)(li / l);
+        const PrimeK& P = PK(T, i);
+        const u64 q = P.q;
+        const size_t off = (size_t)i * N + 2 * n2;
+        const ulonglong2 av = *reinterpret_cast<const ulonglong2*>(a + comp * a_cs + off);
+        ulonglong2 bv = make_ulonglong2(0, 0);
+        if (op != OP_NEG) bv = *reinterpret_cast<const ulonglong2*>(b + comp * b_cs + off);
+        u64 r0, r1;
+        switch (op) {
+            case OP_ADD: r0 = addmod(av.x, bv.x, q); r1 = addmod(av.y, bv.y, q); break;
+            case OP_SUB: r0 = submod(av.x, bv.x, q); r1 = submod(av.y, bv.y, q); break;
+            case OP_SUBNEG: r0 = submod(bv.x, av.x, q); r1 = submod(bv.y, av.y, q); break;
+            case OP_NEG: r0 = av.x ? q - av.x : 0; r1 = av.y ? q - av.y : 0; break;
+            case OP_MULP: r0 = mulmod(av.x, bv.x, q, P.r0, P.r1); r1 = mulmod(av.y, bv.y, q, P.r0, P.r1); break;
+            case OP_ADDP:
+                if (comp == 0) { r0 = addmod(av.x, bv.x, q); r1 = addmod(av.y, bv.y, q); }
+                else { r0 = av.x; r1 = av.y; }
+                break;
+            case OP_SUBP:
+                if (comp == 0) { r0 = submod(av.x, bv.x, q); r1 = submod(av.y, bv.y, q); }
+                else { r0 = av.x; r1 = av.y; }
+                break;
+            default: r0 = r1 = 0;
+        }
+        *reinterpret_cast<ulonglong2*>(out + (size_t)comp * l * N + off) = make_ulonglong2(r0, r1);
+    }
+}
+
+static inline int eltwise_grid(size_t work) {
+    size_t g = (work + 255) / 256;
+    if (g > 8192) g = 8192;
+    return (int)(g ? g : 1);
+}
+
+hipError_t launch_eltwise(const DevTables& T, int op, const u64* a, const u64* b, u64* out, int ncomp, int l,
+                          size_t a_cs, size_t b_cs, hipStream_t st) {
+    const size_t work = (size_t)ncomp * l * T.N / 2;
+    hipLaunchKernelGGL(k_eltwise, dim3(eltwise_grid(work)), dim3(256), 0, st, T, op, a, b, out, ncomp, l, a_cs, b_cs);
+    return hipGetLastError();
+}
+
+// (a0 b0, a0 b1 + a1 b0, a1 b1)  -- pb:177 multiply
+__global__ void k_tensor(DevTables T, const u64* __restrict__ a, const u64* __restrict__ b, u64* __restrict__ out,
+                         int l) {
+    const int N = T.N;
+    const size_t S = (size_t)l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx / N);
+        const PrimeK& P = PK(T, i);
+        const u64 a0 = a[idx], a1 = a[S + idx], b0 = b[idx], b1 = b[S + idx];
+        out[idx] = mulmod(a0, b0, P.q, P.r0, P.r1);
+        u128 m = {0, 0};
+        mac128(m, a0, b1);
+        mac128(m, a1, b0);
+        out[S + idx] = barrett128(m.lo, m.hi, P.q, P.r0, P.r1);
+        out[2 * S + idx] = mulmod(a1, b1, P.q, P.r0, P.r1);
+    }
+}
+hipError_t launch_tensor(const DevTables& T, const u64* a, const u64* b, u64* out3, int l, hipStream_t st) {
+    hipLaunchKernelGGL(k_tensor, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, a, b, out3, l);
+    return hipGetLastError();
+}
+
+// product of two K-limb polynomials (key material: s^2)
+__global__ void k_key_prod(DevTables T, const u64* a, const u64* b, u64* out, int limbs) {
+    const size_t S = (size_t)limbs * T.N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const PrimeK& P = PK(T, (int)(idx / T.N));
+        out[idx] = mulmod(a[idx], b[idx], P.q, P.r0, P.r1);
+    }
+}
+hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st) {
+    hipLaunchKernelGGL(k_key_prod, dim3(eltwise_grid((size_t)limbs * T.N)), dim3(256), 0, st, T, a, b, out, limbs);
+    return hipGetLastError();
+}
+
+__global__ void k_galois_perm(DevTables T, const u64* in, u64* out, int limbs, u64 elt) {
+    const size_t S = (size_t)limbs * T.N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t base = idx - idx % T.N;
+        out[idx] = in[base + galois_src((int)(idx % T.N), elt, T.logN)];
+    }
+}
+hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int limbs, u64 elt, hipStream_t st) {
+    hipLaunchKernelGGL(k_galois_perm, dim3(eltwise_grid((size_t)limbs * T.N)), dim3(256), 0, st, T, in, out, limbs,
+                       elt);
+    return hipGetLastError();
+}
+
+// ============================================================================ rescale (pb:185)
+// 1) last limb of each component -> coefficient form (scratch[comp])
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_intt(DevTables T, const u64* in, u64* scratch, int l) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, comp = blockIdx.x, pi = l - 1;
+    const PrimeK& P = PK(T, pi);
+    const u64* src = in + ((size_t)comp * l + pi) * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[tid + c * TH];
+    __syncthreads();
+    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
+    const u64 half = P.q >> 1;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        scratch[(size_t)comp * N + tid + k * TH] = addmod(csub(lds[lds_pad(tid + k * TH)], P.q), half, P.q);
+}
+// 2) per (i < l-1, comp): NTT_i([v mod q_i] - [half mod q_i]) and combine (a_i - t) * q_last^-1
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_ntt(DevTables T, const u64* in, const u64* scratch,
+                                                                  u64* out, int l) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, i = blockIdx.x, comp = blockIdx.y;
+    const PrimeK& P = PK(T, i);
+    const u64* rs = T.rescale + ((size_t)l * T.L0 + i) * 4;   // inv, inv_s, half mod q_i
+    const u64 inv = rs[0], inv_s = rs[1], hq = rs[2];
+    const u64* src = scratch + (size_t)comp * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = submod(barrett64(src[tid + k * TH], P.q, P.r0, P.r1), hq, P.q);
+    __syncthreads();
+    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
+    const u64* a = in + ((size_t)comp * l + i) * N;
+    u64* o = out + ((size_t)comp * (l - 1) + i) * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        const u64 t = csub(csub(lds[lds_pad(e)], 2 * P.q), P.q);
+        o[e] = shoup(submod(a[e], t, P.q), inv, inv_s, P.q);
+    }
+}
+hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
+                          hipStream_t st) {
+    FHS_DISPATCH_LOGN(T.logN, {
+        hipLaunchKernelGGL((k_rescale_intt<LOGN>), dim3(ncomp), dim3((1 << LOGN) / 16), 0, st, T,
+                           in, scratch, l);
+        hipLaunchKernelGGL((k_rescale_ntt<LOGN>), dim3(l - 1, ncomp), dim3((1 << LOGN) / 16), 0, st,
+                           T, in, scratch, out, l);
+    });
+    return hipGetLastError();
+}
+
+// ============================================================================ key-switch
+// (a) y = INTT(galois(a)) * inv_hat(digit) per data limb (inv_hat folded into the N^-1 stage)
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const KsItem* items, u64* acoef, int l) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, i = blockIdx.x, r = blockIdx.y;
+    const KsItem it = items[r];
+    const PrimeK& P = PK(T, i);
+    const u64* src = it.a + (size_t)i * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        lds[lds_pad(e)] = src[galois_src(e, it.elt, LOGN)];
+    }
+    __syncthreads();
+    const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
+    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)i * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
+    u64* dst = acoef + ((size_t)r * l + i) * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
+}
+
+// (b1) ModUp + NTT: ext[r][j][t] = NTT_t(conv_{digit j -> prime t}(y)) for every extended-basis
+// limb t outside digit j (limbs inside digit j are the input itself and are read by k_ks_ip).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u64* acoef, u64* ext, int l) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, t = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+    const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
+    if (t >= s0 && t < s1) return;   // whole block exits: no barrier is skipped
+    const int pt = t < l ? t : T.L0 + (t - l);
+    const PrimeK& PM = PK(T, pt);
+    const u64 m = PM.q;
+    const u64* yb = acoef + ((size_t)r * l + s0) * N;
+    const u64* hat = T.modup_hat + (((size_t)l * T.dnum + j) * P_) * K + pt;
+    u64 h[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) h[u] = u < ns ? hat[(size_t)u * K] : 0;
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+        const int e = tid + k * TH;
+        u128 s = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (u < ns) mac128(s, yb[(size_t)u * N + e], h[u]);
+        lds[lds_pad(e)] = barrett128(s.lo, s.hi, m, PM.r0, PM.r1);
+    }
+    __syncthreads();
+    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m);
+    u64* o = ext + (((size_t)r * dn + j) * E + t) * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        o[e] = csub(csub(lds[lds_pad(e)], 2 * m), m);
+    }
+}
+
+// (b2) key inner product, lazy 128-bit: acc[r][c][t] = sum_j ext_j[t] (.) key_j[c][t]  (one
+// Barrett reduction per output word instead of one per product)
+__global__ void k_ks_ip(DevTables T, const KsItem* items, const u64* ext, u64* acc, int l, int R) {
+    const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    const size_t per_r = (size_t)E * N;
+    const size_t total = (size_t)R * per_r;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(idx / per_r);
+        const int t = (int)((idx % per_r) / N), n = (int)(idx % N);
+        const int pt = t < l ? t : T.L0 + (t - l);
+        const PrimeK& PM = PK(T, pt);
+        const KsItem it = items[r];
+        const u64* ex = ext + (size_t)r * dn * per_r + (size_t)t * N + n;
+        const u64* key = it.key + (size_t)pt * N + n;
+        const int jown = t < l ? t / P_ : -1;
+        u128 c0 = {0, 0}, c1 = {0, 0};
+        for (int j = 0; j < dn; ++j) {
+            const u64 v = (j == jown) ? it.a[(size_t)t * N + galois_src(n, it.elt, T.logN)] : ex[(size_t)j * per_r];
+            mac128(c0, v, key[(size_t)(2 * j) * K * N]);
+            mac128(c1, v, key[(size_t)(2 * j + 1) * K * N]);
+        }
+        acc[(((size_t)r * 2 + 0) * E + t) * N + n] = barrett128(c0.lo, c0.hi, PM.q, PM.r0, PM.r1);
+        acc[(((size_t)r * 2 + 1) * E + t) * N + n] = barrett128(c1.lo, c1.hi, PM.q, PM.r0, PM.r1);
+    }
+}
+
+// (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_special_intt(DevTables T, const u64* acc, u64* ycoef, int l,
+                                                                      int R) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, k = blockIdx.x, comp = blockIdx.y, r = blockIdx.z;
+    const int P_ = T.P, E = l + P_, pi = T.L0 + k;
+    const PrimeK& P = PK(T, pi);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        lds[lds_pad(e)] = acc[(((size_t)r * 2 + comp) * E + l + k) * N + e];
+    }
+    __syncthreads();
+    const u64* cst = T.md_intt + (size_t)k * 4;
+    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
+    u64* dst = ycoef + (((size_t)r * 2 + comp) * P_ + k) * N;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) dst[tid + kk * TH] = csub(lds[lds_pad(tid + kk * TH)], P.q);
+}
+
+// (d) ModDown: out_c[i] = (acc_c[i] - NTT(conv_P->q_i(y_c))) * P^-1 (+ add_c)
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const KsItem* items, const u64* acc,
+                                                              const u64* ycoef, int l, int R) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, i = blockIdx.x, comp = blockIdx.y, r = blockIdx.z;
+    const int P_ = T.P, E = l + P_;
+    const PrimeK& P = PK(T, i);
+    const u64 q = P.q;
+    const KsItem it = items[r];
+    const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N;
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+        const int e = tid + kk * TH;
+        u128 s = {0, 0};
+        for (int k = 0; k < P_; ++k) mac128(s, y[(size_t)k * N + e], T.md_hat[(size_t)k * T.L0 + i]);
+        lds[lds_pad(e)] = barrett128(s.lo, s.hi, q, P.r0, P.r1);
+    }
+    __syncthreads();
+    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)i * N * 2, q);
+    const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
+    const u64* add = comp == 0 ? it.add0 : it.add1;
+    const u64 aelt = comp == 0 ? it.elt : 1;
+    u64* o = (comp == 0 ? it.out0 : it.out1) + (size_t)i * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        const u64 v = csub(csub(lds[lds_pad(e)], 2 * q), q);
+        const u64 a = acc[(((size_t)r * 2 + comp) * E + i) * N + e];
+        u64 res = shoup(submod(a, v, q), pinv, pinv_s, q);
+        if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
+        o[e] = res;
+    }
+}
+
+size_t keyswitch_workspace_bytes(const DevTables& T, int R, int l) {
+    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
+    // acoef | ext | acc | ycoef
+    return 8 * N * ((size_t)R * l + (size_t)R * dn * E + (size_t)R * 2 * E + (size_t)R * 2 * T.P);
+}
+
+// ModUp + key inner product for R items; leaves acc [R][2][E][N] and ycoef [R][2][P][N]
+template <int LOGN>
+static void ks_front(const DevTables& T, const KsItem* it, int R, int l, u64* ws, hipStream_t st,
+                     hipEvent_t* timer_ev, u64** acc_out, u64** ycoef_out) {
+    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
+    u64* acoef = ws;
+    u64* ext = acoef + (size_t)R * l * N;
+    u64* acc = ext + (size_t)R * dn * E * N;
+    u64* ycoef = acc + (size_t)R * 2 * E * N;
+    const dim3 blk((1 << LOGN) / 16);
+    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l, R), blk, 0, st, T, it, acoef, l);
+    if (timer_ev) hipEventRecord(timer_ev[0], st);
+    hipLaunchKernelGGL((k_modup<LOGN>), dim3(E, dn, R), blk, 0, st, T, acoef, ext, l);
+    if (timer_ev) hipEventRecord(timer_ev[1], st);
+    hipLaunchKernelGGL(k_ks_ip, dim3(eltwise_grid((size_t)R * E * N)), dim3(256), 0, st, T, it, ext, acc, l, R);
+    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), blk, 0, st, T, acc, ycoef, l, R);
+    *acc_out = acc;
+    *ycoef_out = ycoef;
+}
+
+hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, int l, u64* ws, size_t ws_bytes,
+                            void* items_dev, hipStream_t st, hipEvent_t* timer_ev) {
+    if (keyswitch_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
+    hipError_t e = hipMemcpyAsync(items_dev, items_host, sizeof(KsItem) * R, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    const KsItem* it = reinterpret_cast<const KsItem*>(items_dev);
+    FHS_DISPATCH_LOGN(T.logN, {
+        u64 *acc, *ycoef;
+        ks_front<LOGN>(T, it, R, l, ws, st, timer_ev, &acc, &ycoef);
+        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l, 2, R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
+    });
+    return hipGetLastError();
+}
+
+// ============================================================================ BSGS
+// inner[g] = sum_{b < G, gG+b < D} baby[b] (.) pts[gG+b]        (bg:465-476)
+// Block = 4 waves sharing one 64-coefficient slice of limb i: the slice of all G baby steps
+// (both components) is staged once in LDS, each wave then streams the diagonals of its giant
+// groups (g = wave, wave+4, ...) from HBM with lazy 128-bit accumulation.
+__global__ void __launch_bounds__(256) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
+                                                    const u64* const* __restrict__ pts, int G, int B, int D, int l,
+                                                    u64* __restrict__ inner) {
+    extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][64]
+    const int N = T.N;
+    const int i = blockIdx.y, n0 = blockIdx.x * 64, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const size_t S = (size_t)l * N;
+    for (int idx = tid; idx < G * 128; idx += 256) {
+        const int b = idx >> 7, comp = (idx >> 6) & 1, c = idx & 63;
+        sb[idx] = baby[b][comp * S + (size_t)i * N + n0 + c];
+    }
+    __syncthreads();
+    const PrimeK& P = PK(T, i);
+    const u64 q = P.q;
+    const size_t off = (size_t)i * N + n0 + lane;
+    for (int g = wave; g < B; g += 4) {
+        const int bmax = min(G, D - g * G);
+        if (bmax <= 0) continue;
+        u128 c0 = {0, 0}, c1 = {0, 0};
+        const u64* const* pg = pts + (size_t)g * G;
+        int b = 0;
+        for (; b + 4 <= bmax; b += 4) {
+            const u64 p0 = pg[b][off], p1 = pg[b + 1][off], p2 = pg[b + 2][off], p3 = pg[b + 3][off];
+            mac128(c0, sb[(b * 2 + 0) * 64 + lane], p0);
+            mac128(c1, sb[(b * 2 + 1) * 64 + lane], p0);
+            mac128(c0, sb[(b * 2 + 2) * 64 + lane], p1);
+            mac128(c1, sb[(b * 2 + 3) * 64 + lane], p1);
+            mac128(c0, sb[(b * 2 + 4) * 64 + lane], p2);
+            mac128(c1, sb[(b * 2 + 5) * 64 + lane], p2);
+            mac128(c0, sb[(b * 2 + 6) * 64 + lane], p3);
+            mac128(c1, sb[(b * 2 + 7) * 64 + lane], p3);
+            if ((b & 31) == 28) {   // keep the lazy sum < 2^128 for any prime < 2^61
+                c0.lo = barrett128(c0.lo, c0.hi, q, P.r0, P.r1); c0.hi = 0;
+                c1.lo = barrett128(c1.lo, c1.hi, q, P.r0, P.r1); c1.hi = 0;
+            }
+        }
+        for (; b < bmax; ++b) {
+            const u64 p = pg[b][off];
+            mac128(c0, sb[(b * 2 + 0) * 64 + lane], p);
+            mac128(c1, sb[(b * 2 + 1) * 64 + lane], p);
+        }
+        inner[(size_t)g * 2 * S + off] = barrett128(c0.lo, c0.hi, q, P.r0, P.r1);
+        inner[(size_t)g * 2 * S + S + off] = barrett128(c1.lo, c1.hi, q, P.r0, P.r1);
+    }
+}
+hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
+                             int D, int l, u64* inner, hipStream_t st) {
+    if (T.N % 64) return hipErrorInvalidValue;
+    const size_t sh = (size_t)G * 128 * 8;
+    hipLaunchKernelGGL(k_bsgs_inner, dim3(T.N / 64, l), dim3(256), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
+    return hipGetLastError();
+}
+
+// Giant steps.  Exactness: every output limb is a sum of exact residues, so
+//   sum_r ModDown(acc_r) = (sum_r acc_r - NTT(sum_r conv(y_r))) * P^-1   (mod q_i)
+// is bit-identical to rotating and adding one giant step at a time (bg:478-483).
+// base_c = (sum_r acc_r,c) P^-1 + [c==0] sum_r galois_r(inner_r.c0) + inner_0.c ;  convsum_c = sum_r conv(y_r,c)
+__global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, const u64* ycoef, const u64* inner0,
+                            u64* base, u64* convsum, int l, int R) {
+    const int N = T.N, P_ = T.P, E = l + P_;
+    const size_t S = (size_t)l * N;
+    const size_t total = 2 * S;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int comp = (int)(idx / S);
+        const int i = (int)((idx % S) / N), n = (int)(idx % N);
+        const PrimeK& P = PK(T, i);
+        const u64 q = P.q;
+        u128 cs = {0, 0};
+        u64 as = 0, add = inner0[(size_t)comp * S + (size_t)i * N + n];
+        int cnt = 0;
+        for (int r = 0; r < R; ++r) {
+            const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N + n;
+            for (int k = 0; k < P_; ++k) {
+                mac128(cs, y[(size_t)k * N], T.md_hat[(size_t)k * T.L0 + i]);
+                if (++cnt == 48) { cs.lo = barrett128(cs.lo, cs.hi, q, P.r0, P.r1); cs.hi = 0; cnt = 0; }
+            }
+            as = addmod(as, acc[(((size_t)r * 2 + comp) * E + i) * N + n], q);
+            if (comp == 0) {
+                const KsItem it = items[r];
+                add = addmod(add, it.add0[(size_t)i * N + galois_src(n, it.elt, T.logN)], q);
+            }
+        }
+        convsum[idx] = barrett128(cs.lo, cs.hi, q, P.r0, P.r1);
+        base[idx] = addmod(shoup(as, T.md_pinv[2 * i], T.md_pinv[2 * i + 1], q), add, q);
+    }
+}
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_giant_final(DevTables T, const u64* base, const u64* convsum,
+                                                                  u64* out, int l) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, i = blockIdx.x, comp = blockIdx.y;
+    const PrimeK& P = PK(T, i);
+    const size_t off = ((size_t)comp * l + i) * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = convsum[off + tid + k * TH];
+    __syncthreads();
+    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
+    const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        const u64 v = csub(csub(lds[lds_pad(e)], 2 * P.q), P.q);
+        out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, P.q), P.q);
+    }
+}
+
+size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
+    return keyswitch_workspace_bytes(T, R, l) + 8 * (size_t)T.N * 4 * l;
+}
+
+hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
+                             u64* out, u64* ws, size_t ws_bytes, void* items_dev, hipStream_t st, hipEvent_t* timer_ev) {
+    const int R = B - 1;
+    const size_t N = T.N, S = (size_t)l * N;
+    if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
+    if (bsgs_giant_workspace_bytes(T, R, l) > ws_bytes || R > 512) return hipErrorInvalidValue;
+    u64* base = ws + keyswitch_workspace_bytes(T, R, l) / 8;
+    u64* convsum = base + 2 * S;
+    KsItem items[512];
+    for (int r = 0; r < R; ++r) {
+        const int g = r + 1;
+        const u64* ct = inner + (size_t)g * 2 * S;
+        u64 elt = 1;
+        for (int s = 0; s < g * G; ++s) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
+        items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, 0};
+    }
+    hipError_t e = hipMemcpyAsync(items_dev, items, sizeof(KsItem) * R, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    const KsItem* it = reinterpret_cast<const KsItem*>(items_dev);
+    FHS_DISPATCH_LOGN(T.logN, {
+        u64 *acc, *ycoef;
+        ks_front<LOGN>(T, it, R, l, ws, st, timer_ev, &acc, &ycoef);
+        hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, st, T, it, acc, ycoef, inner, base,
+                           convsum, l, R);
+        hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3((1 << LOGN) / 16), 0, st, T, base, convsum, out, l);
+    });
+    return hipGetLastError();
+}
+
+// ============================================================================ sampling / keys
+__device__ __forceinline__ u64 sm64(u64 x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+__device__ __forceinline__ u64 rnd(u64 key, u64 ctr) { return sm64(key ^ sm64(ctr ^ 0xD1B54A32D192ED03ULL)); }
+
+// mode 0: uniform mod q_i directly (NTT-domain sample); 1: ternary; 2: CBD(21) -- small values
+// replicated over limbs in coefficient form (caller runs the forward NTT)
+__global__ void k_sample(DevTables T, int mode, u64 key, u64* out, int l) {
+    const int N = T.N;
+    const size_t S = (size_t)l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx / N), n = (int)(idx % N);
+        const PrimeK& P = PK(T, i);
+        u64 v;
+        if (mode == SAMPLE_UNIFORM) {
+            const u64 ctr = 2 * ((u64)i * N + n);
+            v = barrett128(rnd(key, ctr + 1), rnd(key, ctr), P.q, P.r0, P.r1);
+        } else {
+            const u64 r = rnd(key, (u64)n);
+            long long s;
+            if (mode == SAMPLE_TERNARY) {
+                const u64 t = r % 3;
+                s = t == 2 ? -1 : (long long)t;
+            } else {
+                s = (long long)__popcll(r & 0x1FFFFFULL) - (long long)__popcll((r >> 21) & 0x1FFFFFULL);
+            }
+            v = s >= 0 ? (u64)s : P.q - (u64)(-s);
+        }
+        out[idx] = v;
+    }
+}
+hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int, hipStream_t st) {
+    hipLaunchKernelGGL(k_sample, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, mode, key, out, l);
+    return hipGetLastError();
+}
+
+// key_j[0] = e - a s + [i in digit j] (P mod q_i) s_new ; key_j[1] = a (already in place)
+__global__ void k_swk(DevTables T, u64* key, const u64* e, const u64* s, const u64* snew, int j) {
+    const int N = T.N, K = T.K;
+    const size_t S = (size_t)K * N;
+    u64* k0 = key + (size_t)j * 2 * S;
+    const u64* k1 = k0 + S;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx / N);
+        const PrimeK& P = PK(T, i);
+        u64 v = submod(e[idx], mulmod(k1[idx], s[idx], P.q, P.r0, P.r1), P.q);
+        if (i < T.L0 && i / T.P == j) {
+            const u64 pm = T.md_pinv[2 * T.L0 + i];   // P mod q_i stored after the inverses
+            v = addmod(v, mulmod(pm, snew[idx], P.q, P.r0, P.r1), P.q);
+        }
+        k0[idx] = v;
+    }
+}
+hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,
+                                      const u64* snew_ntt, int digit, hipStream_t st) {
+    hipLaunchKernelGGL(k_swk, dim3(eltwise_grid((size_t)T.K * T.N)), dim3(256), 0, st, T, key, e_ntt, s_ntt, snew_ntt,
+                       digit);
+    return hipGetLastError();
+}
+
+// mode 0 (symmetric): c0 = e0 - c1 s + pt (c1 holds the uniform a); mode 1 (public key):
+// c0 = u pk0 + e0 + pt, c1 = u pk1 + e1.  pk limbs are at the top level (stride L0 N).
+__global__ void k_encrypt(DevTables T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1, const u64* u,
+                          const u64* e0, const u64* e1, const u64* pt, int l) {
+    const int N = T.N;
+    const size_t S = (size_t)l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx / N);
+        const PrimeK& P = PK(T, i);
+        const u64 q = P.q;
+        const u64 m = pt ? pt[idx] : 0;
+        if (mode == 0) {
+            c0[idx] = addmod(submod(e0[idx], mulmod(c1[idx], s_or_pk0[idx], q, P.r0, P.r1), q), m, q);
+        } else {
+            c0[idx] = addmod(addmod(mulmod(u[idx], s_or_pk0[idx], q, P.r0, P.r1), e0[idx], q), m, q);
+            c1[idx] = addmod(mulmod(u[idx], pk1[idx], q, P.r0, P.r1), e1[idx], q);
+        }
+    }
+}
+hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
+                                  const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st) {
+    hipLaunchKernelGGL(k_encrypt, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, mode, c0, c1, s_or_pk0,
+                       pk1, u_ntt, e0, e1, pt, l);
+    return hipGetLastError();
+}
+
+// m = c0 + c1 s + c2 s^2 (s at key level: limb i of s is at i*N)
+__global__ void k_decrypt(DevTables T, const u64* ct, int ncomp, const u64* s, u64* out, int l) {
+    const int N = T.N;
+    const size_t S = (size_t)l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const int i = (int)(idx / N);
+        const PrimeK& P = PK(T, i);
+        const u64 sv = s[idx];
+        u64 v = ct[idx], sp = sv;
+        for (int k = 1; k < ncomp; ++k) {
+            v = addmod(v, mulmod(ct[k * S + idx], sp, P.q, P.r0, P.r1), P.q);
+            sp = mulmod(sp, sv, P.q, P.r0, P.r1);
+        }
+        out[idx] = v;
+    }
+}
+hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st) {
+    hipLaunchKernelGGL(k_decrypt, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, ct, ncomp, s, out, l);
+    return hipGetLastError();
+}
+
+// exact residue of integral doubles: coef [count][N] -> out [count][l][N] (coefficient form)
+__global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64* out, int l) {
+    const int N = T.N;
+    const size_t total = (size_t)count * l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int n = (int)(idx % N);
+        const size_t rest = idx / N;
+        const int i = (int)(rest % l);
+        const size_t v = rest / l;
+        const PrimeK& P = PK(T, i);
+        const double d = coef[v * N + n];
+        const bool neg = d < 0;
+        const double a = neg ? -d : d;
+        u64 r;
+        if (a < 9.2e18) {
+            r = barrett64((u64)a, P.q, P.r0, P.r1);
+        } else {
+            const u64 bits = (u64)__double_as_longlong(a);
+            const int ex = (int)((bits >> 52) & 0x7FF) - 1075;
+            const u64 mant = (bits & ((1ULL << 52) - 1)) | (1ULL << 52);
+            r = mulmod(barrett64(mant, P.q, P.r0, P.r1), T.pow2[(size_t)i * 1088 + ex], P.q, P.r0, P.r1);
+        }
+        out[idx] = (neg && r) ? P.q - r : r;
+    }
+}
+hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st) {
+    hipLaunchKernelGGL(k_encode_reduce, dim3(eltwise_grid((size_t)count * l * T.N)), dim3(256), 0, st, T, coef, count,
+                       out, l);
+    return hipGetLastError();
+}
+
+}  // namespace fhs

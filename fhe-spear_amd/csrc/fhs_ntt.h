@@ -1,0 +1,129 @@
+// fhs_ntt.h -- negacyclic NTT cores for one RNS limb per workgroup (gfx950).
+//
+// Layout: a limb of N = 2^LOGN uint64 lives in LDS (N + N/16 words, one pad word per 16 to break
+// the power-of-two strides; 136 KiB at N = 16384 -> one workgroup per CU, 16 waves of 64).  The
+// T = N/EPT threads (EPT = 16 elements per thread by default) sweep the stages in passes of up to RL = 3 or 4 stages (radix-8 / radix-16):
+// per pass each thread loads a group of 2^R elements from LDS into registers, runs the R butterfly
+// stages there, and stores the group back.  RL = 4 gives LOGN = 14 as 4+4+4+2 (four LDS sweeps);
+// RL = 3 (3+3+3+3+2) halves the live registers for kernels that keep other state in registers
+// (k_modup_ip holds 32 accumulator words per thread).
+//
+// Transform convention (same as the oracle, oracle/ckks_oracle.c ock_ntt_fwd/inv):
+//   forward  Cooley-Tukey, natural -> bit-reversed:   out[i] = a(psi^(2 rev(i) + 1))
+//   inverse  Gentleman-Sande, bit-reversed -> natural, scaled by N^-1 (folded into stage 0)
+// Twiddles tw[2k] = psi^rev(k) (inverse table: psi^-rev(k)), tw[2k+1] = Shoup companion.
+// Values are Harvey-lazy: forward keeps [0, 4q) (input must be < 4q), inverse keeps [0, 2q).
+#pragma once
+#include "fhs_modarith.h"
+
+namespace fhs {
+
+__device__ __forceinline__ int lds_pad(int e) { return e + (e >> 4); }
+
+__device__ __forceinline__ void ld_tw(const u64* __restrict__ tw, int idx, u64& w, u64& wp) {
+    const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(tw + 2 * idx);
+    w = v.x;
+    wp = v.y;
+}
+
+// One pass over stages [S, S+R) (forward numbering: stage s has m = 2^s blocks, stride N>>(s+1)).
+// Groups: {j0 + k*TL : k < 2^R}, j0 = blk*2*TF + off, off < TL; thread tid owns groups
+// gid = tid + c*T for c < (N/2^R)/T.
+template <int LOGN, int S, int R, bool FWD, int EPT>
+__device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
+                                         u64 s1, u64 s1s) {
+    constexpr int N = 1 << LOGN, T = N / EPT;
+    constexpr int TF = N >> (S + 1);
+    constexpr int TL = TF >> (R - 1);
+    constexpr int GS = 1 << R;
+    constexpr int NG = EPT / GS;
+    const u64 q2 = 2 * q;
+#pragma unroll 1
+    for (int c = 0; c < NG; ++c) {
+        const int gid = tid + c * T;
+        const int blk = gid / TL, off = gid % TL;
+        const int j0 = blk * 2 * TF + off;
+        u64 x[GS];
+#pragma unroll
+        for (int k = 0; k < GS; ++k) x[k] = lds[lds_pad(j0 + k * TL)];
+        if constexpr (FWD) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const int half = GS >> (u + 1);
+#pragma unroll
+                for (int k = 0; k < GS; ++k) {
+                    if (k & half) continue;
+                    u64 w, wp;
+                    ld_tw(tw, (1 << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
+                    u64 X = x[k];
+                    X = X >= q2 ? X - q2 : X;
+                    const u64 t = shoup_lazy(x[k + half], w, wp, q);
+                    x[k] = X + t;
+                    x[k + half] = X - t + q2;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = R - 1; u >= 0; --u) {
+                const int half = GS >> (u + 1);
+#pragma unroll
+                for (int k = 0; k < GS; ++k) {
+                    if (k & half) continue;
+                    const u64 X = x[k], Y = x[k + half];
+                    if (S == 0 && u == 0) {   // last GS stage: fold N^-1 (and any caller scale)
+                        x[k] = shoup_lazy(X + Y, s0, s0s, q);
+                        x[k + half] = shoup_lazy(X - Y + q2, s1, s1s, q);
+                    } else {
+                        u64 w, wp;
+                        ld_tw(tw, (1 << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
+                        const u64 s = X + Y;
+                        x[k] = s >= q2 ? s - q2 : s;
+                        x[k + half] = shoup_lazy(X - Y + q2, w, wp, q);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < GS; ++k) lds[lds_pad(j0 + k * TL)] = x[k];
+    }
+}
+
+template <int LOGN, int RL, int S, int EPT>
+__device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q) {
+    if constexpr (S < LOGN) {
+        constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
+        ntt_pass<LOGN, S, R, true, EPT>(lds, tid, tw, q, 0, 0, 0, 0);
+        __syncthreads();
+        fwd_from<LOGN, RL, S + R, EPT>(lds, tid, tw, q);
+    }
+}
+// inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first
+template <int LOGN, int RL, int S, int EPT>
+__device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
+                                         u64 s1, u64 s1s) {
+    if constexpr (S < LOGN) {
+        constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
+        inv_from<LOGN, RL, S + R, EPT>(lds, tid, tw, q, s0, s0s, s1, s1s);
+        ntt_pass<LOGN, S, R, false, EPT>(lds, tid, tw, q, s0, s0s, s1, s1s);
+        __syncthreads();
+    }
+}
+
+// Forward transform in LDS.  Entry: input (< 4q) at padded natural positions, after a barrier.
+// Exit: bit-reversed-order output in [0, 4q), after a barrier.
+template <int LOGN, int RL = 3, int EPT = 16>
+__device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q) {
+    static_assert(LOGN >= 8 && LOGN <= 14, "LDS-resident NTT supports 256 <= N <= 16384");
+    static_assert(EPT >= 16 && (EPT & (EPT - 1)) == 0, "EPT must be a power of two >= 16");
+    fwd_from<LOGN, RL, 0, EPT>(lds, tid, tw, q);
+}
+// Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
+// per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.
+template <int LOGN, int RL = 3, int EPT = 16>
+__device__ __forceinline__ void ntt_inv_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
+                                            u64 s1, u64 s1s) {
+    static_assert(LOGN >= 8 && LOGN <= 14, "LDS-resident NTT supports 256 <= N <= 16384");
+    inv_from<LOGN, RL, 0, EPT>(lds, tid, tw, q, s0, s0s, s1, s1s);
+}
+
+}  // namespace fhs

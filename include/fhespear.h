@@ -1,0 +1,186 @@
+/*
+ * fhespear.h -- C ABI of libfhespear_hip.so, the MI355X-native CKKS engine behind FHE-SPEAR's
+ * BSGS diagonal matrix-vector path.
+ *
+ * It replaces gpu/phantom_binding.cu (the pybind11 module `pyPhantom`, pb) and the un-vendored
+ * PhantomFHE arithmetic under it.  Each entry point names the reference binding/call site it
+ * stands in for.  The Python module fhe-spear_amd/python/pyPhantom binds these with ctypes
+ * (INTEGRATION.md shows the binding and the fhe_common.py switch).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; objects are opaque handles freed with *_destroy.
+ *  - Every function returns an fhs_status (0 = OK); fhs_last_error() returns a thread-local
+ *    message for the last failure.  FHS_ERR_OOM messages contain "out of memory" (the reference
+ *    string-matches that text, scripts/bootstrap_generation.py:1164-1166).
+ *  - Ciphertexts/plaintexts are device-resident in HBM: [comp][limb][N] uint64, NTT form,
+ *    bit-reversed evaluation order.  chain_index c holds L0 + 1 - c data limbs (pb:144, tf:33).
+ *  - All work is ordered on one HIP stream per context; calls are serialised per context and
+ *    are safe from several host threads (bg:223-249).  Functions that return host data
+ *    synchronise the stream.
+ */
+#ifndef FHESPEAR_H
+#define FHESPEAR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int fhs_status;
+enum {
+    FHS_OK = 0,
+    FHS_ERR_INVALID = 1,      /* bad argument / unsupported parameter */
+    FHS_ERR_OOM = 2,          /* device or host allocation failed ("out of memory") */
+    FHS_ERR_HIP = 3,          /* HIP runtime error */
+    FHS_ERR_LEVEL = 4,        /* operands at different chain indices / no level left */
+    FHS_ERR_SCALE = 5,        /* scale mismatch on add */
+    FHS_ERR_KEY = 6,          /* missing Galois key for a rotation step */
+    FHS_ERR_NODEVICE = 7      /* no HIP device available */
+};
+
+typedef struct fhs_context fhs_context;
+typedef struct fhs_ciphertext fhs_ciphertext;
+typedef struct fhs_plaintext fhs_plaintext;
+typedef struct fhs_secret_key fhs_secret_key;
+typedef struct fhs_public_key fhs_public_key;
+typedef struct fhs_relin_key fhs_relin_key;
+typedef struct fhs_galois_keys fhs_galois_keys;
+
+const char* fhs_last_error(void);
+const char* fhs_version(void);
+int fhs_device_count(void);
+
+/* ---- parameters (pb:78-98) ---- */
+/* pb:81 create_coeff_modulus: SEAL CoeffModulus::Create (largest primes = 1 mod 2N per size) */
+fhs_status fhs_create_coeff_modulus(uint64_t N, const int* bit_sizes, int n, uint64_t* primes_out);
+/* pb:124-126 get_elt_from_step(s): 5^s mod 2N (s<0 -> 5^(N/2-|s|), s=0 -> 2N-1) */
+uint64_t fhs_galois_elt_from_step(int step, uint64_t N);
+
+/* pb:85-98 params + context(params).  primes: key-level list, the last `special` are the
+ * special primes; galois_elts: the set create_galois_keys will generate (NULL/0 = default
+ * power-of-two steps + conjugation, as Phantom does when set_galois_elts is not called). */
+fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int nprimes, int special,
+                              const uint64_t* galois_elts, int n_elts, int device, fhs_context** out);
+fhs_status fhs_context_destroy(fhs_context* ctx);
+fhs_status fhs_context_info(const fhs_context* ctx, uint64_t* N, int* L0, int* P, int* n_elts);
+fhs_status fhs_context_galois_elts(const fhs_context* ctx, uint64_t* elts_out);
+fhs_status fhs_synchronize(fhs_context* ctx);
+/* bytes currently held by the context's device pool (diagnostics) */
+fhs_status fhs_memory_in_use(fhs_context* ctx, uint64_t* bytes);
+
+/* ---- keys (pb:100-124) ---- */
+/* pb:100 secret_key(ctx).  Sampling is deterministic in `seed`. */
+fhs_status fhs_secret_key_create(fhs_context* ctx, uint64_t seed, fhs_secret_key** out);
+fhs_status fhs_secret_key_destroy(fhs_secret_key* sk);
+fhs_status fhs_gen_public_key(fhs_context* ctx, fhs_secret_key* sk, fhs_public_key** out);      /* pb:102 */
+fhs_status fhs_gen_relin_key(fhs_context* ctx, fhs_secret_key* sk, fhs_relin_key** out);        /* pb:103 */
+/* pb:104 create_galois_keys: keys for elts (NULL/0 = the context's set) */
+fhs_status fhs_create_galois_keys(fhs_context* ctx, fhs_secret_key* sk, const uint64_t* elts, int n,
+                                  fhs_galois_keys** out);
+fhs_status fhs_public_key_destroy(fhs_public_key* pk);
+fhs_status fhs_relin_key_destroy(fhs_relin_key* rk);
+fhs_status fhs_galois_keys_destroy(fhs_galois_keys* gk);
+fhs_status fhs_galois_keys_has(const fhs_galois_keys* gk, uint64_t elt, int* has);
+/* export one switching key [dnum][2][L0+P][N] (parity tests) */
+fhs_status fhs_galois_key_export(fhs_context* ctx, const fhs_galois_keys* gk, uint64_t elt, uint64_t* host);
+fhs_status fhs_relin_key_export(fhs_context* ctx, const fhs_relin_key* rk, uint64_t* host);
+fhs_status fhs_secret_key_export(fhs_context* ctx, const fhs_secret_key* sk, uint64_t* host /* [L0+P][N] */);
+fhs_status fhs_public_key_export(fhs_context* ctx, const fhs_public_key* pk, uint64_t* host /* [2][L0][N] */);
+fhs_status fhs_galois_keys_bytes(const fhs_galois_keys* gk, uint64_t* bytes);
+
+/* ---- objects (pb:157-163) ---- */
+fhs_status fhs_ciphertext_destroy(fhs_ciphertext* ct);
+fhs_status fhs_plaintext_destroy(fhs_plaintext* pt);
+fhs_status fhs_ciphertext_info(const fhs_ciphertext* ct, int* ncomp, int* chain_index, int* nlimbs, double* scale);
+fhs_status fhs_ciphertext_set_scale(fhs_ciphertext* ct, double scale);                              /* pb:163 */
+fhs_status fhs_plaintext_info(const fhs_plaintext* pt, int* chain_index, int* nlimbs, double* scale);
+fhs_status fhs_ciphertext_export(fhs_context* ctx, const fhs_ciphertext* ct, uint64_t* host);
+fhs_status fhs_ciphertext_import(fhs_context* ctx, const uint64_t* host, int ncomp, int chain_index, double scale,
+                                 fhs_ciphertext** out);
+fhs_status fhs_plaintext_export(fhs_context* ctx, const fhs_plaintext* pt, uint64_t* host);
+fhs_status fhs_plaintext_import(fhs_context* ctx, const uint64_t* host, int chain_index, double scale,
+                                fhs_plaintext** out);
+/* device pointer of the limb data (zero-copy interop with torch / RCCL) */
+fhs_status fhs_ciphertext_device_ptr(const fhs_ciphertext* ct, void** dptr, uint64_t* bytes);
+
+/* ---- CKKS encoder (pb:128-156) ---- */
+/* values: n complex numbers interleaved (re, im); n <= N/2, zero padded.  pb:141-149 */
+fhs_status fhs_encode(fhs_context* ctx, const double* re_im, size_t n, double scale, int chain_index,
+                      fhs_plaintext** out);
+/* batch: count vectors of n complex values each (bg:382 encode_*_vector_batch) */
+fhs_status fhs_encode_batch(fhs_context* ctx, const double* re_im, size_t count, size_t n, double scale,
+                            int chain_index, fhs_plaintext** out_array);
+/* real-valued fast paths: values are n doubles */
+fhs_status fhs_encode_real(fhs_context* ctx, const double* values, size_t n, double scale, int chain_index,
+                           fhs_plaintext** out);
+fhs_status fhs_encode_real_batch(fhs_context* ctx, const double* values, size_t count, size_t n, double scale,
+                                 int chain_index, fhs_plaintext** out_array);
+/* pb:150-156 decode: writes N/2 complex (re, im) */
+fhs_status fhs_decode(fhs_context* ctx, const fhs_plaintext* pt, double* re_im_out);
+
+/* ---- encryption (pb:105-116) ---- */
+fhs_status fhs_encrypt_symmetric(fhs_context* ctx, fhs_secret_key* sk, const fhs_plaintext* pt, fhs_ciphertext** out);
+fhs_status fhs_encrypt_asymmetric(fhs_context* ctx, fhs_public_key* pk, const fhs_plaintext* pt, fhs_ciphertext** out);
+fhs_status fhs_decrypt(fhs_context* ctx, fhs_secret_key* sk, const fhs_ciphertext* ct, fhs_plaintext** out);
+
+/* ---- evaluator (pb:165-205); every op returns a NEW object ---- */
+fhs_status fhs_add(fhs_context* ctx, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out);       /* pb:167 */
+fhs_status fhs_sub(fhs_context* ctx, const fhs_ciphertext* a, const fhs_ciphertext* b, int negate, fhs_ciphertext** out); /* pb:173 */
+fhs_status fhs_negate(fhs_context* ctx, const fhs_ciphertext* a, fhs_ciphertext** out);                            /* pb:165 */
+fhs_status fhs_add_plain(fhs_context* ctx, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out);  /* pb:169 */
+fhs_status fhs_sub_plain(fhs_context* ctx, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out);  /* pb:175 */
+fhs_status fhs_multiply_plain(fhs_context* ctx, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out); /* pb:181 */
+fhs_status fhs_multiply(fhs_context* ctx, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out);  /* pb:177 */
+fhs_status fhs_relinearize(fhs_context* ctx, const fhs_ciphertext* a, const fhs_relin_key* rk, fhs_ciphertext** out); /* pb:183 */
+fhs_status fhs_rescale_to_next(fhs_context* ctx, const fhs_ciphertext* a, fhs_ciphertext** out);                   /* pb:185 */
+fhs_status fhs_mod_switch_to_next(fhs_context* ctx, const fhs_ciphertext* a, fhs_ciphertext** out);                /* pb:191-193 */
+fhs_status fhs_mod_switch_to(fhs_context* ctx, const fhs_ciphertext* a, int chain_index, fhs_ciphertext** out);    /* pb:198-199 */
+fhs_status fhs_plain_mod_switch_to_next(fhs_context* ctx, const fhs_plaintext* a, fhs_plaintext** out);            /* pb:187-189 */
+fhs_status fhs_plain_mod_switch_to(fhs_context* ctx, const fhs_plaintext* a, int chain_index, fhs_plaintext** out);/* pb:195-196 */
+/* pb:203 rotate: left rotation of the N/2 slots by `step` (bg:219, bg:479) */
+fhs_status fhs_rotate(fhs_context* ctx, const fhs_ciphertext* a, int step, const fhs_galois_keys* gk, fhs_ciphertext** out);
+/* pb:201 apply_galois with an explicit element */
+fhs_status fhs_apply_galois(fhs_context* ctx, const fhs_ciphertext* a, uint64_t elt, const fhs_galois_keys* gk,
+                            fhs_ciphertext** out);
+/* batch of rotations of possibly different inputs: out[i] = rotate(in[i], steps[i]) */
+fhs_status fhs_rotate_many(fhs_context* ctx, const fhs_ciphertext* const* in, const int* steps, int n,
+                           const fhs_galois_keys* gk, fhs_ciphertext** out);
+
+/* ---- fused BSGS (fork-only pyPhantom symbols, bg:459, bg:515) ----
+ * Semantics identical, limb for limb, to the loop scripts/bootstrap_generation.py:464-485:
+ *   out = rescale( sum_g rot_{gG}( sum_{b: gG+b<D} baby[b] (.) pts[gG+b] ) )
+ * baby: G ciphertexts (baby[b] = rot_b(x)); pts: D plaintexts at the baby steps' level. */
+fhs_status fhs_bsgs_multiply_accumulate(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
+                                        const fhs_plaintext* const* pts, int D, int B,
+                                        const fhs_galois_keys* gk, fhs_ciphertext** out);
+/* host staging of pre-encoded diagonals (bg:336-358: offload_plaintexts / upload_plaintexts).
+ * host buffer holds count x nlimbs x N uint64 (pinned when allocated by fhs_host_alloc). */
+fhs_status fhs_offload_plaintexts(fhs_context* ctx, const fhs_plaintext* const* pts, int count, uint64_t* host);
+fhs_status fhs_upload_plaintexts(fhs_context* ctx, const uint64_t* host, int count, int chain_index, double scale,
+                                 fhs_plaintext** out_array);
+/* bg:449 bsgs_from_cpu: streams diagonals from host memory through the BSGS */
+fhs_status fhs_bsgs_from_cpu(fhs_context* ctx, const fhs_ciphertext* const* baby, int G, const uint64_t* host,
+                             int D, int B, int chain_index, double scale, const fhs_galois_keys* gk,
+                             fhs_ciphertext** out);
+fhs_status fhs_host_alloc(uint64_t bytes, void** ptr);   /* pinned host memory */
+fhs_status fhs_host_free(void* ptr);
+
+/* ---- measurement hooks (bench.py) ---- */
+/* fill n plaintexts with i.i.d. uniform limbs mod q_i (SURVEY.md §8d throughput workload) */
+fhs_status fhs_random_plaintexts(fhs_context* ctx, uint64_t seed, int count, int chain_index, double scale,
+                                 fhs_plaintext** out_array);
+/* HIP events on the context stream: record returns an opaque id usable with fhs_event_elapsed */
+fhs_status fhs_event_record(fhs_context* ctx, void** ev);
+fhs_status fhs_event_elapsed(void* start, void* stop, float* ms);
+fhs_status fhs_event_destroy(void* ev);
+/* Device time of one kernel, bracketed by HIP events on the context stream around each launch:
+ * kernel_id 0 = k_bsgs_inner (ct x pt Hadamard-accumulate), 1 = k_modup_ip (ModUp + NTT + key
+ * inner product of every key-switch), -1 = off.  Returns the time/launches accumulated since the
+ * last reset, then arms the timer for kernel_id. */
+fhs_status fhs_kernel_timer(fhs_context* ctx, int kernel_id, float* ms, int* launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,262 @@
+"""GPU parity: libfhespear_hip (through the pyPhantom ctypes shim) vs the CPU oracle, bit-exact on
+limbs, plus the committed golden fixtures produced by the reference's own BSGS orchestration
+(tests/golden/make_golden.py).  Every test here needs an MI355X: -m gpu."""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+
+@pytest.fixture(scope="module")
+def ph(require_gpu):
+    import pyPhantom
+    return pyPhantom
+
+
+def make_ctx(ph, N, L0, P, steps=(), bits=59, seed=99):
+    primes = ph.create_coeff_modulus(N, [bits] * (L0 + P))
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(P)
+    if steps:
+        parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(list(steps), N))))
+    parms.set_coeff_modulus(primes)
+    ctx = ph.context(parms)
+    sk = ph.secret_key(ctx, seed=seed)
+    return ctx, sk, [int(q) for q in primes]
+
+
+def oracle_for(primes, N, P):
+    from oracle.oracle import Oracle
+    return Oracle(N, primes, P)
+
+
+def rand_ct(o, rng, ncomp, l):
+    return np.stack([np.stack([rng.integers(0, o.primes[i], o.N, dtype=np.uint64) for i in range(l)])
+                     for _ in range(ncomp)])
+
+
+def rand_pt(o, rng, l):
+    return np.stack([rng.integers(0, o.primes[i], o.N, dtype=np.uint64) for i in range(l)])
+
+
+PARAMS = [(1024, 6, 3), (2048, 4, 1), (4096, 6, 2)]
+
+
+@pytest.mark.parametrize("N,L0,P", PARAMS)
+def test_keys_and_encryption_match_oracle(ph, N, L0, P):
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=[1, 5, -3], seed=1234)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(1234)
+    assert np.array_equal(sk.export(), s)
+    gk = sk.create_galois_keys(ctx)
+    for st in (1, 5, -3):
+        elt = ph.get_elt_from_step(st, N)
+        assert np.array_equal(gk.export(elt), o.gen_galois_key(1234, s, elt)), f"galois key step {st}"
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(0)
+    pt = ph.plaintext_from_numpy(ctx, rand_pt(o, rng, L0), 1, 2.0 ** 40)
+    ct = sk.encrypt_symmetric(ctx, pt)
+    assert np.array_equal(ct.to_numpy(), o.encrypt_symmetric(1234, 0, s, pt.to_numpy()))
+    pk = sk.gen_publickey(ctx)
+    cta = pk.encrypt_asymmetric(ctx, pt)
+    pk_o = o.gen_public_key(1234, s)
+    assert np.array_equal(cta.to_numpy(), o.encrypt_asymmetric(1234, 1 << 20, pk_o, pt.to_numpy()))
+    # decrypt parity
+    assert np.array_equal(sk.decrypt(ctx, ct).to_numpy(), o.decrypt(s, ct.to_numpy()))
+    del enc
+
+
+@pytest.mark.parametrize("N,L0,P", PARAMS)
+def test_elementwise_ops_match_oracle(ph, N, L0, P):
+    ctx, sk, primes = make_ctx(ph, N, L0, P)
+    o = oracle_for(primes, N, P)
+    rng = np.random.default_rng(N + L0)
+    for l in (L0, max(2, L0 - 1)):
+        ci = L0 + 1 - l
+        a, b = rand_ct(o, rng, 2, l), rand_ct(o, rng, 2, l)
+        p = rand_pt(o, rng, l)
+        A = ph.ciphertext_from_numpy(ctx, a, ci, 2.0 ** 40)
+        Bc = ph.ciphertext_from_numpy(ctx, b, ci, 2.0 ** 40)
+        Pp = ph.plaintext_from_numpy(ctx, p, ci, 2.0 ** 40)
+        assert np.array_equal(ph.add(ctx, A, Bc).to_numpy(), o.add(a, b))
+        assert np.array_equal(ph.sub(ctx, A, Bc).to_numpy(), o.sub(a, b))
+        assert np.array_equal(ph.sub(ctx, A, Bc, True).to_numpy(), o.sub(b, a))
+        assert np.array_equal(ph.negate(ctx, A).to_numpy(), o.negate(a))
+        assert np.array_equal(ph.multiply_plain(ctx, A, Pp).to_numpy(), o.multiply_plain(a, p))
+        assert np.array_equal(ph.add_plain(ctx, A, Pp).to_numpy(), o.add_plain(a, p))
+        m = ph.multiply(ctx, A, Bc)
+        assert m.size() == 3 and np.array_equal(m.to_numpy(), o.multiply(a, b))
+        r = ph.rescale_to_next(ctx, A)
+        assert r.chain_index() == ci + 1 and np.array_equal(r.to_numpy(), o.rescale(a))
+        d = ph.mod_switch_to_next(ctx, A)
+        assert np.array_equal(d.to_numpy(), a[:, :-1])
+        assert ph.multiply_plain(ctx, A, Pp).scale() == 2.0 ** 80
+
+
+@pytest.mark.parametrize("N,L0,P", PARAMS)
+def test_rotate_and_relinearize_match_oracle(ph, N, L0, P):
+    steps = [1, 2, 7, -1]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=77)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(77)
+    gk = sk.create_galois_keys(ctx)
+    rlk = sk.gen_relinkey(ctx)
+    rng = np.random.default_rng(5)
+    for l in (L0, 2):
+        ci = L0 + 1 - l
+        a = rand_ct(o, rng, 2, l)
+        A = ph.ciphertext_from_numpy(ctx, a, ci, 2.0 ** 40)
+        # several rotations queued back to back -> one batched key-switch launch
+        outs = [ph.rotate(ctx, A, st, gk) for st in steps]
+        for st, out in zip(steps, outs):
+            want = o.rotate_elt(a, o.gen_galois_key(77, s, ph.get_elt_from_step(st, N)), ph.get_elt_from_step(st, N))
+            assert np.array_equal(out.to_numpy(), want), f"rotate step {st} at l={l}"
+        c3 = rand_ct(o, rng, 3, l)
+        C3 = ph.ciphertext_from_numpy(ctx, c3, ci, 2.0 ** 40)
+        assert np.array_equal(ph.relinearize(ctx, C3, rlk).to_numpy(), o.relinearize(c3, o.gen_relin_key(77, s)))
+
+
+def test_encode_decode_and_rotation_semantics(ph):
+    N, L0, P = 2048, 6, 3
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=[1, 3, -2])
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(3)
+    x = rng.normal(0, 1, N // 2)
+    pt = enc.encode_double_vector(ctx, x, 2.0 ** 40)
+    assert np.max(np.abs(np.array(enc.decode_double_vector(ctx, pt)) - x)) < 1e-6
+    z = rng.normal(0, 1, N // 2) + 1j * rng.normal(0, 1, N // 2)
+    ptc = enc.encode_complex_vector(ctx, z, 2.0 ** 40)
+    assert np.max(np.abs(np.array(enc.decode_complex_vector(ctx, ptc)) - z)) < 1e-6
+    # oracle encoder agrees to within rounding of the f64 FFT
+    o = oracle_for(primes, N, P)
+    dec_o = o.decode(pt.to_numpy(), 2.0 ** 40).real
+    assert np.max(np.abs(dec_o - x)) < 1e-6
+    gk = sk.create_galois_keys(ctx)
+    ct = sk.encrypt_symmetric(ctx, pt)
+    for st in (1, 3, -2):
+        r = ph.rotate(ctx, ct, st, gk)
+        d = np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, r)))
+        assert np.max(np.abs(d - np.roll(x, -st))) < 1e-5, st   # left rotation, pb:203
+    # batch encode == single encode
+    mats = rng.normal(0, 0.1, (3, N // 2))
+    batch = enc.encode_double_vector_batch(ctx, mats, 2.0 ** 40, chain_index=2)
+    for i in range(3):
+        assert batch[i].chain_index() == 2
+        assert np.array_equal(batch[i].to_numpy(), enc.encode_double_vector(ctx, mats[i], 2.0 ** 40, 2).to_numpy())
+
+
+def _load_golden(name):
+    man = json.loads((GOLDEN / "manifest.json").read_text())
+    return man["cases"][name], np.load(GOLDEN / man["cases"][name]["file"])
+
+
+@pytest.mark.parametrize("case", ["bsgs_real_n512", "bsgs_complex_n512", "bsgs_real_n1024_p1"])
+def test_bsgs_fused_matches_reference_loop_golden(ph, case):
+    """Golden fixture = reference bg:464-485 loop executed on the oracle; the fused GPU op must
+    reproduce its output limbs exactly from the same baby steps, diagonals and keys."""
+    meta, z = _load_golden(case)
+    N, L0, P, D, G, B = (meta[k] for k in ("N", "L0", "P", "D", "G", "B"))
+    primes = [int(q) for q in z["primes"]]
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(P)
+    parms.set_galois_elts(meta["giant_elts"])
+    parms.set_coeff_modulus(primes)
+    ctx = ph.context(parms)
+    sk = ph.secret_key(ctx, seed=meta["sk_seed"])
+    gk = sk.create_galois_keys(ctx)
+    import hashlib
+    for elt, digest in meta["giant_key_sha256"].items():
+        assert hashlib.sha256(gk.export(int(elt)).tobytes()).hexdigest() == digest
+    ci = meta["chain_index_in"]
+    baby = [ph.ciphertext_from_numpy(ctx, z["baby"][b], ci, meta["scale"]) for b in range(G)]
+    pts = [ph.plaintext_from_numpy(ctx, z["pts"][k], ci, meta["diag_scale"]) for k in range(D)]
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    assert y.chain_index() == meta["chain_index_out"]
+    assert np.isclose(y.scale(), meta["scale_out"], rtol=1e-12)
+    assert np.array_equal(y.to_numpy(), z["out"])
+    # streamed-from-host variant (bg:449) is the same computation
+    data, cci, sc, cms, pmd = ph.offload_plaintexts(pts)
+    y2 = ph.bsgs_from_cpu(ctx, baby, data, cci, sc, cms, pmd, G, B, D, gk)
+    assert np.array_equal(y2.to_numpy(), z["out"])
+    up = ph.upload_plaintexts(data, cci, sc, cms, pmd)
+    assert np.array_equal(up[3].to_numpy(), z["pts"][3])
+
+
+def test_bsgs_fused_equals_op_by_op_loop(ph):
+    """Fused bsgs_multiply_accumulate == the bg:464-485 loop issued op by op through pyPhantom."""
+    N, L0, P, D = 2048, 6, 3, 64
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=5)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(8)
+    x = rng.normal(0, 0.1, D)
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), 2.0 ** 59))
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    pts = ph.random_plaintexts(ctx, 3, D, ct.chain_index(), 2.0 ** 59)
+    res = None
+    for g in range(B):
+        inner = None
+        for b in range(G):
+            k = g * G + b
+            if k >= D:
+                continue
+            term = ph.multiply_plain(ctx, baby[b], pts[k])
+            inner = term if inner is None else ph.add(ctx, inner, term)
+        if g > 0:
+            inner = ph.rotate(ctx, inner, g * G, gk)
+        res = inner if res is None else ph.add(ctx, res, inner)
+    res = ph.rescale_to_next(ctx, res)
+    fused = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    assert np.array_equal(fused.to_numpy(), res.to_numpy())
+
+
+def test_bsgs_decrypts_to_matvec(ph):
+    """Accuracy contract of tf:272-298 (corr > 0.999) on the reference's diagonal layout."""
+    import __graft_entry__ as ge
+    N, L0, P, D = 4096, 6, 3, 128
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(42)
+    x = rng.normal(0, 0.1, D)
+    W = rng.normal(0, 0.02, (D, D))
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), 2.0 ** 59))
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    pts = enc.encode_double_vector_batch(ctx, ge._rolled_diagonals(W, D, G, N // 2), 2.0 ** 59,
+                                         chain_index=ct.chain_index())
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    dec = np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, y)))[:D]
+    ref = W @ x
+    assert np.corrcoef(dec, ref)[0, 1] > 0.999999
+    assert np.max(np.abs(dec - ref)) < 1e-8
+
+
+def test_errors(ph):
+    ctx, sk, primes = make_ctx(ph, 1024, 6, 3, steps=[1])
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, [1.0], 2.0 ** 40))
+    with pytest.raises(ValueError):
+        ph.rotate(ctx, ct, 2, gk)      # no key for step 2
+    low = ph.mod_switch_to_next(ctx, ct)
+    with pytest.raises(ValueError):
+        ph.add(ctx, ct, low)           # chain index mismatch
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(1024)
+    parms.set_special_modulus_size(3)
+    parms.set_coeff_modulus(ph.create_coeff_modulus(1024, [59] * 8))   # L0 = 5, not a multiple of 3
+    with pytest.raises(ValueError):
+        ph.context(parms)
