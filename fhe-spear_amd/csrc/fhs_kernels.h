@@ -34,6 +34,15 @@ struct KsItem {
     u64 pad;
 };
 
+// Optional per-kernel event timer (bench.py): rec(ctx, id, begin, stream) is called around launches.
+enum KernelId { KID_BSGS_INNER = 0, KID_MODUP = 1, KID_KS_IP = 2, KID_MODDOWN = 3, KID_KS_INTT = 4, KID_SPECIAL_INTT = 5,
+                KID_GIANT_SUM = 6, KID_GIANT_FINAL = 7, KID_RESCALE = 8, KID_COUNT = 9 };
+struct KTimer {
+    void* ctx;
+    void (*rec)(void* ctx, int id, int begin, hipStream_t st);
+};
+#define FHS_TMARK(tm, id, b, st) do { if (tm) (tm)->rec((tm)->ctx, (id), (b), (st)); } while (0)
+
 // all launchers enqueue on `st` and return hipSuccess or the first launch error
 hipError_t launch_ntt_fwd(const DevTables& T, u64* data, int limbs, int l_split, int npoly, size_t poly_stride,
                           hipStream_t st);
@@ -43,16 +52,16 @@ hipError_t launch_eltwise(const DevTables& T, int op, const u64* a, const u64* b
                           size_t a_cstride, size_t b_cstride, hipStream_t st);
 hipError_t launch_tensor(const DevTables& T, const u64* a, const u64* b, u64* out3, int l, hipStream_t st);
 hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
-                          hipStream_t st);
+                          hipStream_t st, const KTimer* tm = nullptr);
 hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, int l, u64* workspace,
-                            size_t ws_bytes, void* items_dev, hipStream_t st, hipEvent_t* timer_ev);
+                            size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm);
 size_t keyswitch_workspace_bytes(const DevTables& T, int R, int l);
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
-                             int D, int l, u64* inner, hipStream_t st);
+                             int D, int l, u64* inner, hipStream_t st, const KTimer* tm);
 // giant-step key-switches of inner[1..B-1] (rotation by g*G), summed with inner[0]; output 2 x l limbs
 hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
                              u64* out, u64* workspace, size_t ws_bytes, void* items_dev, hipStream_t st,
-                             hipEvent_t* timer_ev);
+                             const KTimer* tm);
 size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l);
 hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,

@@ -244,13 +244,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_ntt(DevTables T, c
     }
 }
 hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
-                          hipStream_t st) {
+                          hipStream_t st, const KTimer* tm) {
+    FHS_TMARK(tm, KID_RESCALE, 1, st);
     FHS_DISPATCH_LOGN(T.logN, {
         hipLaunchKernelGGL((k_rescale_intt<LOGN>), dim3(ncomp), dim3((1 << LOGN) / 16), 0, st, T,
                            in, scratch, l);
         hipLaunchKernelGGL((k_rescale_ntt<LOGN>), dim3(l - 1, ncomp), dim3((1 << LOGN) / 16), 0, st,
                            T, in, scratch, out, l);
     });
+    FHS_TMARK(tm, KID_RESCALE, 0, st);
     return hipGetLastError();
 }
 
@@ -407,34 +409,42 @@ size_t keyswitch_workspace_bytes(const DevTables& T, int R, int l) {
 
 // ModUp + key inner product for R items; leaves acc [R][2][E][N] and ycoef [R][2][P][N]
 template <int LOGN>
-static void ks_front(const DevTables& T, const KsItem* it, int R, int l, u64* ws, hipStream_t st,
-                     hipEvent_t* timer_ev, u64** acc_out, u64** ycoef_out) {
+static void ks_front(const DevTables& T, const KsItem* it, int R, int l, u64* ws, hipStream_t st, const KTimer* tm,
+                     u64** acc_out, u64** ycoef_out) {
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     u64* acoef = ws;
     u64* ext = acoef + (size_t)R * l * N;
     u64* acc = ext + (size_t)R * dn * E * N;
     u64* ycoef = acc + (size_t)R * 2 * E * N;
     const dim3 blk((1 << LOGN) / 16);
+    FHS_TMARK(tm, KID_KS_INTT, 1, st);
     hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l, R), blk, 0, st, T, it, acoef, l);
-    if (timer_ev) hipEventRecord(timer_ev[0], st);
+    FHS_TMARK(tm, KID_KS_INTT, 0, st);
+    FHS_TMARK(tm, KID_MODUP, 1, st);
     hipLaunchKernelGGL((k_modup<LOGN>), dim3(E, dn, R), blk, 0, st, T, acoef, ext, l);
-    if (timer_ev) hipEventRecord(timer_ev[1], st);
+    FHS_TMARK(tm, KID_MODUP, 0, st);
+    FHS_TMARK(tm, KID_KS_IP, 1, st);
     hipLaunchKernelGGL(k_ks_ip, dim3(eltwise_grid((size_t)R * E * N)), dim3(256), 0, st, T, it, ext, acc, l, R);
+    FHS_TMARK(tm, KID_KS_IP, 0, st);
+    FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
     hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), blk, 0, st, T, acc, ycoef, l, R);
+    FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
     *acc_out = acc;
     *ycoef_out = ycoef;
 }
 
 hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, int l, u64* ws, size_t ws_bytes,
-                            void* items_dev, hipStream_t st, hipEvent_t* timer_ev) {
+                            void* items_dev, hipStream_t st, const KTimer* tm) {
     if (keyswitch_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
     hipError_t e = hipMemcpyAsync(items_dev, items_host, sizeof(KsItem) * R, hipMemcpyHostToDevice, st);
     if (e != hipSuccess) return e;
     const KsItem* it = reinterpret_cast<const KsItem*>(items_dev);
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
-        ks_front<LOGN>(T, it, R, l, ws, st, timer_ev, &acc, &ycoef);
+        ks_front<LOGN>(T, it, R, l, ws, st, tm, &acc, &ycoef);
+        FHS_TMARK(tm, KID_MODDOWN, 1, st);
         hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l, 2, R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
+        FHS_TMARK(tm, KID_MODDOWN, 0, st);
     });
     return hipGetLastError();
 }
@@ -465,23 +475,24 @@ __global__ void __launch_bounds__(256) k_bsgs_inner(DevTables T, const u64* cons
         u128 c0 = {0, 0}, c1 = {0, 0};
         const u64* const* pg = pts + (size_t)g * G;
         int b = 0;
-        for (; b + 4 <= bmax; b += 4) {
-            const u64 p0 = pg[b][off], p1 = pg[b + 1][off], p2 = pg[b + 2][off], p3 = pg[b + 3][off];
-            mac128(c0, sb[(b * 2 + 0) * 64 + lane], p0);
-            mac128(c1, sb[(b * 2 + 1) * 64 + lane], p0);
-            mac128(c0, sb[(b * 2 + 2) * 64 + lane], p1);
-            mac128(c1, sb[(b * 2 + 3) * 64 + lane], p1);
-            mac128(c0, sb[(b * 2 + 4) * 64 + lane], p2);
-            mac128(c1, sb[(b * 2 + 5) * 64 + lane], p2);
-            mac128(c0, sb[(b * 2 + 6) * 64 + lane], p3);
-            mac128(c1, sb[(b * 2 + 7) * 64 + lane], p3);
-            if ((b & 31) == 28) {   // keep the lazy sum < 2^128 for any prime < 2^61
+        // 8 diagonal loads in flight per wave-iteration; lazy sums reduced every 32 products so
+        // they stay < 2^128 for any prime < 2^61
+        for (; b + 8 <= bmax; b += 8) {
+            if (b && (b & 31) == 0) {
                 c0.lo = barrett128(c0.lo, c0.hi, q, P.r0, P.r1); c0.hi = 0;
                 c1.lo = barrett128(c1.lo, c1.hi, q, P.r0, P.r1); c1.hi = 0;
             }
+            u64 p[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) p[u] = __builtin_nontemporal_load(pg[b + u] + off);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                mac128(c0, sb[((b + u) * 2 + 0) * 64 + lane], p[u]);
+                mac128(c1, sb[((b + u) * 2 + 1) * 64 + lane], p[u]);
+            }
         }
         for (; b < bmax; ++b) {
-            const u64 p = pg[b][off];
+            const u64 p = __builtin_nontemporal_load(pg[b] + off);
             mac128(c0, sb[(b * 2 + 0) * 64 + lane], p);
             mac128(c1, sb[(b * 2 + 1) * 64 + lane], p);
         }
@@ -490,10 +501,12 @@ __global__ void __launch_bounds__(256) k_bsgs_inner(DevTables T, const u64* cons
     }
 }
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
-                             int D, int l, u64* inner, hipStream_t st) {
-    if (T.N % 64) return hipErrorInvalidValue;
+                             int D, int l, u64* inner, hipStream_t st, const KTimer* tm) {
+    if (T.N % 64 || G > 64) return hipErrorInvalidValue;
     const size_t sh = (size_t)G * 128 * 8;
+    FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
     hipLaunchKernelGGL(k_bsgs_inner, dim3(T.N / 64, l), dim3(256), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
+    FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
     return hipGetLastError();
 }
 
@@ -557,7 +570,7 @@ size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
 }
 
 hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
-                             u64* out, u64* ws, size_t ws_bytes, void* items_dev, hipStream_t st, hipEvent_t* timer_ev) {
+                             u64* out, u64* ws, size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm) {
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
     if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
@@ -577,10 +590,14 @@ hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B,
     const KsItem* it = reinterpret_cast<const KsItem*>(items_dev);
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
-        ks_front<LOGN>(T, it, R, l, ws, st, timer_ev, &acc, &ycoef);
+        ks_front<LOGN>(T, it, R, l, ws, st, tm, &acc, &ycoef);
+        FHS_TMARK(tm, KID_GIANT_SUM, 1, st);
         hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, st, T, it, acc, ycoef, inner, base,
                            convsum, l, R);
+        FHS_TMARK(tm, KID_GIANT_SUM, 0, st);
+        FHS_TMARK(tm, KID_GIANT_FINAL, 1, st);
         hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3((1 << LOGN) / 16), 0, st, T, base, convsum, out, l);
+        FHS_TMARK(tm, KID_GIANT_FINAL, 0, st);
     });
     return hipGetLastError();
 }

@@ -122,6 +122,9 @@ _SIGS = {
     "fhs_event_elapsed": (C.c_int, [_vp, _vp, C.POINTER(C.c_float)]),
     "fhs_event_destroy": (C.c_int, [_vp]),
     "fhs_kernel_timer": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_float), _ip, C.c_int]),
+    "fhs_kernel_timer_arm": (C.c_int, [_vp, C.c_uint32]),
+    "fhs_ciphertext_copy_to_device": (C.c_int, [_vp, _vp, _vp]),
+    "fhs_ciphertext_from_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
 }
 for _name, (_res, _args) in _SIGS.items():
     _f = getattr(_lib, _name)
@@ -720,12 +723,40 @@ class Event:
             self._h = None
 
 
-def kernel_timer(ctx, kernel_id=-1, reset=True):
-    """Arm the per-kernel HIP-event timer (0 = k_bsgs_inner, 1 = k_modup, -1 = off); returns
-    (ms, launches) accumulated since the previous call."""
-    ms, n = C.c_float(), C.c_int()
-    _check(_lib.fhs_kernel_timer(ctx._h, int(kernel_id), C.byref(ms), C.byref(n), 1 if reset else 0), "kernel_timer")
-    return float(ms.value), int(n.value)
+KERNEL_IDS = {"k_bsgs_inner": 0, "k_modup": 1, "k_ks_ip": 2, "k_moddown": 3, "k_ks_intt": 4,
+              "k_ks_special_intt": 5, "k_giant_sum": 6, "k_giant_final": 7, "rescale": 8}
+
+
+def kernel_timer_arm(ctx, names=None):
+    """Record HIP events around every launch of the named kernels (None = all, [] = off)."""
+    ids = KERNEL_IDS.values() if names is None else [KERNEL_IDS[n] for n in names]
+    mask = 0
+    for i in ids:
+        mask |= 1 << i
+    _check(_lib.fhs_kernel_timer_arm(ctx._h, mask), "kernel_timer_arm")
+
+
+def kernel_timer_read(ctx, reset=False):
+    """{kernel: (ms, launches)} accumulated since the last reset."""
+    out = {}
+    for name, kid in KERNEL_IDS.items():
+        ms, n = C.c_float(), C.c_int()
+        _check(_lib.fhs_kernel_timer(ctx._h, kid, C.byref(ms), C.byref(n), 0), "kernel_timer")
+        out[name] = (float(ms.value), int(n.value))
+    if reset:
+        _check(_lib.fhs_kernel_timer(ctx._h, -1, None, None, 1), "kernel_timer")
+    return out
+
+
+def ciphertext_copy_to_device(ctx, ct, dst_ptr):
+    _check(_lib.fhs_ciphertext_copy_to_device(ctx._h, ct._h, _vp(int(dst_ptr))), "copy_to_device")
+
+
+def ciphertext_from_device(ctx, src_ptr, ncomp, chain_index, scale):
+    h = _vp()
+    _check(_lib.fhs_ciphertext_from_device(ctx._h, _vp(int(src_ptr)), int(ncomp), int(chain_index), float(scale),
+                                           C.byref(h)), "from_device")
+    return ciphertext(ctx, h)
 
 
 def device_count():

@@ -174,11 +174,17 @@ fhs_status fhs_random_plaintexts(fhs_context* ctx, uint64_t seed, int count, int
 fhs_status fhs_event_record(fhs_context* ctx, void** ev);
 fhs_status fhs_event_elapsed(void* start, void* stop, float* ms);
 fhs_status fhs_event_destroy(void* ev);
-/* Device time of one kernel, bracketed by HIP events on the context stream around each launch:
- * kernel_id 0 = k_bsgs_inner (ct x pt Hadamard-accumulate), 1 = k_modup_ip (ModUp + NTT + key
- * inner product of every key-switch), -1 = off.  Returns the time/launches accumulated since the
- * last reset, then arms the timer for kernel_id. */
+/* Per-kernel device time from HIP events recorded on the context stream around each launch.
+ * Kernel ids: 0 k_bsgs_inner (ct x pt Hadamard-accumulate), 1 k_modup (ModUp + NTT), 2 k_ks_ip
+ * (key inner product), 3 k_moddown, 4 k_ks_intt, 5 k_ks_special_intt, 6 k_giant_sum,
+ * 7 k_giant_final, 8 rescale.  arm(mask) enables ids (bit i); timer() reports kernel_id's
+ * accumulated ms / launch count and optionally resets every accumulator. */
+fhs_status fhs_kernel_timer_arm(fhs_context* ctx, uint32_t mask);
 fhs_status fhs_kernel_timer(fhs_context* ctx, int kernel_id, float* ms, int* launches, int reset);
+/* device-to-device copies of ciphertext limbs to / from caller-owned HBM (RCCL gather in bench.py) */
+fhs_status fhs_ciphertext_copy_to_device(fhs_context* ctx, const fhs_ciphertext* ct, void* dst);
+fhs_status fhs_ciphertext_from_device(fhs_context* ctx, const void* src, int ncomp, int chain_index, double scale,
+                                      fhs_ciphertext** out);
 
 #ifdef __cplusplus
 }
