@@ -123,14 +123,14 @@ def main():
         import torch
         out_words = 2 * (L0 - 1) * N
         gather_buf = torch.empty(out_words, dtype=torch.int64, device=f"cuda:{local}")
-        gather_list = [torch.empty_like(gather_buf) for _ in range(world)] if rank == 0 else None
+        import fhespear_dist
 
     def step():
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
         if dist is not None:     # cfg4: output ciphertexts to rank 0 over RCCL (xGMI)
             ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
-            dist.gather(gather_buf, gather_list, dst=0)
+            fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
         return y
 
     for _ in range(args.warmup):
