@@ -13,6 +13,17 @@
 #include "fhs_kernels.h"
 #include "fhs_ntt.h"
 
+// build-time tuning knobs (A/B variants are built with -D...; defaults are the shipped choice)
+#ifndef FHS_INNER_WAVES
+#define FHS_INNER_WAVES 8      // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
+#endif
+#ifndef FHS_MODUP_RL
+#define FHS_MODUP_RL 3         // radix (log2) of the register passes in k_modup's NTT
+#endif
+#ifndef FHS_NTT_RL
+#define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
+#endif
+
 namespace fhs {
 
 #define FHS_DISPATCH_LOGN(logN, ...)                   \
@@ -57,7 +68,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_fwd(DevTables T, u64* 
 #pragma unroll
     for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = p[tid + k * TH];
     __syncthreads();
-    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)pi * N * 2, q);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)pi * N * 2, q);
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
@@ -77,7 +88,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_inv(DevTables T, u64* 
 #pragma unroll
     for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = p[tid + c * TH];
     __syncthreads();
-    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
+    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
 #pragma unroll
     for (int k = 0; k < 16; ++k) p[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
 }
@@ -213,7 +224,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_intt(DevTables T, 
 #pragma unroll
     for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[tid + c * TH];
     __syncthreads();
-    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
+    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
     const u64 half = P.q >> 1;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -233,7 +244,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_ntt(DevTables T, c
 #pragma unroll
     for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = submod(barrett64(src[tid + k * TH], P.q, P.r0, P.r1), hq, P.q);
     __syncthreads();
-    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
     const u64* a = in + ((size_t)comp * l + i) * N;
     u64* o = out + ((size_t)comp * (l - 1) + i) * N;
 #pragma unroll
@@ -273,7 +284,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const
     }
     __syncthreads();
     const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
-    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)i * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
+    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)i * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
     u64* dst = acoef + ((size_t)r * l + i) * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
@@ -307,7 +318,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
         lds[lds_pad(e)] = barrett128(s.lo, s.hi, m, PM.r0, PM.r1);
     }
     __syncthreads();
-    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m);
+    ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m);
     u64* o = ext + (((size_t)r * dn + j) * E + t) * N;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -359,7 +370,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_special_intt(DevTables 
     }
     __syncthreads();
     const u64* cst = T.md_intt + (size_t)k * 4;
-    ntt_inv_lds<LOGN>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
+    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
     u64* dst = ycoef + (((size_t)r * 2 + comp) * P_ + k) * N;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) dst[tid + kk * TH] = csub(lds[lds_pad(tid + kk * TH)], P.q);
@@ -385,7 +396,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
         lds[lds_pad(e)] = barrett128(s.lo, s.hi, q, P.r0, P.r1);
     }
     __syncthreads();
-    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)i * N * 2, q);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, q);
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
     const u64* add = comp == 0 ? it.add0 : it.add1;
     const u64 aelt = comp == 0 ? it.elt : 1;
@@ -454,14 +465,14 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
 // Block = 4 waves sharing one 64-coefficient slice of limb i: the slice of all G baby steps
 // (both components) is staged once in LDS, each wave then streams the diagonals of its giant
 // groups (g = wave, wave+4, ...) from HBM with lazy 128-bit accumulation.
-__global__ void __launch_bounds__(256) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
+__global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
                                                     const u64* const* __restrict__ pts, int G, int B, int D, int l,
                                                     u64* __restrict__ inner) {
     extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][64]
     const int N = T.N;
     const int i = blockIdx.y, n0 = blockIdx.x * 64, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t S = (size_t)l * N;
-    for (int idx = tid; idx < G * 128; idx += 256) {
+    for (int idx = tid; idx < G * 128; idx += 64 * FHS_INNER_WAVES) {
         const int b = idx >> 7, comp = (idx >> 6) & 1, c = idx & 63;
         sb[idx] = baby[b][comp * S + (size_t)i * N + n0 + c];
     }
@@ -469,7 +480,7 @@ __global__ void __launch_bounds__(256) k_bsgs_inner(DevTables T, const u64* cons
     const PrimeK& P = PK(T, i);
     const u64 q = P.q;
     const size_t off = (size_t)i * N + n0 + lane;
-    for (int g = wave; g < B; g += 4) {
+    for (int g = wave; g < B; g += FHS_INNER_WAVES) {
         const int bmax = min(G, D - g * G);
         if (bmax <= 0) continue;
         u128 c0 = {0, 0}, c1 = {0, 0};
@@ -505,7 +516,7 @@ hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, con
     if (T.N % 64 || G > 64) return hipErrorInvalidValue;
     const size_t sh = (size_t)G * 128 * 8;
     FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-    hipLaunchKernelGGL(k_bsgs_inner, dim3(T.N / 64, l), dim3(256), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
+    hipLaunchKernelGGL(k_bsgs_inner, dim3(T.N / 64, l), dim3(64 * FHS_INNER_WAVES), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
     FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
     return hipGetLastError();
 }
@@ -555,7 +566,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_giant_final(DevTables T, c
 #pragma unroll
     for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = convsum[off + tid + k * TH];
     __syncthreads();
-    ntt_fwd_lds<LOGN>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
