@@ -269,19 +269,28 @@ static size_t pt_bytes(const fhs_plaintext* pt) { return 8ull * pt->l * pt->ctx-
 static fhs_status flush(fhs_context* c) {
     if (c->pending.empty()) return FHS_OK;
     const int R = (int)c->pending.size(), l = c->pending_l;
+    // distinct inputs: rotations of the same ciphertext share one (hoisted) ModUp
     std::vector<KsItem> items(R);
-    for (int r = 0; r < R; ++r) items[r] = c->pending[r].item;
-    const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, l);
+    std::vector<const uint64_t*> uniq;
+    std::map<const uint64_t*, int> idx;
+    for (int r = 0; r < R; ++r) {
+        items[r] = c->pending[r].item;
+        auto ins = idx.emplace(items[r].a, (int)uniq.size());
+        if (ins.second) uniq.push_back(items[r].a);
+        items[r].src = (uint64_t)ins.first->second;
+    }
+    const int U = (int)uniq.size();
+    const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, U, l);
     uint64_t* ws = nullptr;
     hipError_t e = dalloc(c, &ws, wsb);
     if (e != hipSuccess) return hip_fail(e, "key-switch workspace");
-    e = fhs::launch_keyswitch(c->T, items.data(), R, l, ws, wsb, c->items_dev, c->st, c->timer_mask ? &c->ktimer : nullptr);
+    e = fhs::launch_keyswitch(c->T, items.data(), R, reinterpret_cast<const fhs::u64* const*>(uniq.data()), U, l, ws,
+                              wsb, c->items_dev, c->st, c->timer_mask ? &c->ktimer : nullptr);
     dfree(c, ws, wsb);
     c->pending.clear();
     c->pending_refs.clear();
     c->pending_outs.clear();
     c->pending_l = -1;
-    // the items buffer is reused by the next launch: keep host/device ordered
     if (e != hipSuccess) return hip_fail(e, "key-switch launch");
     return FHS_OK;
 }
@@ -404,6 +413,26 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
             }
         }
     }
+    // ---- centred-extension tables: floor(2^128/q_u) per digit source, Q_S and ns Q_S mod every prime
+    std::vector<uint64_t> mu_R((size_t)(L0 + 1) * dnum * P * 2, 0), mu_Q((size_t)(L0 + 1) * dnum * K * 2, 0);
+    for (int l = 1; l <= L0; ++l) {
+        const int dn = (l + P - 1) / P;
+        for (int j = 0; j < dn; ++j) {
+            const int s0 = j * P, s1 = std::min(s0 + P, l), ns = s1 - s0;
+            for (int u = 0; u < ns; ++u) {
+                const hu128 R = (~(hu128)0) / primes[s0 + u];
+                mu_R[(((size_t)l * dnum + j) * P + u) * 2 + 0] = (uint64_t)R;
+                mu_R[(((size_t)l * dnum + j) * P + u) * 2 + 1] = (uint64_t)(R >> 64);
+            }
+            for (int t = 0; t < K; ++t) {
+                const uint64_t m = primes[t];
+                uint64_t Qm = 1;
+                for (int u = 0; u < ns; ++u) Qm = h_mulmod(Qm, primes[s0 + u] % m, m);
+                mu_Q[(((size_t)l * dnum + j) * K + t) * 2 + 0] = Qm;
+                mu_Q[(((size_t)l * dnum + j) * K + t) * 2 + 1] = h_mulmod(Qm, (uint64_t)ns, m);
+            }
+        }
+    }
     // ---- ModDown tables
     std::vector<uint64_t> md_intt((size_t)P * 4), md_hat((size_t)P * L0), md_pinv((size_t)3 * L0);
     for (int k = 0; k < P; ++k) {
@@ -469,12 +498,14 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");
     HIPCHK(up(mu_intt.data(), 8 * mu_intt.size(), (const void**)&T.modup_intt), "tables");
     HIPCHK(up(mu_hat.data(), 8 * mu_hat.size(), (const void**)&T.modup_hat), "tables");
+    HIPCHK(up(mu_R.data(), 8 * mu_R.size(), (const void**)&T.modup_R), "tables");
+    HIPCHK(up(mu_Q.data(), 8 * mu_Q.size(), (const void**)&T.modup_Q), "tables");
     HIPCHK(up(md_intt.data(), 8 * md_intt.size(), (const void**)&T.md_intt), "tables");
     HIPCHK(up(md_hat.data(), 8 * md_hat.size(), (const void**)&T.md_hat), "tables");
     HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
     HIPCHK(up(rs.data(), 8 * rs.size(), (const void**)&T.rescale), "tables");
     HIPCHK(up(pow2.data(), 8 * pow2.size(), (const void**)&T.pow2), "tables");
-    HIPCHK(hipMalloc(&c->items_dev, sizeof(KsItem) * fhs_context::kMaxItems), "items buffer");
+    HIPCHK(hipMalloc(&c->items_dev, (sizeof(KsItem) + sizeof(void*)) * fhs_context::kMaxItems), "items buffer");
     c->tables.push_back(c->items_dev);
     HIPCHK(hipMalloc(&c->ptrs_dev, sizeof(void*) * 2 * fhs_context::kMaxPtrs), "pointer buffer");
     c->tables.push_back(c->ptrs_dev);
@@ -1164,10 +1195,16 @@ extern "C" fhs_status fhs_multiply(fhs_context* c, const fhs_ciphertext* a, cons
 
 static fhs_status run_keyswitch(fhs_context* c, std::vector<KsItem>& items, int l) {
     const int R = (int)items.size();
-    const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, l);
+    std::vector<const uint64_t*> uniq;
+    for (int r = 0; r < R; ++r) {
+        items[r].src = (uint64_t)uniq.size();
+        uniq.push_back(items[r].a);
+    }
+    const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, R, l);
     uint64_t* ws = nullptr;
     HIPCHK(dalloc(c, &ws, wsb), "key-switch workspace");
-    hipError_t e = fhs::launch_keyswitch(c->T, items.data(), R, l, ws, wsb, c->items_dev, c->st, nullptr);
+    hipError_t e = fhs::launch_keyswitch(c->T, items.data(), R, reinterpret_cast<const fhs::u64* const*>(uniq.data()), R,
+                                         l, ws, wsb, c->items_dev, c->st, nullptr);
     dfree(c, ws, wsb);
     if (e != hipSuccess) return hip_fail(e, "key-switch");
     return FHS_OK;

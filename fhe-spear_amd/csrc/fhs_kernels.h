@@ -14,6 +14,8 @@ struct DevTables {
     const u64* tw_inv;        // [K][N][2]  psi^-rev(k), Shoup
     const u64* modup_intt;    // [L0+1][L0][4]  INTT stage-0 constants with inv_hat folded in
     const u64* modup_hat;     // [L0+1][dnum][P][K]  (Q_S / q_u) mod prime(t)
+    const u64* modup_R;       // [L0+1][dnum][P][2]  floor(2^128 / q_u) (centred-extension count)
+    const u64* modup_Q;       // [L0+1][dnum][K][2]  Q_S mod prime(t), ns*Q_S mod prime(t)
     const u64* md_intt;       // [P][4]  INTT constants with inv(P/p_k) folded in
     const u64* md_hat;        // [P][L0]  (P / p_k) mod q_i
     const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup
@@ -22,16 +24,19 @@ struct DevTables {
     int N, logN, L0, P, K, dnum;
 };
 
-// One key-switch input of a batch.
+// One key-switch of a batch: out = KS_key( galois_elt(a) ) + (galois_elt(add0), add1).
+// Items whose `a` is the same polynomial share ONE ModUp (hoisting): the exact centred base
+// extension commutes with the automorphism, so the result is bit-identical to a ModUp of
+// galois_elt(a).  `src` indexes the batch's list of distinct inputs.
 struct KsItem {
-    const u64* a;        // poly to switch (NTT form, l limbs), read through galois elt `elt`
+    const u64* a;        // poly to switch (NTT form, l limbs), un-permuted
     const u64* add0;     // added to output comp 0 (through `elt`), may be null
     const u64* add1;     // added to output comp 1 (identity), may be null
     const u64* key;      // [dnum][2][K][N]
     u64* out0;           // l limbs
     u64* out1;           // l limbs
-    u64 elt;             // galois element applied to a / add0 (1 = identity)
-    u64 pad;
+    u64 elt;             // galois element (1 = identity)
+    u64 src;             // index of `a` in the distinct-input list
 };
 
 // Optional per-kernel event timer (bench.py): rec(ctx, id, begin, stream) is called around launches.
@@ -53,9 +58,10 @@ hipError_t launch_eltwise(const DevTables& T, int op, const u64* a, const u64* b
 hipError_t launch_tensor(const DevTables& T, const u64* a, const u64* b, u64* out3, int l, hipStream_t st);
 hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
                           hipStream_t st, const KTimer* tm = nullptr);
-hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, int l, u64* workspace,
-                            size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm);
-size_t keyswitch_workspace_bytes(const DevTables& T, int R, int l);
+// items_host[r].src must index uniq_host (U distinct inputs); items_dev holds >= R items + U pointers
+hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, const u64* const* uniq_host, int U,
+                            int l, u64* workspace, size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm);
+size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l);
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
                              int D, int l, u64* inner, hipStream_t st, const KTimer* tm);
 // giant-step key-switches of inner[1..B-1] (rotation by g*G), summed with inner[0]; output 2 x l limbs

@@ -13,6 +13,9 @@
 #include "fhs_kernels.h"
 #include "fhs_ntt.h"
 
+#include <cstring>
+#include <vector>
+
 // build-time tuning knobs (A/B variants are built with -D...; defaults are the shipped choice)
 #ifndef FHS_INNER_WAVES
 #define FHS_INNER_WAVES 8      // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
@@ -268,58 +271,152 @@ hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scra
 }
 
 // ============================================================================ key-switch
-// (a) y = INTT(galois(a)) * inv_hat(digit) per data limb (inv_hat folded into the N^-1 stage)
+// (a) y = INTT(a) * inv_hat(digit) per data limb of every distinct input (inv_hat folded into
+// the N^-1 stage).  No automorphism here: it is applied after the (hoisted) ModUp.
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const KsItem* items, u64* acoef, int l) {
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const u64* const* uniq, u64* acoef, int l) {
     constexpr int N = 1 << LOGN, TH = N / 16;
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, i = blockIdx.x, r = blockIdx.y;
-    const KsItem it = items[r];
+    const int tid = threadIdx.x, i = blockIdx.x, u = blockIdx.y;
     const PrimeK& P = PK(T, i);
-    const u64* src = it.a + (size_t)i * N;
+    const u64* src = uniq[u] + (size_t)i * N;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
-        lds[lds_pad(e)] = src[galois_src(e, it.elt, LOGN)];
-    }
+    for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[tid + c * TH];
     __syncthreads();
     const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
     ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)i * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
-    u64* dst = acoef + ((size_t)r * l + i) * N;
+    u64* dst = acoef + ((size_t)u * l + i) * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
 }
 
-// (b1) ModUp + NTT: ext[r][j][t] = NTT_t(conv_{digit j -> prime t}(y)) for every extended-basis
-// limb t outside digit j (limbs inside digit j are the input itself and are read by k_ks_ip).
+// Exact centred-extension count, slow path (|frac - 1/2| < 2^-58; never seen on random data
+// but required for exactness): v = carry + [2X >= (2 carry + 1) Q_S], X = sum_u y_u Q_S/q_u.
+__device__ __noinline__ int centered_exact(const u64* y, const u64* qs, int ns, int carry) {
+    u64 X[10], Q[10], t[10];
+    for (int w = 0; w < 10; ++w) { X[w] = 0; Q[w] = 0; }
+    Q[0] = 1;
+    for (int u = 0; u < ns; ++u) {
+        u64 cy = 0;
+        for (int w = 0; w < 10; ++w) {
+            const u64 lo = Q[w] * qs[u], hi = __umul64hi(Q[w], qs[u]);
+            const u64 z = lo + cy;
+            cy = hi + (z < lo);
+            Q[w] = z;
+        }
+    }
+    for (int u = 0; u < ns; ++u) {
+        for (int w = 0; w < 10; ++w) t[w] = 0;
+        t[0] = y[u];
+        for (int v = 0; v < ns; ++v) {
+            if (v == u) continue;
+            u64 cy = 0;
+            for (int w = 0; w < 10; ++w) {
+                const u64 lo = t[w] * qs[v], hi = __umul64hi(t[w], qs[v]);
+                const u64 z = lo + cy;
+                cy = hi + (z < lo);
+                t[w] = z;
+            }
+        }
+        u64 cy = 0;
+        for (int w = 0; w < 10; ++w) {
+            const u64 z1 = X[w] + t[w];
+            const u64 c1 = z1 < X[w];
+            const u64 z2 = z1 + cy;
+            cy = c1 + (z2 < z1);
+            X[w] = z2;
+        }
+    }
+    // compare 2X with (2 carry + 1) Q from the top word down
+    const u64 mlt = (u64)(2 * carry + 1);
+    u64 L[10], Rr[10], cl = 0, cr = 0;
+    for (int w = 0; w < 10; ++w) {
+        L[w] = (X[w] << 1) | cl;
+        cl = X[w] >> 63;
+        const u64 lo = Q[w] * mlt, hi = __umul64hi(Q[w], mlt);
+        const u64 z = lo + cr;
+        cr = hi + (z < lo);
+        Rr[w] = z;
+    }
+    for (int w = 9; w >= 0; --w)
+        if (L[w] != Rr[w]) return carry + (L[w] > Rr[w] ? 1 : 0);
+    return carry + 1;
+}
+
+// (a2) v[u][j][n] = round(sum_{u in digit j} y_u / q_u): fixed-point fast path (error < 2 ns ulp
+// of 2^-64), exact fallback within 64 ulp of a half (oracle: ock_centered_count).
+__global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, int l, int U) {
+    const int N = T.N, P_ = T.P, dn = (l + P_ - 1) / P_;
+    const size_t total = (size_t)U * dn * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int n = (int)(idx % N);
+        const int j = (int)((idx / N) % dn);
+        const int u = (int)(idx / ((size_t)N * dn));
+        const int s0 = j * P_, ns = min(s0 + P_, l) - s0;
+        const u64* yb = acoef + ((size_t)u * l + s0) * N + n;
+        int v;
+        if (ns == 1) {
+            v = yb[0] > (PK(T, s0).q >> 1) ? 1 : 0;
+        } else {
+            const u64* R = T.modup_R + (((size_t)l * T.dnum + j) * P_) * 2;
+            u64 lo = 0, ys[8], qs[8];
+            int carry = 0;
+            for (int k = 0; k < ns; ++k) {
+                ys[k] = yb[(size_t)k * N];
+                qs[k] = PK(T, s0 + k).q;
+                const u64 F = ys[k] * R[2 * k + 1] + __umul64hi(ys[k], R[2 * k]);
+                lo += F;
+                carry += lo < F;
+            }
+            const u64 half = 1ULL << 63;
+            const u64 d = lo >= half ? lo - half : half - lo;
+            v = d > 64 ? carry + (lo >= half ? 1 : 0) : centered_exact(ys, qs, ns, carry);
+        }
+        vout[idx] = (unsigned char)v;
+    }
+}
+
+// (b1) ModUp + NTT: ext[u][j][t] = NTT_t(centred conv_{digit j -> t}(y_u)) for t outside digit
+// j, and a copy of the input limb t for t inside digit j.
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u64* acoef, u64* ext, int l) {
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u64* const* uniq, const u64* acoef,
+                                                            const unsigned char* vcnt, u64* ext, int l) {
     constexpr int N = 1 << LOGN, TH = N / 16;
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, t = blockIdx.x, j = blockIdx.y, r = blockIdx.z;
+    const int tid = threadIdx.x, t = blockIdx.x, j = blockIdx.y, u = blockIdx.z;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
-    if (t >= s0 && t < s1) return;   // whole block exits: no barrier is skipped
+    u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
+    if (t >= s0 && t < s1) {   // own limb: plain copy (whole block takes this branch)
+        const u64* src = uniq[u] + (size_t)t * N;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) o[tid + c * TH] = src[tid + c * TH];
+        return;
+    }
     const int pt = t < l ? t : T.L0 + (t - l);
     const PrimeK& PM = PK(T, pt);
     const u64 m = PM.q;
-    const u64* yb = acoef + ((size_t)r * l + s0) * N;
+    const u64* yb = acoef + ((size_t)u * l + s0) * N;
     const u64* hat = T.modup_hat + (((size_t)l * T.dnum + j) * P_) * K + pt;
+    const u64* qv = T.modup_Q + (((size_t)l * T.dnum + j) * K + pt) * 2;
+    const u64 Qm = qv[0], nsQm = qv[1];
+    const unsigned char* vb = vcnt + ((size_t)u * dn + j) * N;
     u64 h[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) h[u] = u < ns ? hat[(size_t)u * K] : 0;
+    for (int k = 0; k < 8; ++k) h[k] = k < ns ? hat[(size_t)k * K] : 0;
 #pragma unroll 4
     for (int k = 0; k < 16; ++k) {
         const int e = tid + k * TH;
         u128 s = {0, 0};
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (u < ns) mac128(s, yb[(size_t)u * N + e], h[u]);
-        lds[lds_pad(e)] = barrett128(s.lo, s.hi, m, PM.r0, PM.r1);
+        for (int w = 0; w < 8; ++w)
+            if (w < ns) mac128(s, yb[(size_t)w * N + e], h[w]);
+        mac128(s, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
+        lds[lds_pad(e)] = submod(barrett128(s.lo, s.hi, m, PM.r0, PM.r1), nsQm, m);
     }
     __syncthreads();
     ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m);
-    u64* o = ext + (((size_t)r * dn + j) * E + t) * N;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
@@ -327,8 +424,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     }
 }
 
-// (b2) key inner product, lazy 128-bit: acc[r][c][t] = sum_j ext_j[t] (.) key_j[c][t]  (one
-// Barrett reduction per output word instead of one per product)
+// (b2) key inner product with the automorphism applied on the fly, lazy 128-bit over digits:
+// acc[r][c][t][n] = sum_j ext[src][j][t][galois_src(n)] * key_j[c][t][n].
+// The NTT-domain automorphism maps every aligned run of 64 slots onto an aligned run of 64 slots
+// (bit-reversed order: the low 6 bits of the slot index are the top 6 bits of the evaluation
+// exponent, which k * (.) permutes among themselves), so each wave's gather touches exactly one
+// 512-byte region: four whole cache lines, no amplification.
 __global__ void k_ks_ip(DevTables T, const KsItem* items, const u64* ext, u64* acc, int l, int R) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const size_t per_r = (size_t)E * N;
@@ -340,14 +441,18 @@ __global__ void k_ks_ip(DevTables T, const KsItem* items, const u64* ext, u64* a
         const int pt = t < l ? t : T.L0 + (t - l);
         const PrimeK& PM = PK(T, pt);
         const KsItem it = items[r];
-        const u64* ex = ext + (size_t)r * dn * per_r + (size_t)t * N + n;
+        const int sn = galois_src(n, it.elt, T.logN);
+        const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
         const u64* key = it.key + (size_t)pt * N + n;
-        const int jown = t < l ? t / P_ : -1;
         u128 c0 = {0, 0}, c1 = {0, 0};
         for (int j = 0; j < dn; ++j) {
-            const u64 v = (j == jown) ? it.a[(size_t)t * N + galois_src(n, it.elt, T.logN)] : ex[(size_t)j * per_r];
+            const u64 v = ex[(size_t)j * per_r];
             mac128(c0, v, key[(size_t)(2 * j) * K * N]);
             mac128(c1, v, key[(size_t)(2 * j + 1) * K * N]);
+            if ((j & 31) == 31) {   // keep the lazy sums < 2^128 for > 32 digits of 61-bit primes
+                c0.lo = barrett128(c0.lo, c0.hi, PM.q, PM.r0, PM.r1); c0.hi = 0;
+                c1.lo = barrett128(c1.lo, c1.hi, PM.q, PM.r0, PM.r1); c1.hi = 0;
+            }
         }
         acc[(((size_t)r * 2 + 0) * E + t) * N + n] = barrett128(c0.lo, c0.hi, PM.q, PM.r0, PM.r1);
         acc[(((size_t)r * 2 + 1) * E + t) * N + n] = barrett128(c1.lo, c1.hi, PM.q, PM.r0, PM.r1);
@@ -412,27 +517,31 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
     }
 }
 
-size_t keyswitch_workspace_bytes(const DevTables& T, int R, int l) {
+size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l) {
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
-    // acoef | ext | acc | ycoef
-    return 8 * N * ((size_t)R * l + (size_t)R * dn * E + (size_t)R * 2 * E + (size_t)R * 2 * T.P);
+    // acoef | ext | acc | ycoef | centred counts (bytes, rounded up to words)
+    return 8 * N * ((size_t)U * l + (size_t)U * dn * E + (size_t)R * 2 * E + (size_t)R * 2 * T.P) +
+           ((size_t)U * dn * N + 7) / 8 * 8;
 }
 
-// ModUp + key inner product for R items; leaves acc [R][2][E][N] and ycoef [R][2][P][N]
+// INTT + centred ModUp per distinct input, then key inner product and special-limb INTT per item;
+// leaves acc [R][2][E][N] and ycoef [R][2][P][N]
 template <int LOGN>
-static void ks_front(const DevTables& T, const KsItem* it, int R, int l, u64* ws, hipStream_t st, const KTimer* tm,
-                     u64** acc_out, u64** ycoef_out) {
+static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uniq, int R, int U, int l, u64* ws,
+                     hipStream_t st, const KTimer* tm, u64** acc_out, u64** ycoef_out) {
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     u64* acoef = ws;
-    u64* ext = acoef + (size_t)R * l * N;
-    u64* acc = ext + (size_t)R * dn * E * N;
+    u64* ext = acoef + (size_t)U * l * N;
+    u64* acc = ext + (size_t)U * dn * E * N;
     u64* ycoef = acc + (size_t)R * 2 * E * N;
+    unsigned char* vcnt = reinterpret_cast<unsigned char*>(ycoef + (size_t)R * 2 * T.P * N);
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l, R), blk, 0, st, T, it, acoef, l);
+    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l, U), blk, 0, st, T, uniq, acoef, l);
+    hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, acoef, vcnt, l, U);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
-    hipLaunchKernelGGL((k_modup<LOGN>), dim3(E, dn, R), blk, 0, st, T, acoef, ext, l);
+    hipLaunchKernelGGL((k_modup<LOGN>), dim3(E, dn, U), blk, 0, st, T, uniq, acoef, vcnt, ext, l);
     FHS_TMARK(tm, KID_MODUP, 0, st);
     FHS_TMARK(tm, KID_KS_IP, 1, st);
     hipLaunchKernelGGL(k_ks_ip, dim3(eltwise_grid((size_t)R * E * N)), dim3(256), 0, st, T, it, ext, acc, l, R);
@@ -444,15 +553,29 @@ static void ks_front(const DevTables& T, const KsItem* it, int R, int l, u64* ws
     *ycoef_out = ycoef;
 }
 
-hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, int l, u64* ws, size_t ws_bytes,
-                            void* items_dev, hipStream_t st, const KTimer* tm) {
-    if (keyswitch_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
-    hipError_t e = hipMemcpyAsync(items_dev, items_host, sizeof(KsItem) * R, hipMemcpyHostToDevice, st);
+static hipError_t upload_items(const KsItem* items, int R, const u64* const* uniq, int U, void* dev, hipStream_t st,
+                               const KsItem** it_dev, const u64* const** uniq_dev) {
+    // one staging copy: [R items][U pointers]
+    static thread_local std::vector<unsigned char> buf;
+    buf.resize(sizeof(KsItem) * R + sizeof(u64*) * U);
+    memcpy(buf.data(), items, sizeof(KsItem) * R);
+    memcpy(buf.data() + sizeof(KsItem) * R, uniq, sizeof(u64*) * U);
+    hipError_t e = hipMemcpyAsync(dev, buf.data(), buf.size(), hipMemcpyHostToDevice, st);
+    *it_dev = reinterpret_cast<const KsItem*>(dev);
+    *uniq_dev = reinterpret_cast<const u64* const*>(static_cast<unsigned char*>(dev) + sizeof(KsItem) * R);
+    return e;
+}
+
+hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, const u64* const* uniq_host, int U,
+                            int l, u64* ws, size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm) {
+    if (keyswitch_workspace_bytes(T, R, U, l) > ws_bytes) return hipErrorInvalidValue;
+    const KsItem* it;
+    const u64* const* uq;
+    hipError_t e = upload_items(items_host, R, uniq_host, U, items_dev, st, &it, &uq);
     if (e != hipSuccess) return e;
-    const KsItem* it = reinterpret_cast<const KsItem*>(items_dev);
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
-        ks_front<LOGN>(T, it, R, l, ws, st, tm, &acc, &ycoef);
+        ks_front<LOGN>(T, it, uq, R, U, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_MODDOWN, 1, st);
         hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l, 2, R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
         FHS_TMARK(tm, KID_MODDOWN, 0, st);
@@ -577,7 +700,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_giant_final(DevTables T, c
 }
 
 size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
-    return keyswitch_workspace_bytes(T, R, l) + 8 * (size_t)T.N * 4 * l;
+    return keyswitch_workspace_bytes(T, R, R, l) + 8 * (size_t)T.N * 4 * l;
 }
 
 hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
@@ -586,22 +709,25 @@ hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B,
     const size_t N = T.N, S = (size_t)l * N;
     if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
     if (bsgs_giant_workspace_bytes(T, R, l) > ws_bytes || R > 512) return hipErrorInvalidValue;
-    u64* base = ws + keyswitch_workspace_bytes(T, R, l) / 8;
+    u64* base = ws + keyswitch_workspace_bytes(T, R, R, l) / 8;
     u64* convsum = base + 2 * S;
     KsItem items[512];
+    const u64* uniq[512];
     for (int r = 0; r < R; ++r) {
         const int g = r + 1;
         const u64* ct = inner + (size_t)g * 2 * S;
         u64 elt = 1;
         for (int s = 0; s < g * G; ++s) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
-        items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, 0};
+        items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)r};
+        uniq[r] = ct + S;
     }
-    hipError_t e = hipMemcpyAsync(items_dev, items, sizeof(KsItem) * R, hipMemcpyHostToDevice, st);
+    const KsItem* it;
+    const u64* const* uq;
+    hipError_t e = upload_items(items, R, uniq, R, items_dev, st, &it, &uq);
     if (e != hipSuccess) return e;
-    const KsItem* it = reinterpret_cast<const KsItem*>(items_dev);
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
-        ks_front<LOGN>(T, it, R, l, ws, st, tm, &acc, &ycoef);
+        ks_front<LOGN>(T, it, uq, R, R, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_GIANT_SUM, 1, st);
         hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, st, T, it, acc, ycoef, inner, base,
                            convsum, l, R);

@@ -289,6 +289,53 @@ void ock_rescale_to_next(const ock_ctx* c, const uint64_t* in, uint64_t* out, in
 }
 
 /* ------------------------------------------------------------------ hybrid key-switch */
+/* Exact centred base extension count: v = round(sum_u y_u / q_u) = the number of Q_S to subtract
+ * from X = sum_u y_u (Q_S/q_u) so that X - v Q_S lies in (-Q_S/2, Q_S/2).  Fast path: 64-bit
+ * fixed-point sum of frac(y_u/q_u) via R_u = floor(2^128/q_u) (error < 2 ns ulp); when the
+ * fraction is within 64 ulp of 1/2 the decision is made exactly with multi-word integers.
+ * Exactness makes the extension commute with the signed coefficient permutations of Galois
+ * automorphisms, so a hoisted ModUp (one per input, rotations applied afterwards) is
+ * bit-identical to one ModUp per rotated input.   */
+static int ock_centered_count(const uint64_t* y, const uint64_t* qs, int ns) {
+    if (ns == 1) return y[0] > (qs[0] >> 1);
+    uint64_t lo = 0; int carry = 0;
+    for (int u = 0; u < ns; u++) {
+        u128 R = (~(u128)0) / qs[u];                       /* floor(2^128 / q) for odd q */
+        uint64_t R0 = (uint64_t)R, R1 = (uint64_t)(R >> 64);
+        uint64_t F = y[u] * R1 + (uint64_t)(((u128)y[u] * R0) >> 64);
+        lo += F; carry += (lo < F);
+    }
+    uint64_t half = (uint64_t)1 << 63;
+    uint64_t d = lo >= half ? lo - half : half - lo;
+    if (d > 64) return carry + (lo >= half);
+    /* exact: v = carry + [2X >= (2 carry + 1) Q] with X = sum_u y_u prod_{u' != u} q_u' */
+    uint64_t X[10] = {0}, Q[10] = {0}, t[10];
+    Q[0] = 1;
+    for (int u = 0; u < ns; u++) {
+        u128 cy = 0;
+        for (int w = 0; w < 10; w++) { u128 z = (u128)Q[w] * qs[u] + cy; Q[w] = (uint64_t)z; cy = z >> 64; }
+    }
+    for (int u = 0; u < ns; u++) {
+        memset(t, 0, sizeof t); t[0] = y[u];
+        for (int v = 0; v < ns; v++) {
+            if (v == u) continue;
+            u128 cy = 0;
+            for (int w = 0; w < 10; w++) { u128 z = (u128)t[w] * qs[v] + cy; t[w] = (uint64_t)z; cy = z >> 64; }
+        }
+        u128 cy = 0;
+        for (int w = 0; w < 10; w++) { u128 z = (u128)X[w] + t[w] + cy; X[w] = (uint64_t)z; cy = z >> 64; }
+    }
+    /* lhs = 2X, rhs = (2 carry + 1) Q */
+    uint64_t L[10], Rr[10]; u128 cy = 0;
+    for (int w = 0; w < 10; w++) { u128 z = ((u128)X[w] << 1) + cy; L[w] = (uint64_t)z; cy = z >> 64; }
+    cy = 0;
+    for (int w = 0; w < 10; w++) { u128 z = (u128)Q[w] * (uint64_t)(2 * carry + 1) + cy; Rr[w] = (uint64_t)z; cy = z >> 64; }
+    int ge = 1;
+    for (int w = 9; w >= 0; w--) { if (L[w] != Rr[w]) { ge = L[w] > Rr[w]; break; } }
+    return carry + ge;
+}
+int ock_centered_count_test(const uint64_t* y, const uint64_t* qs, int ns) { return ock_centered_count(y, qs, ns); }
+
 /* Digit j of level l covers data primes [jP, min(jP+P, l)).  ModUp (approximate fast base
  * conversion) -> inner product with key digits over Q_l u P -> ModDown by P (no rounding
  * term).  This is the per-rotation (non-hoisted) key-switch the reference issues at bg:219 and
@@ -316,16 +363,21 @@ void ock_keyswitch(const ock_ctx* c, const uint64_t* a, const uint64_t* key, int
             if (t >= s0 && t < s1) {
                 memcpy(ext, a + (size_t)t * N, 8 * N);
             } else {
-                uint64_t hm[8];
+                uint64_t hm[8], Qm = 1;
                 for (int u = 0; u < ns; u++) {
                     uint64_t h = 1;
                     for (int v = 0; v < ns; v++) if (v != u) h = mulmod(h, c->q[s0 + v] % m, m);
                     hm[u] = h;
+                    Qm = mulmod(Qm, c->q[s0 + u] % m, m);
                 }
                 for (uint64_t n = 0; n < N; n++) {
+                    uint64_t yy[8];
+                    for (int u = 0; u < ns; u++) yy[u] = y[(size_t)u * N + n];
+                    int v = ock_centered_count(yy, c->q + s0, ns);
                     u128 s = 0;
-                    for (int u = 0; u < ns; u++) s += (u128)y[(size_t)u * N + n] * hm[u];
-                    ext[n] = (uint64_t)(s % m);
+                    for (int u = 0; u < ns; u++) s += (u128)yy[u] * hm[u];
+                    uint64_t r = (uint64_t)(s % m);
+                    ext[n] = submod(r, mulmod((uint64_t)v, Qm, m), m);   /* X - v Q_S (centred) */
                 }
                 ock_ntt_fwd(c, ext, pi);
             }
@@ -385,6 +437,102 @@ void ock_rotate(const ock_ctx* c, const uint64_t* ct, const uint64_t* gkey, uint
         out[S + o] = k1[o];
     }
     free(r); free(k0); free(k1);
+}
+
+/* Hoisted rotations of ONE ciphertext: ModUp(c1) once, then per rotation the NTT-domain
+ * automorphism of every extended digit, key inner product and ModDown.  With the exact centred
+ * extension this equals ock_rotate per element, limb for limb (tests/test_cpu.py). */
+void ock_rotate_hoisted(const ock_ctx* c, const uint64_t* ct, const uint64_t* const* gkeys, const uint64_t* elts,
+                        int nrot, int l, uint64_t* const* outs) {
+    uint64_t N = c->N; int P = c->P, L0 = c->L0, K = c->K, E = l + P;
+    int dnum = (l + P - 1) / P;
+    size_t S = (size_t)l * N;
+    const uint64_t* c1 = ct + S;
+    uint64_t* acoef = (uint64_t*)malloc(8 * S);
+    memcpy(acoef, c1, 8 * S);
+    for (int i = 0; i < l; i++) ock_ntt_inv(c, acoef + (size_t)i * N, i);
+    uint64_t* ext = (uint64_t*)malloc(8 * N * (size_t)dnum * E);   /* [j][t][N] */
+    for (int j = 0; j < dnum; j++) {
+        int s0 = j * P, s1 = s0 + P < l ? s0 + P : l, ns = s1 - s0;
+        uint64_t y[8][1];
+        (void)y;
+        for (int t = 0; t < E; t++) {
+            int pi = ext_prime(c, l, t); uint64_t m = c->q[pi];
+            uint64_t* dst = ext + ((size_t)j * E + t) * N;
+            if (t >= s0 && t < s1) { memcpy(dst, c1 + (size_t)t * N, 8 * N); continue; }
+            uint64_t hm[8], ih[8], Qm = 1;
+            for (int u = 0; u < ns; u++) {
+                uint64_t h = 1, hq = 1, q = c->q[s0 + u];
+                for (int v = 0; v < ns; v++) if (v != u) { h = mulmod(h, c->q[s0 + v] % m, m); hq = mulmod(hq, c->q[s0 + v] % q, q); }
+                hm[u] = h; ih[u] = invmod(hq, q);
+                Qm = mulmod(Qm, c->q[s0 + u] % m, m);
+            }
+            for (uint64_t n = 0; n < N; n++) {
+                uint64_t yy[8];
+                for (int u = 0; u < ns; u++) yy[u] = mulmod(acoef[(size_t)(s0 + u) * N + n], ih[u], c->q[s0 + u]);
+                int v = ock_centered_count(yy, c->q + s0, ns);
+                u128 sum = 0;
+                for (int u = 0; u < ns; u++) sum += (u128)yy[u] * hm[u];
+                dst[n] = submod((uint64_t)(sum % m), mulmod((uint64_t)v, Qm, m), m);
+            }
+            ock_ntt_fwd(c, dst, pi);
+        }
+    }
+    uint64_t* perm = (uint64_t*)malloc(8 * N);
+    uint64_t* acc = (uint64_t*)malloc(8 * N * 2 * (size_t)E);
+    uint64_t* yp = (uint64_t*)malloc(8 * N * P);
+    uint64_t* tmp = (uint64_t*)malloc(8 * N);
+    for (int r = 0; r < nrot; r++) {
+        uint64_t elt = elts[r];
+        const uint64_t* key = gkeys[r];
+        memset(acc, 0, 8 * N * 2 * (size_t)E);
+        for (int j = 0; j < dnum; j++)
+            for (int t = 0; t < E; t++) {
+                int pi = ext_prime(c, l, t); uint64_t m = c->q[pi];
+                ock_apply_galois_ntt(c, ext + ((size_t)j * E + t) * N, perm, elt);
+                for (int comp = 0; comp < 2; comp++) {
+                    const uint64_t* kp = key + (((size_t)j * 2 + comp) * K + pi) * N;
+                    uint64_t* ap = acc + ((size_t)comp * E + t) * N;
+                    for (uint64_t n = 0; n < N; n++) ap[n] = addmod(ap[n], mulmod(perm[n], kp[n], m), m);
+                }
+            }
+        uint64_t* out = outs[r];
+        for (int comp = 0; comp < 2; comp++) {
+            for (int k = 0; k < P; k++) {
+                int pi = L0 + k; uint64_t p = c->q[pi], hat = 1;
+                for (int v = 0; v < P; v++) if (v != k) hat = mulmod(hat, c->q[L0 + v] % p, p);
+                uint64_t ihp = invmod(hat, p);
+                uint64_t* dst = yp + (size_t)k * N;
+                memcpy(dst, acc + ((size_t)comp * E + l + k) * N, 8 * N);
+                ock_ntt_inv(c, dst, pi);
+                for (uint64_t n = 0; n < N; n++) dst[n] = mulmod(dst[n], ihp, p);
+            }
+            for (int i = 0; i < l; i++) {
+                uint64_t q = c->q[i], hmk[8], Pm = 1;
+                for (int k = 0; k < P; k++) {
+                    uint64_t h = 1;
+                    for (int v = 0; v < P; v++) if (v != k) h = mulmod(h, c->q[L0 + v] % q, q);
+                    hmk[k] = h; Pm = mulmod(Pm, c->q[L0 + k] % q, q);
+                }
+                uint64_t Pinv = invmod(Pm, q);
+                for (uint64_t n = 0; n < N; n++) {
+                    u128 sum = 0;
+                    for (int k = 0; k < P; k++) sum += (u128)yp[(size_t)k * N + n] * hmk[k];
+                    tmp[n] = (uint64_t)(sum % q);
+                }
+                ock_ntt_fwd(c, tmp, i);
+                const uint64_t* ap = acc + ((size_t)comp * E + i) * N;
+                uint64_t* o = out + (size_t)comp * S + (size_t)i * N;
+                for (uint64_t n = 0; n < N; n++) o[n] = mulmod(submod(ap[n], tmp[n], q), Pinv, q);
+            }
+        }
+        /* + galois(c0) */
+        for (int i = 0; i < l; i++) {
+            ock_apply_galois_ntt(c, ct + (size_t)i * N, perm, elt);
+            for (uint64_t n = 0; n < N; n++) out[(size_t)i * N + n] = addmod(out[(size_t)i * N + n], perm[n], c->q[i]);
+        }
+    }
+    free(acoef); free(ext); free(perm); free(acc); free(yp); free(tmp);
 }
 
 void ock_relinearize(const ock_ctx* c, const uint64_t* ct3, const uint64_t* rlk, int l, uint64_t* out) {

@@ -64,8 +64,13 @@ void ock_rescale_to_next(const ock_ctx* c, const uint64_t* in, uint64_t* out, in
 /* hybrid key-switch of poly a (NTT, l limbs) with key [dnum][2][L0+P][N]; out0/out1 l limbs */
 void ock_keyswitch(const ock_ctx* c, const uint64_t* a, const uint64_t* key, int l,
                    uint64_t* out0, uint64_t* out1);
+/* exact centred base-extension count (exposed for tests) */
+int ock_centered_count_test(const uint64_t* y, const uint64_t* qs, int ns);
 /* rotate = galois(elt) + key-switch of c1 (pb:203) */
 void ock_rotate(const ock_ctx* c, const uint64_t* ct, const uint64_t* gkey, uint64_t elt, int l, uint64_t* out);
+/* nrot rotations of one ciphertext with a single (hoisted) ModUp; identical limbs to ock_rotate */
+void ock_rotate_hoisted(const ock_ctx* c, const uint64_t* ct, const uint64_t* const* gkeys, const uint64_t* elts,
+                        int nrot, int l, uint64_t* const* outs);
 /* relinearize 3-component ct with relin key (pb:183) */
 void ock_relinearize(const ock_ctx* c, const uint64_t* ct3, const uint64_t* rlk, int l, uint64_t* out);
 

@@ -62,6 +62,9 @@ def lib():
         L.ock_keyswitch.argtypes = [vp, _u64p, _u64p, C.c_int, _u64p, _u64p]
         L.ock_rotate.argtypes = [vp, _u64p, _u64p, C.c_uint64, C.c_int, _u64p]
         L.ock_relinearize.argtypes = [vp, _u64p, _u64p, C.c_int, _u64p]
+        L.ock_rotate_hoisted.argtypes = [vp, _u64p, C.POINTER(_u64p), _u64p, C.c_int, C.c_int, C.POINTER(_u64p)]
+        L.ock_centered_count_test.argtypes = [_u64p, _u64p, C.c_int]
+        L.ock_centered_count_test.restype = C.c_int
         L.ock_bsgs_loop.argtypes = [vp, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p),
                                     C.c_int, C.c_int, C.c_int, C.c_int, _u64p]
         L.ock_gen_secret.argtypes = [vp, C.c_uint64, _u64p]
@@ -91,6 +94,12 @@ def create_coeff_modulus(N: int, bits) -> list[int]:
     if rc != 0:
         raise ValueError(f"create_coeff_modulus failed rc={rc}")
     return [int(x) for x in out]
+
+
+def centered_count(y, qs) -> int:
+    y = np.ascontiguousarray(np.asarray(y, dtype=np.uint64))
+    q = np.ascontiguousarray(np.asarray(qs, dtype=np.uint64))
+    return int(lib().ock_centered_count_test(_p(y), _p(q), len(y)))
 
 
 def galois_elt(step: int, N: int) -> int:
@@ -201,6 +210,17 @@ class Oracle:
         out = np.empty_like(ct)
         lib().ock_rotate(self._h, _p(ct), _p(np.ascontiguousarray(gkey)), elt, l, _p(out))
         return out
+
+    def rotate_hoisted(self, ct, keys, elts):
+        l = ct.shape[1]
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        keys = [np.ascontiguousarray(k, dtype=np.uint64) for k in keys]
+        e = np.ascontiguousarray(np.asarray(elts, dtype=np.uint64))
+        outs = [np.empty_like(ct) for _ in keys]
+        KA = (_u64p * len(keys))(*[_p(k) for k in keys])
+        OA = (_u64p * len(outs))(*[_p(o) for o in outs])
+        lib().ock_rotate_hoisted(self._h, _p(ct), KA, _p(e), len(keys), l, OA)
+        return outs
 
     def relinearize(self, ct3, rlk):
         l = ct3.shape[1]

@@ -231,3 +231,35 @@ def test_two_rank_exchange_gloo():
     assert res[0][4] == [[(2 * p0 - 3) % p0, 10], [(2 * p1 - 4) % p1, 15]]
     assert res[0][5] == [["r", "v"], ["o"], ["ffn_key_0"], ["ffn_val_0"]]
     assert res[1][5] == [["k"], [], ["ffn_key_1"], ["ffn_val_1"]]
+
+
+# ------------------------------------------------------------------ exact centred ModUp / hoisting
+def test_centered_count_exact_including_near_half(orc):
+    from math import prod
+    rng = np.random.default_rng(11)
+    for ns in (1, 2, 3, 4):
+        qs = orc.create_coeff_modulus(1 << 14, [59] * ns)
+        Q = prod(qs)
+        for trial in range(3000):
+            y = [int(rng.integers(0, q)) for q in qs]
+            if ns > 1 and trial % 2:       # steer sum_u y_u/q_u to within a few ulp of k + 1/2
+                f = sum(y[u] / qs[u] for u in range(ns - 1))
+                tgt = (np.floor(f) + 1.5 - f) % 1.0
+                y[-1] = (int(tgt * qs[-1]) + int(rng.integers(-3, 4))) % qs[-1]
+            X = sum(yu * (Q // qu) for yu, qu in zip(y, qs))
+            assert orc.centered_count(y, qs) == (2 * X + Q) // (2 * Q)
+
+
+def test_hoisted_rotations_bit_identical_to_individual(orc):
+    N, L0, P = 1024, 6, 3
+    qs = orc.create_coeff_modulus(N, [59] * (L0 + P))
+    o = orc.Oracle(N, qs, P)
+    s = o.gen_secret(8)
+    rng = np.random.default_rng(4)
+    for l in (6, 4):
+        ct = np.stack([np.stack([rng.integers(0, qs[i], N, dtype=np.uint64) for i in range(l)]) for _ in range(2)])
+        steps = [1, 2, 5, -1]
+        elts = [orc.galois_elt(k, N) for k in steps]
+        keys = [o.gen_galois_key(8, s, e) for e in elts]
+        for h, k, e in zip(o.rotate_hoisted(ct, keys, elts), keys, elts):
+            assert np.array_equal(h, o.rotate_elt(ct, k, e))
