@@ -74,6 +74,31 @@ static uint64_t h_pow(uint64_t b, uint64_t e, uint64_t q) {
 }
 static uint64_t h_inv(uint64_t a, uint64_t q) { return h_pow(a % q, q - 2, q); }
 static uint64_t h_shoup(uint64_t w, uint64_t q) { return (uint64_t)(((hu128)w << 64) / q); }
+
+// q = 2^b - d qualifies for pm_reduce128 (fhs_modarith.h) when its three folds provably take
+// every 128-bit input below 2q: B_{k+1} = (B_k >> b) d + 2^b - 1 from B_0 = 2^128 - 1, with the
+// fold-2 quotient < 2^64 and the fold-3 quotient < 2^32.  Returns the PrimeK.pm word or 0.
+static uint64_t pm_word(uint64_t q, int logN) {
+    int b = 64 - __builtin_clzll(q);
+    if (b < 40 || b > 62) return 0;
+    const uint64_t d = (1ull << b) - q;
+    if (d >= (1ull << 32)) return 0;
+    const hu128 lim = ((hu128)1 << b) - 1;
+    const hu128 B0 = ~(hu128)0;
+    const hu128 h1 = B0 >> b;                       // < 2^88: product with d may overflow -> check
+    if ((h1 >> 96) != 0) return 0;
+    const hu128 B1 = h1 * d + lim;                  // h1 < 2^96, d < 2^32 -> < 2^128
+    if (B1 < h1 * d) return 0;
+    const hu128 h2 = B1 >> b;
+    if ((h2 >> 64) != 0) return 0;
+    const hu128 B2 = h2 * d + lim;
+    const hu128 h3 = B2 >> b;
+    if ((h3 >> 32) != 0) return 0;
+    const hu128 B3 = h3 * d + lim;
+    if (B3 >= 2 * (hu128)q) return 0;
+    const bool lazy = (hu128)q * (uint64_t)(4 + 2 * logN) < ((hu128)1 << 64);   // fhs_ntt.h LAZY bound
+    return (d << 8) | (lazy ? 128u : 0u) | (uint64_t)b;
+}
 static bool h_is_prime(uint64_t n) {
     if (n < 2) return false;
     const uint64_t bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
@@ -385,7 +410,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
         }
         const uint64_t ninv = h_inv(N % q, q);
         const uint64_t w1n = h_mulmod(twi[((size_t)i * N + 1) * 2], ninv, q);
-        pk[i] = PrimeK{q, (uint64_t)r, (uint64_t)(r >> 64), ninv, h_shoup(ninv, q), w1n, h_shoup(w1n, q), 0};
+        pk[i] = PrimeK{q, (uint64_t)r, (uint64_t)(r >> 64), ninv, h_shoup(ninv, q), w1n, h_shoup(w1n, q), pm_word(q, c->logN)};
     }
     // ---- ModUp tables per level l: digit j covers [jP, min(jP+P, l))
     std::vector<uint64_t> mu_intt((size_t)(L0 + 1) * L0 * 4, 0), mu_hat((size_t)(L0 + 1) * dnum * P * K, 0);
@@ -1555,5 +1580,14 @@ extern "C" fhs_status fhs_ciphertext_from_device(fhs_context* c, const void* src
     HIPCHK(hipMemcpyAsync(ct->d, src, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st), "from_device");
     HIPCHK(hipStreamSynchronize(c->st), "from_device");
     *out = ct;
+    return FHS_OK;
+}
+
+extern "C" fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* out, int* pm_used) {
+    if (!out || q < 3) return FHS_ERR_INVALID;
+    const uint64_t w = pm_word(q, 14);
+    if (pm_used) *pm_used = w != 0;
+    *out = w ? pm_reduce128(lo, hi, q, (unsigned)(w & 127), (unsigned)(w >> 8))
+             : (uint64_t)((((hu128)hi << 64) | lo) % q);
     return FHS_OK;
 }

@@ -20,6 +20,15 @@
 #ifndef FHS_INNER_WAVES
 #define FHS_INNER_WAVES 8      // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
 #endif
+#ifndef FHS_MODUP_MAP
+#define FHS_MODUP_MAP 2     // block->(limb, input) map of k_modup: 0 plain, 1 XCD t-inner, 2 XCD m-major
+#endif
+#ifndef FHS_MODDOWN_MAP
+#define FHS_MODDOWN_MAP 0
+#endif
+#ifndef FHS_MODUP_CH
+#define FHS_MODUP_CH 4
+#endif
 #ifndef FHS_MODUP_RL
 #define FHS_MODUP_RL 3         // radix (log2) of the register passes in k_modup's NTT
 #endif
@@ -44,6 +53,44 @@ namespace fhs {
 __device__ __forceinline__ const PrimeK& PK(const DevTables& T, int i) {
     return reinterpret_cast<const PrimeK*>(T.primes)[i];
 }
+
+// XCD-aware block decode.  Workgroups are dealt round-robin over the 8 XCDs (observed placement,
+// MI355X_MICROARCH.md "Workgroup dispatch"; speed only, never correctness), so block b runs on the
+// XCD shared by all blocks b' == b (mod 8).  Giving XCD x only the limbs t == x (mod 8) keeps that
+// XCD's L2 (4 MiB) holding ~E/8 primes' twiddle tables instead of all E (10 MiB at E = 39).
+// Grid = 8 * ceil(E/8) * M blocks; returns false for the padding blocks.
+//   t-inner: an XCD cycles its primes fastest (blocks sharing an input m = (digit, input) run together)
+//   t-outer: an XCD finishes one limb t across all m before the next (shared per-limb data stays hot)
+__host__ __device__ __forceinline__ int xcd_grid(int E, int M) { return 8 * ((E + 7) / 8) * M; }
+__device__ __forceinline__ bool xcd_tinner(int E, int M, int& t, int& m) {
+    const int b = blockIdx.x, x = b & 7, k = b >> 3, nx = (E - x + 7) >> 3;
+    if (nx <= 0 || k >= nx * M) return false;
+    t = x + 8 * (k % nx);
+    m = k / nx;
+    return true;
+}
+// m-major: XCD x takes the inputs m == x (mod 8), all limbs t of one m back to back
+__device__ __forceinline__ bool xcd_mmajor(int E, int M, int& t, int& m) {
+    const int b = blockIdx.x, x = b & 7, k = b >> 3, nm = (M - x + 7) >> 3;
+    if (nm <= 0 || k >= nm * E) return false;
+    m = x + 8 * (k / E);
+    t = k % E;
+    return true;
+}
+__host__ __device__ __forceinline__ int xcd_grid_m(int E, int M) { return 8 * ((M + 7) / 8) * E; }
+// plain: blockIdx.x = t + E * m (t fastest)
+__device__ __forceinline__ bool plain_tm(int E, int M, int& t, int& m) {
+    t = blockIdx.x % E;
+    m = blockIdx.x / E;
+    return m < M;
+}
+__device__ __forceinline__ bool xcd_touter(int E, int M, int& t, int& m) {
+    const int b = blockIdx.x, x = b & 7, k = b >> 3, nx = (E - x + 7) >> 3;
+    if (nx <= 0 || k >= nx * M) return false;
+    t = x + 8 * (k / M);
+    m = k % M;
+    return true;
+}
 __device__ __forceinline__ int limb_prime(int b, int l_split, int L0) { return b < l_split ? b : L0 + (b - l_split); }
 
 // NTT-domain automorphism X -> X^elt: output slot e reads input slot galois_src(e)
@@ -66,16 +113,17 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_fwd(DevTables T, u64* 
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
     const int tid = threadIdx.x, b = blockIdx.x;
     const int pi = limb_prime(b, l_split, T.L0);
-    const u64 q = PK(T, pi).q;
+    const RedU R = redu(PK(T, pi));
+    const u64 q = R.q;
     u64* p = data + blockIdx.y * poly_stride + (size_t)b * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = p[tid + k * TH];
     __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)pi * N * 2, q);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)pi * N * 2, q, R.lazy);
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        p[e] = csub(csub(lds[lds_pad(e)], 2 * q), q);
+        p[e] = fwd_canon(lds[lds_pad(e)], R);
     }
 }
 
@@ -139,7 +187,7 @@ __global__ void k_eltwise(DevTables T, int op, const u64* __restrict__ a, const 
             case OP_SUB: r0 = submod(av.x, bv.x, q); r1 = submod(av.y, bv.y, q); break;
             case OP_SUBNEG: r0 = submod(bv.x, av.x, q); r1 = submod(bv.y, av.y, q); break;
             case OP_NEG: r0 = av.x ? q - av.x : 0; r1 = av.y ? q - av.y : 0; break;
-            case OP_MULP: r0 = mulmod(av.x, bv.x, q, P.r0, P.r1); r1 = mulmod(av.y, bv.y, q, P.r0, P.r1); break;
+            case OP_MULP: r0 = mulmod(av.x, bv.x, P); r1 = mulmod(av.y, bv.y, P); break;
             case OP_ADDP:
                 if (comp == 0) { r0 = addmod(av.x, bv.x, q); r1 = addmod(av.y, bv.y, q); }
                 else { r0 = av.x; r1 = av.y; }
@@ -176,12 +224,12 @@ __global__ void k_tensor(DevTables T, const u64* __restrict__ a, const u64* __re
         const int i = (int)(idx / N);
         const PrimeK& P = PK(T, i);
         const u64 a0 = a[idx], a1 = a[S + idx], b0 = b[idx], b1 = b[S + idx];
-        out[idx] = mulmod(a0, b0, P.q, P.r0, P.r1);
+        out[idx] = mulmod(a0, b0, P);
         u128 m = {0, 0};
         mac128(m, a0, b1);
         mac128(m, a1, b0);
-        out[S + idx] = barrett128(m.lo, m.hi, P.q, P.r0, P.r1);
-        out[2 * S + idx] = mulmod(a1, b1, P.q, P.r0, P.r1);
+        out[S + idx] = reduce128(m.lo, m.hi, P);
+        out[2 * S + idx] = mulmod(a1, b1, P);
     }
 }
 hipError_t launch_tensor(const DevTables& T, const u64* a, const u64* b, u64* out3, int l, hipStream_t st) {
@@ -194,7 +242,7 @@ __global__ void k_key_prod(DevTables T, const u64* a, const u64* b, u64* out, in
     const size_t S = (size_t)limbs * T.N;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
         const PrimeK& P = PK(T, (int)(idx / T.N));
-        out[idx] = mulmod(a[idx], b[idx], P.q, P.r0, P.r1);
+        out[idx] = mulmod(a[idx], b[idx], P);
     }
 }
 hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st) {
@@ -245,15 +293,16 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_ntt(DevTables T, c
     const u64 inv = rs[0], inv_s = rs[1], hq = rs[2];
     const u64* src = scratch + (size_t)comp * N;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = submod(barrett64(src[tid + k * TH], P.q, P.r0, P.r1), hq, P.q);
+    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = submod(reduce64(src[tid + k * TH], P), hq, P.q);
     __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
+    const RedU RU = redu(P);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q, RU.lazy);
     const u64* a = in + ((size_t)comp * l + i) * N;
     u64* o = out + ((size_t)comp * (l - 1) + i) * N;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        const u64 t = csub(csub(lds[lds_pad(e)], 2 * P.q), P.q);
+        const u64 t = fwd_canon(lds[lds_pad(e)], RU);
         o[e] = shoup(submod(a[e], t, P.q), inv, inv_s, P.q);
     }
 }
@@ -274,10 +323,12 @@ hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scra
 // (a) y = INTT(a) * inv_hat(digit) per data limb of every distinct input (inv_hat folded into
 // the N^-1 stage).  No automorphism here: it is applied after the (hoisted) ModUp.
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const u64* const* uniq, u64* acoef, int l) {
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const u64* const* uniq, u64* acoef, int l, int U) {
     constexpr int N = 1 << LOGN, TH = N / 16;
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, i = blockIdx.x, u = blockIdx.y;
+    const int tid = threadIdx.x;
+    int i, u;
+    if (!plain_tm(l, U, i, u)) return;
     const PrimeK& P = PK(T, i);
     const u64* src = uniq[u] + (size_t)i * N;
 #pragma unroll
@@ -381,11 +432,20 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
 // j, and a copy of the input limb t for t inside digit j.
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u64* const* uniq, const u64* acoef,
-                                                            const unsigned char* vcnt, u64* ext, int l) {
+                                                            const unsigned char* vcnt, u64* ext, int l, int U) {
     constexpr int N = 1 << LOGN, TH = N / 16;
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, t = blockIdx.x, j = blockIdx.y, u = blockIdx.z;
+    const int tid = threadIdx.x;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    int t, mi;
+#if FHS_MODUP_MAP == 1
+    if (!xcd_tinner(E, dn * U, t, mi)) return;
+#elif FHS_MODUP_MAP == 2
+    if (!xcd_mmajor(E, dn * U, t, mi)) return;
+#else
+    if (!plain_tm(E, dn * U, t, mi)) return;
+#endif
+    const int j = mi % dn, u = mi / dn;
     const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
     u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
     if (t >= s0 && t < s1) {   // own limb: plain copy (whole block takes this branch)
@@ -402,25 +462,44 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     const u64* qv = T.modup_Q + (((size_t)l * T.dnum + j) * K + pt) * 2;
     const u64 Qm = qv[0], nsQm = qv[1];
     const unsigned char* vb = vcnt + ((size_t)u * dn + j) * N;
-    u64 h[8];
+    const RedU R = redu(PM);
+    constexpr int CH = FHS_MODUP_CH;
+    // CH outputs per thread at a time; the digit's ns input limbs stream through a runtime loop so
+    // the CH loads of one limb are issued together (no per-element guards between loads).
+#pragma unroll 1
+    for (int half = 0; half < 16 / CH; ++half) {
+        u128 acc[CH];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) h[k] = k < ns ? hat[(size_t)k * K] : 0;
-#pragma unroll 4
-    for (int k = 0; k < 16; ++k) {
-        const int e = tid + k * TH;
-        u128 s = {0, 0};
+        for (int k = 0; k < CH; ++k) acc[k] = u128{0, 0};
+#pragma unroll 1
+        for (int w = 0; w < ns; ++w) {
+            const u64 hw = hat[(size_t)w * K];
+            const u64* yw = yb + (size_t)w * N + half * CH * TH + tid;
+            u64 y[CH];
 #pragma unroll
-        for (int w = 0; w < 8; ++w)
-            if (w < ns) mac128(s, yb[(size_t)w * N + e], h[w]);
-        mac128(s, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
-        lds[lds_pad(e)] = submod(barrett128(s.lo, s.hi, m, PM.r0, PM.r1), nsQm, m);
+            for (int k = 0; k < CH; ++k) y[k] = yw[k * TH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) mac128(acc[k], y[k], hw);
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const int e = tid + (half * CH + k) * TH;
+#ifdef FHS_EXP_NOCONV
+            lds[lds_pad(e)] = acc[k].lo ^ vb[e];
+#else
+            mac128(acc[k], (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
+            lds[lds_pad(e)] = submod(reduce128(acc[k].lo, acc[k].hi, R), nsQm, m);
+#endif
+        }
     }
     __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m);
+#ifndef FHS_EXP_NONTT
+    ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m, R.lazy);
+#endif
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        o[e] = csub(csub(lds[lds_pad(e)], 2 * m), m);
+        o[e] = fwd_canon(lds[lds_pad(e)], R);
     }
 }
 
@@ -430,33 +509,33 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 // (bit-reversed order: the low 6 bits of the slot index are the top 6 bits of the evaluation
 // exponent, which k * (.) permutes among themselves), so each wave's gather touches exactly one
 // 512-byte region: four whole cache lines, no amplification.
-__global__ void k_ks_ip(DevTables T, const KsItem* items, const u64* ext, u64* acc, int l, int R) {
+__global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items, const u64* ext, u64* acc, int l,
+                                                int R) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    const int NB = N >> 8;
+    int t, m;
+    if (!xcd_touter(E, R * NB, t, m)) return;   // rotations of one limb t run together on one XCD
+    const int r = m / NB, n = ((m % NB) << 8) + threadIdx.x;
     const size_t per_r = (size_t)E * N;
-    const size_t total = (size_t)R * per_r;
-    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (size_t)gridDim.x * blockDim.x) {
-        const int r = (int)(idx / per_r);
-        const int t = (int)((idx % per_r) / N), n = (int)(idx % N);
-        const int pt = t < l ? t : T.L0 + (t - l);
-        const PrimeK& PM = PK(T, pt);
-        const KsItem it = items[r];
-        const int sn = galois_src(n, it.elt, T.logN);
-        const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
-        const u64* key = it.key + (size_t)pt * N + n;
-        u128 c0 = {0, 0}, c1 = {0, 0};
-        for (int j = 0; j < dn; ++j) {
-            const u64 v = ex[(size_t)j * per_r];
-            mac128(c0, v, key[(size_t)(2 * j) * K * N]);
-            mac128(c1, v, key[(size_t)(2 * j + 1) * K * N]);
-            if ((j & 31) == 31) {   // keep the lazy sums < 2^128 for > 32 digits of 61-bit primes
-                c0.lo = barrett128(c0.lo, c0.hi, PM.q, PM.r0, PM.r1); c0.hi = 0;
-                c1.lo = barrett128(c1.lo, c1.hi, PM.q, PM.r0, PM.r1); c1.hi = 0;
-            }
+    const int pt = t < l ? t : T.L0 + (t - l);
+    const RedU RD = redu(PK(T, pt));
+    const KsItem it = items[r];
+    const int sn = galois_src(n, it.elt, T.logN);
+    const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
+    const u64* key = it.key + (size_t)pt * N + n;
+    u128 c0 = {0, 0}, c1 = {0, 0};
+#pragma unroll 4
+    for (int j = 0; j < dn; ++j) {
+        const u64 v = ex[(size_t)j * per_r];
+        mac128(c0, v, __builtin_nontemporal_load(key + (size_t)(2 * j) * K * N));
+        mac128(c1, v, __builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N));
+        if ((j & 31) == 31) {   // keep the lazy sums < 2^128 for > 32 digits of 61-bit primes
+            c0.lo = reduce128(c0.lo, c0.hi, RD); c0.hi = 0;
+            c1.lo = reduce128(c1.lo, c1.hi, RD); c1.hi = 0;
         }
-        acc[(((size_t)r * 2 + 0) * E + t) * N + n] = barrett128(c0.lo, c0.hi, PM.q, PM.r0, PM.r1);
-        acc[(((size_t)r * 2 + 1) * E + t) * N + n] = barrett128(c1.lo, c1.hi, PM.q, PM.r0, PM.r1);
     }
+    acc[(((size_t)r * 2 + 0) * E + t) * N + n] = reduce128(c0.lo, c0.hi, RD);
+    acc[(((size_t)r * 2 + 1) * E + t) * N + n] = reduce128(c1.lo, c1.hi, RD);
 }
 
 // (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
@@ -487,8 +566,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
                                                               const u64* ycoef, int l, int R) {
     constexpr int N = 1 << LOGN, TH = N / 16;
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, i = blockIdx.x, comp = blockIdx.y, r = blockIdx.z;
+    const int tid = threadIdx.x;
     const int P_ = T.P, E = l + P_;
+    int i, m;
+#if FHS_MODDOWN_MAP == 1
+    if (!xcd_tinner(l, 2 * R, i, m)) return;
+#else
+    if (!plain_tm(l, 2 * R, i, m)) return;
+#endif
+    const int comp = m & 1, r = m >> 1;
     const PrimeK& P = PK(T, i);
     const u64 q = P.q;
     const KsItem it = items[r];
@@ -498,10 +584,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
         const int e = tid + kk * TH;
         u128 s = {0, 0};
         for (int k = 0; k < P_; ++k) mac128(s, y[(size_t)k * N + e], T.md_hat[(size_t)k * T.L0 + i]);
-        lds[lds_pad(e)] = barrett128(s.lo, s.hi, q, P.r0, P.r1);
+        lds[lds_pad(e)] = reduce128(s.lo, s.hi, P);
     }
     __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, q);
+    const RedU RU = redu(P);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, q, RU.lazy);
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
     const u64* add = comp == 0 ? it.add0 : it.add1;
     const u64 aelt = comp == 0 ? it.elt : 1;
@@ -509,7 +596,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        const u64 v = csub(csub(lds[lds_pad(e)], 2 * q), q);
+        const u64 v = fwd_canon(lds[lds_pad(e)], RU);
         const u64 a = acc[(((size_t)r * 2 + comp) * E + i) * N + e];
         u64 res = shoup(submod(a, v, q), pinv, pinv_s, q);
         if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
@@ -537,14 +624,14 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     unsigned char* vcnt = reinterpret_cast<unsigned char*>(ycoef + (size_t)R * 2 * T.P * N);
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l, U), blk, 0, st, T, uniq, acoef, l);
+    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, acoef, l, U);
     hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, acoef, vcnt, l, U);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
-    hipLaunchKernelGGL((k_modup<LOGN>), dim3(E, dn, U), blk, 0, st, T, uniq, acoef, vcnt, ext, l);
+    hipLaunchKernelGGL((k_modup<LOGN>), dim3(FHS_MODUP_MAP == 1 ? xcd_grid((int)E, (int)(dn * U)) : FHS_MODUP_MAP == 2 ? xcd_grid_m((int)E, (int)(dn * U)) : (int)(E * dn * U)), blk, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     FHS_TMARK(tm, KID_MODUP, 0, st);
     FHS_TMARK(tm, KID_KS_IP, 1, st);
-    hipLaunchKernelGGL(k_ks_ip, dim3(eltwise_grid((size_t)R * E * N)), dim3(256), 0, st, T, it, ext, acc, l, R);
+    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid((int)E, R * (int)(N >> 8))), dim3(256), 0, st, T, it, ext, acc, l, R);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
     hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), blk, 0, st, T, acc, ycoef, l, R);
@@ -577,7 +664,7 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
         u64 *acc, *ycoef;
         ks_front<LOGN>(T, it, uq, R, U, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_MODDOWN, 1, st);
-        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l, 2, R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
+        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(FHS_MODDOWN_MAP == 1 ? xcd_grid(l, 2 * R) : l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
         FHS_TMARK(tm, KID_MODDOWN, 0, st);
     });
     return hipGetLastError();
@@ -613,8 +700,8 @@ __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T
         // they stay < 2^128 for any prime < 2^61
         for (; b + 8 <= bmax; b += 8) {
             if (b && (b & 31) == 0) {
-                c0.lo = barrett128(c0.lo, c0.hi, q, P.r0, P.r1); c0.hi = 0;
-                c1.lo = barrett128(c1.lo, c1.hi, q, P.r0, P.r1); c1.hi = 0;
+                c0.lo = reduce128(c0.lo, c0.hi, P); c0.hi = 0;
+                c1.lo = reduce128(c1.lo, c1.hi, P); c1.hi = 0;
             }
             u64 p[8];
 #pragma unroll
@@ -630,8 +717,8 @@ __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T
             mac128(c0, sb[(b * 2 + 0) * 64 + lane], p);
             mac128(c1, sb[(b * 2 + 1) * 64 + lane], p);
         }
-        inner[(size_t)g * 2 * S + off] = barrett128(c0.lo, c0.hi, q, P.r0, P.r1);
-        inner[(size_t)g * 2 * S + S + off] = barrett128(c1.lo, c1.hi, q, P.r0, P.r1);
+        inner[(size_t)g * 2 * S + off] = reduce128(c0.lo, c0.hi, P);
+        inner[(size_t)g * 2 * S + S + off] = reduce128(c1.lo, c1.hi, P);
     }
 }
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
@@ -666,7 +753,7 @@ __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, co
             const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N + n;
             for (int k = 0; k < P_; ++k) {
                 mac128(cs, y[(size_t)k * N], T.md_hat[(size_t)k * T.L0 + i]);
-                if (++cnt == 48) { cs.lo = barrett128(cs.lo, cs.hi, q, P.r0, P.r1); cs.hi = 0; cnt = 0; }
+                if (++cnt == 48) { cs.lo = reduce128(cs.lo, cs.hi, P); cs.hi = 0; cnt = 0; }
             }
             as = addmod(as, acc[(((size_t)r * 2 + comp) * E + i) * N + n], q);
             if (comp == 0) {
@@ -674,7 +761,7 @@ __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, co
                 add = addmod(add, it.add0[(size_t)i * N + galois_src(n, it.elt, T.logN)], q);
             }
         }
-        convsum[idx] = barrett128(cs.lo, cs.hi, q, P.r0, P.r1);
+        convsum[idx] = reduce128(cs.lo, cs.hi, P);
         base[idx] = addmod(shoup(as, T.md_pinv[2 * i], T.md_pinv[2 * i + 1], q), add, q);
     }
 }
@@ -689,12 +776,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_giant_final(DevTables T, c
 #pragma unroll
     for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = convsum[off + tid + k * TH];
     __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q);
+    const RedU RU = redu(P);
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q, RU.lazy);
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        const u64 v = csub(csub(lds[lds_pad(e)], 2 * P.q), P.q);
+        const u64 v = fwd_canon(lds[lds_pad(e)], RU);
         out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, P.q), P.q);
     }
 }
@@ -759,7 +847,7 @@ __global__ void k_sample(DevTables T, int mode, u64 key, u64* out, int l) {
         u64 v;
         if (mode == SAMPLE_UNIFORM) {
             const u64 ctr = 2 * ((u64)i * N + n);
-            v = barrett128(rnd(key, ctr + 1), rnd(key, ctr), P.q, P.r0, P.r1);
+            v = reduce128(rnd(key, ctr + 1), rnd(key, ctr), P);
         } else {
             const u64 r = rnd(key, (u64)n);
             long long s;
@@ -788,10 +876,10 @@ __global__ void k_swk(DevTables T, u64* key, const u64* e, const u64* s, const u
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
         const int i = (int)(idx / N);
         const PrimeK& P = PK(T, i);
-        u64 v = submod(e[idx], mulmod(k1[idx], s[idx], P.q, P.r0, P.r1), P.q);
+        u64 v = submod(e[idx], mulmod(k1[idx], s[idx], P), P.q);
         if (i < T.L0 && i / T.P == j) {
             const u64 pm = T.md_pinv[2 * T.L0 + i];   // P mod q_i stored after the inverses
-            v = addmod(v, mulmod(pm, snew[idx], P.q, P.r0, P.r1), P.q);
+            v = addmod(v, mulmod(pm, snew[idx], P), P.q);
         }
         k0[idx] = v;
     }
@@ -815,10 +903,10 @@ __global__ void k_encrypt(DevTables T, int mode, u64* c0, u64* c1, const u64* s_
         const u64 q = P.q;
         const u64 m = pt ? pt[idx] : 0;
         if (mode == 0) {
-            c0[idx] = addmod(submod(e0[idx], mulmod(c1[idx], s_or_pk0[idx], q, P.r0, P.r1), q), m, q);
+            c0[idx] = addmod(submod(e0[idx], mulmod(c1[idx], s_or_pk0[idx], P), q), m, q);
         } else {
-            c0[idx] = addmod(addmod(mulmod(u[idx], s_or_pk0[idx], q, P.r0, P.r1), e0[idx], q), m, q);
-            c1[idx] = addmod(mulmod(u[idx], pk1[idx], q, P.r0, P.r1), e1[idx], q);
+            c0[idx] = addmod(addmod(mulmod(u[idx], s_or_pk0[idx], P), e0[idx], q), m, q);
+            c1[idx] = addmod(mulmod(u[idx], pk1[idx], P), e1[idx], q);
         }
     }
 }
@@ -839,8 +927,8 @@ __global__ void k_decrypt(DevTables T, const u64* ct, int ncomp, const u64* s, u
         const u64 sv = s[idx];
         u64 v = ct[idx], sp = sv;
         for (int k = 1; k < ncomp; ++k) {
-            v = addmod(v, mulmod(ct[k * S + idx], sp, P.q, P.r0, P.r1), P.q);
-            sp = mulmod(sp, sv, P.q, P.r0, P.r1);
+            v = addmod(v, mulmod(ct[k * S + idx], sp, P), P.q);
+            sp = mulmod(sp, sv, P);
         }
         out[idx] = v;
     }
@@ -866,12 +954,12 @@ __global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64*
         const double a = neg ? -d : d;
         u64 r;
         if (a < 9.2e18) {
-            r = barrett64((u64)a, P.q, P.r0, P.r1);
+            r = reduce64((u64)a, P);
         } else {
             const u64 bits = (u64)__double_as_longlong(a);
             const int ex = (int)((bits >> 52) & 0x7FF) - 1075;
             const u64 mant = (bits & ((1ULL << 52) - 1)) | (1ULL << 52);
-            r = mulmod(barrett64(mant, P.q, P.r0, P.r1), T.pow2[(size_t)i * 1088 + ex], P.q, P.r0, P.r1);
+            r = mulmod(reduce64(mant, P), T.pow2[(size_t)i * 1088 + ex], P);
         }
         out[idx] = (neg && r) ? P.q - r : r;
     }

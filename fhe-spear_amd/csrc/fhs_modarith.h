@@ -25,12 +25,33 @@ __device__ __forceinline__ void mac128(u128& acc, u64 a, u64 b) {
     acc.hi += hi + (acc.lo < lo);
 }
 
-__device__ __forceinline__ u64 csub(u64 a, u64 q) { return a >= q ? a - q : a; }
+__host__ __device__ __forceinline__ u64 csub(u64 a, u64 q) { return a >= q ? a - q : a; }
 
+// 64x64 products spelled out in 32-bit halves: gfx950 issues v_mad_u64_u32 / v_mul_lo_u32 /
+// v_mul_hi_u32 at about the rate of a 64-bit add (tools/microbench/instrate.hip), so what counts is
+// the instruction total; this form lets the compiler fold the carries into the mad accumulators.
+__device__ __forceinline__ u64 mul32w(uint32_t a, uint32_t b) { return (u64)a * b; }
+__device__ __forceinline__ u64 mulhi64x(u64 a, u64 b) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const u64 t = mul32w(a1, b0) + __umulhi(a0, b0);
+    const u64 s = mul32w(a0, b1) + (uint32_t)t;
+    return mul32w(a1, b1) + (t >> 32) + (s >> 32);
+}
+__device__ __forceinline__ u64 mullo64x(u64 a, u64 b) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const u64 p = mul32w(a0, b0);
+    const uint32_t hi = (uint32_t)(p >> 32) + a1 * b0 + a0 * b1;
+    return ((u64)hi << 32) | (uint32_t)p;
+}
 // Shoup: w * a mod q given wp = floor(w 2^64 / q); result in [0, 2q) for any 64-bit a.
 __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, u64 q) {
-    u64 qh = __umul64hi(a, wp);
+#ifdef FHS_OLD_SHOUP
+    const u64 qh = __umul64hi(a, wp);
     return a * w - qh * q;
+#else
+    const u64 qh = mulhi64x(a, wp);
+    return mullo64x(a, w) - mullo64x(qh, q);
+#endif
 }
 __device__ __forceinline__ u64 shoup(u64 a, u64 w, u64 wp, u64 q) { return csub(shoup_lazy(a, w, wp, q), q); }
 
@@ -49,10 +70,37 @@ __device__ __forceinline__ u64 barrett128(u64 lo, u64 hi, u64 q, u64 r0, u64 r1)
     r = csub(r, q);
     return csub(r, q);
 }
-__device__ __forceinline__ u64 barrett64(u64 a, u64 q, u64 r0, u64 r1) { return barrett128(a, 0, q, r0, r1); }
 
-__device__ __forceinline__ u64 mulmod(u64 a, u64 b, u64 q, u64 r0, u64 r1) {
-    return barrett128(a * b, __umul64hi(a, b), q, r0, r1);
+// Pseudo-Mersenne reduction for q = 2^b - d (d < 2^32): x = x_h 2^b + x_l == x_h d + x_l (mod q).
+// Three folds take any 128-bit x below 2q; the host (pm_eligible in fhs_host.hip) proves the
+// fold bounds for each prime before enabling this path.  SEAL-style Create() primes sit just
+// below 2^b, so d is small (< 2^27 for the reference's 59-bit chain).  Six 32x32->64 multiplies
+// against ~23 for barrett128.
+__host__ __device__ __forceinline__ u64 pm_reduce128(u64 lo, u64 hi, u64 q, unsigned b, unsigned d) {
+    const u64 mask = (1ull << b) - 1;
+    const unsigned sb = 64 - b;
+    // fold 1: x_h = top 2^64 + mid, top < 2^(64-b)
+    const u64 top = hi >> b;
+    const u64 mid = (hi << sb) | (lo >> b);
+    const u64 p0 = (u64)(uint32_t)mid * d;
+    const u64 p1 = (u64)(uint32_t)(mid >> 32) * d;
+    u64 s_lo = p0 + (p1 << 32);
+    u64 s_hi = (p1 >> 32) + (u64)(uint32_t)top * d + (s_lo < p0);
+    const u64 xl = lo & mask;
+    s_lo += xl;
+    s_hi += (s_lo < xl);
+    // fold 2: x_h < 2^64
+    const u64 h2 = (s_hi << sb) | (s_lo >> b);
+    const u64 q0 = (u64)(uint32_t)h2 * d;
+    const u64 q1 = (u64)(uint32_t)(h2 >> 32) * d;
+    u64 t_lo = q0 + (q1 << 32);
+    u64 t_hi = (q1 >> 32) + (t_lo < q0);
+    const u64 yl = s_lo & mask;
+    t_lo += yl;
+    t_hi += (t_lo < yl);
+    // fold 3: x_h < 2^32
+    const u64 h3 = (t_hi << sb) | (t_lo >> b);
+    return csub((u64)(uint32_t)h3 * d + (t_lo & mask), q);
 }
 __device__ __forceinline__ u64 addmod(u64 a, u64 b, u64 q) { return csub(a + b, q); }
 __device__ __forceinline__ u64 submod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
@@ -63,5 +111,45 @@ struct PrimeK {
     u64 r0, r1;       // Barrett floor(2^128/q)
     u64 ninv, ninv_s; // N^-1 and Shoup companion
     u64 w1ninv, w1ninv_s;  // psi_rev_inv[1] * N^-1 (last GS stage)
-    u64 pad;
+    u64 pm;           // (d << 8) | lazy << 7 | b when q = 2^b - d passes the pm_reduce128 bounds, else 0;
+                      // lazy: q (4 + 2 logN) < 2^64, so forward-NTT values never leave 64 bits
 };
+
+__device__ __forceinline__ u64 reduce128(u64 lo, u64 hi, const PrimeK& P) {
+    if (P.pm) return pm_reduce128(lo, hi, P.q, (unsigned)(P.pm & 127), (unsigned)(P.pm >> 8));
+    return barrett128(lo, hi, P.q, P.r0, P.r1);
+}
+// Wave-uniform view of a prime's reduction constants (SGPRs): kernels whose prime is uniform per
+// wave use it so the pseudo-Mersenne / Barrett choice is a scalar branch, not a divergent one.
+__device__ __forceinline__ u64 rfl64(u64 x) {
+    // the builtin is int -> int: widen through uint32_t so the low word is not sign-extended
+    return ((u64)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+           (u64)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+}
+struct RedU {
+    u64 q, r0, r1;
+    unsigned b, d;
+    bool lazy;   // forward NTT may skip Harvey's conditional subtraction (PrimeK.pm bit 7)
+};
+__device__ __forceinline__ RedU redu(const PrimeK& P) {
+    const u64 pm = rfl64(P.pm);
+    return RedU{rfl64(P.q), rfl64(P.r0), rfl64(P.r1), (unsigned)(pm & 127), (unsigned)(pm >> 8), (pm & 128) != 0};
+}
+__device__ __forceinline__ u64 reduce128(u64 lo, u64 hi, const RedU& R) {
+    if (R.b) return pm_reduce128(lo, hi, R.q, R.b, R.d);
+    return barrett128(lo, hi, R.q, R.r0, R.r1);
+}
+// Any 64-bit value of a pseudo-Mersenne prime (b >= 41) to [0, q): one fold, one subtraction.
+__device__ __forceinline__ u64 pm_fold64(u64 x, const RedU& R) {
+    const u64 h = x >> R.b;
+    return csub((x & ((1ull << R.b) - 1)) + (u64)(uint32_t)h * R.d, R.q);
+}
+// Canonical residue of a forward-NTT output: lazy outputs are < (4 + 2 logN) q, Harvey ones < 4q.
+__device__ __forceinline__ u64 fwd_canon(u64 x, const RedU& R) {
+#ifndef FHS_NO_LAZY
+    if (R.lazy) return pm_fold64(x, R);
+#endif
+    return csub(csub(x, 2 * R.q), R.q);
+}
+__device__ __forceinline__ u64 reduce64(u64 a, const PrimeK& P) { return reduce128(a, 0, P); }
+__device__ __forceinline__ u64 mulmod(u64 a, u64 b, const PrimeK& P) { return reduce128(a * b, __umul64hi(a, b), P); }

@@ -29,7 +29,12 @@ __device__ __forceinline__ void ld_tw(const u64* __restrict__ tw, int idx, u64& 
 // One pass over stages [S, S+R) (forward numbering: stage s has m = 2^s blocks, stride N>>(s+1)).
 // Groups: {j0 + k*TL : k < 2^R}, j0 = blk*2*TF + off, off < TL; thread tid owns groups
 // gid = tid + c*T for c < (N/2^R)/T.
-template <int LOGN, int S, int R, bool FWD, int EPT>
+// LAZY (forward only): no conditional subtraction at all; a value that entered below B leaves
+// stage s below B + 2 s q (the Shoup product is < 2q for any 64-bit input), so 14 stages from
+// B = 4q stay below 32q < 2^64 for q < 2^59 (host flag PrimeK.pm bit 7).
+// When a group's block index is wave-uniform (TL >= 64) it is read through readfirstlane so the
+// twiddle loads become scalar loads.
+template <int LOGN, int S, int R, bool FWD, int EPT, bool LAZY = false>
 __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
                                          u64 s1, u64 s1s) {
     constexpr int N = 1 << LOGN, T = N / EPT;
@@ -41,7 +46,11 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
 #pragma unroll 1
     for (int c = 0; c < NG; ++c) {
         const int gid = tid + c * T;
+        #ifdef FHS_NO_SCALAR_TW
         const int blk = gid / TL, off = gid % TL;
+#else
+        const int blk = TL >= 64 ? __builtin_amdgcn_readfirstlane(gid) / TL : gid / TL, off = gid % TL;
+#endif
         const int j0 = blk * 2 * TF + off;
         u64 x[GS];
 #pragma unroll
@@ -56,10 +65,10 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
                     u64 w, wp;
                     ld_tw(tw, (1 << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
                     u64 X = x[k];
-                    X = X >= q2 ? X - q2 : X;
+                    if constexpr (!LAZY) X = X >= q2 ? X - q2 : X;
                     const u64 t = shoup_lazy(x[k + half], w, wp, q);
                     x[k] = X + t;
-                    x[k + half] = X - t + q2;
+                    x[k + half] = X + (q2 - t);
                 }
             }
         } else {
@@ -88,13 +97,13 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
     }
 }
 
-template <int LOGN, int RL, int S, int EPT>
+template <int LOGN, int RL, int S, int EPT, bool LAZY>
 __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q) {
     if constexpr (S < LOGN) {
         constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
-        ntt_pass<LOGN, S, R, true, EPT>(lds, tid, tw, q, 0, 0, 0, 0);
+        ntt_pass<LOGN, S, R, true, EPT, LAZY>(lds, tid, tw, q, 0, 0, 0, 0);
         __syncthreads();
-        fwd_from<LOGN, RL, S + R, EPT>(lds, tid, tw, q);
+        fwd_from<LOGN, RL, S + R, EPT, LAZY>(lds, tid, tw, q);
     }
 }
 // inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first
@@ -110,12 +119,19 @@ __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restric
 }
 
 // Forward transform in LDS.  Entry: input (< 4q) at padded natural positions, after a barrier.
-// Exit: bit-reversed-order output in [0, 4q), after a barrier.
+// Exit: bit-reversed-order output, after a barrier: < 4q (Harvey) or < (4 + 2 LOGN) q when
+// `lazy` (wave-uniform; RedU::lazy); fwd_canon() maps either to [0, q).
 template <int LOGN, int RL = 3, int EPT = 16>
-__device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q) {
+__device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, bool lazy) {
     static_assert(LOGN >= 8 && LOGN <= 14, "LDS-resident NTT supports 256 <= N <= 16384");
     static_assert(EPT >= 16 && (EPT & (EPT - 1)) == 0, "EPT must be a power of two >= 16");
-    fwd_from<LOGN, RL, 0, EPT>(lds, tid, tw, q);
+#ifdef FHS_NO_LAZY
+    lazy = false;
+#endif
+    if (lazy)
+        fwd_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q);
+    else
+        fwd_from<LOGN, RL, 0, EPT, false>(lds, tid, tw, q);
 }
 // Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.

@@ -185,6 +185,10 @@ fhs_status fhs_kernel_timer(fhs_context* ctx, int kernel_id, float* ms, int* lau
 fhs_status fhs_ciphertext_copy_to_device(fhs_context* ctx, const fhs_ciphertext* ct, void* dst);
 fhs_status fhs_ciphertext_from_device(fhs_context* ctx, const void* src, int ncomp, int chain_index, double scale,
                                       fhs_ciphertext** out);
+/* Host-side diagnostic of the device reduction arithmetic (no GPU needed): reduces hi:lo mod q with
+ * the pseudo-Mersenne folds the kernels use when q qualifies (*pm_used = 1), else *pm_used = 0 and
+ * *out = (hi:lo) mod q.  Exists so the CPU test suite can check the fold bounds against big ints. */
+fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* out, int* pm_used);
 
 #ifdef __cplusplus
 }

@@ -263,3 +263,50 @@ def test_hoisted_rotations_bit_identical_to_individual(orc):
         keys = [o.gen_galois_key(8, s, e) for e in elts]
         for h, k, e in zip(o.rotate_hoisted(ct, keys, elts), keys, elts):
             assert np.array_equal(h, o.rotate_elt(ct, k, e))
+
+
+def _lib():
+    import ctypes
+    lib_path = REPO / "fhe-spear_amd" / "lib" / "libfhespear_hip.so"
+    if not lib_path.exists():
+        import __graft_entry__
+        __graft_entry__.build()
+    return ctypes.CDLL(str(lib_path))
+
+
+def test_pseudo_mersenne_reduction_matches_bigint(orc):
+    """The kernels' q = 2^b - d folds (fhs_modarith.h pm_reduce128) against Python big ints, on
+    the reference's 59-bit chain (all eligible), on 60-bit primes, and on adversarial inputs
+    (all-ones, multiples of q, q-1 products, 2^128 - 1)."""
+    import ctypes
+    lib = _lib()
+    lib.fhs_debug_reduce128.argtypes = [ctypes.c_uint64] * 3 + [ctypes.POINTER(ctypes.c_uint64),
+                                                              ctypes.POINTER(ctypes.c_int)]
+    rng = np.random.default_rng(7)
+    primes = orc.create_coeff_modulus(16384, [59] * 39) + orc.create_coeff_modulus(32768, [60] * 4) \
+        + orc.create_coeff_modulus(4096, [36] * 3)
+    out, used = ctypes.c_uint64(), ctypes.c_int()
+    n_pm = 0
+    for q in primes:
+        xs = [(1 << 128) - 1, q * q - 1, (q - 1) ** 2, q << 64, ((1 << 128) // q) * q, (1 << 64) - 1, 0, q]
+        xs += [int(a) << 64 | int(b) for a, b in rng.integers(0, 2 ** 63, size=(200, 2), dtype=np.int64)]
+        xs += [((int(a) << 64) | int(b)) * 4 % (1 << 128) for a, b in rng.integers(0, 2 ** 63, size=(50, 2), dtype=np.int64)]
+        for x in xs:
+            assert lib.fhs_debug_reduce128(q, x & ((1 << 64) - 1), x >> 64, ctypes.byref(out), ctypes.byref(used)) == 0
+            assert out.value == x % q, (q, x)
+        n_pm += used.value
+        if q.bit_length() == 59 and q in primes[:39]:
+            assert used.value == 1, "reference 59-bit chain must take the pseudo-Mersenne path"
+    assert n_pm >= 43
+
+
+def test_device_ntt_passes_emulated_match_direct_evaluation(tmp_path):
+    """fhs_ntt.h's forward (Harvey and lazy) and inverse passes, compiled for the host through a
+    shim header and run thread-by-thread between barriers, against a direct O(N^2) evaluation
+    a(psi^(2 rev(i) + 1)) -- the same convention the oracle pins (test_ntt_is_evaluation_at_odd_powers)."""
+    import subprocess
+    exe = tmp_path / "ntt_emu"
+    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{REPO / 'tools/debug/shim'}", f"-I{REPO / 'fhe-spear_amd/csrc'}",
+                    str(REPO / "tools/debug/ntt_emu.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
