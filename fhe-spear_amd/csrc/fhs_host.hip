@@ -346,8 +346,9 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
                     "context_create: data primes (L0) must be a multiple of special_modulus_size (README.md:59)");
     if (special > 8) return fail(FHS_ERR_INVALID, "context_create: special_modulus_size > 8 unsupported");
     for (int i = 0; i < nprimes; ++i) {
-        if (primes[i] >= (1ull << 61) || (primes[i] - 1) % (2 * N) != 0 || !h_is_prime(primes[i]))
-            return fail(FHS_ERR_INVALID, "context_create: every modulus must be a prime < 2^61, = 1 mod 2N");
+        if (primes[i] >= (1ull << 60) || (primes[i] - 1) % (2 * N) != 0 || !h_is_prime(primes[i]))
+            return fail(FHS_ERR_INVALID, "context_create: every modulus must be a prime < 2^60 (SEAL's 60-bit "
+                                         "limit; Acc3 in fhs_modarith.h relies on it), = 1 mod 2N");
         for (int j = 0; j < i; ++j)
             if (primes[j] == primes[i]) return fail(FHS_ERR_INVALID, "context_create: duplicate modulus");
     }

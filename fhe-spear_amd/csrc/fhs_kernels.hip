@@ -18,7 +18,10 @@
 
 // build-time tuning knobs (A/B variants are built with -D...; defaults are the shipped choice)
 #ifndef FHS_INNER_WAVES
-#define FHS_INNER_WAVES 8      // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
+#define FHS_INNER_WAVES 16     // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
+#endif
+#ifndef FHS_INNER_VEC
+#define FHS_INNER_VEC 2       // consecutive coefficients per lane in k_bsgs_inner (2: 16-byte loads)
 #endif
 #ifndef FHS_MODUP_MAP
 #define FHS_MODUP_MAP 2     // block->(limb, input) map of k_modup: 0 plain, 1 XCD t-inner, 2 XCD m-major
@@ -471,16 +474,21 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
         u128 acc[CH];
 #pragma unroll
         for (int k = 0; k < CH; ++k) acc[k] = u128{0, 0};
+        Acc3 a3[CH];
+#pragma unroll
+        for (int k = 0; k < CH; ++k) a3[k] = Acc3{0, 0, 0};
 #pragma unroll 1
-        for (int w = 0; w < ns; ++w) {
-            const u64 hw = hat[(size_t)w * K];
+        for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
+            const Split30 hw = split30(hat[(size_t)w * K]);
             const u64* yw = yb + (size_t)w * N + half * CH * TH + tid;
             u64 y[CH];
 #pragma unroll
             for (int k = 0; k < CH; ++k) y[k] = yw[k * TH];
 #pragma unroll
-            for (int k = 0; k < CH; ++k) mac128(acc[k], y[k], hw);
+            for (int k = 0; k < CH; ++k) acc3_mac(a3[k], split30(y[k]), hw);
         }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) acc3_fold(acc[k], a3[k]);
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
             const int e = tid + (half * CH + k) * TH;
@@ -524,16 +532,19 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
     const u64* key = it.key + (size_t)pt * N + n;
     u128 c0 = {0, 0}, c1 = {0, 0};
+    Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
 #pragma unroll 4
     for (int j = 0; j < dn; ++j) {
-        const u64 v = ex[(size_t)j * per_r];
-        mac128(c0, v, __builtin_nontemporal_load(key + (size_t)(2 * j) * K * N));
-        mac128(c1, v, __builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N));
-        if ((j & 31) == 31) {   // keep the lazy sums < 2^128 for > 32 digits of 61-bit primes
-            c0.lo = reduce128(c0.lo, c0.hi, RD); c0.hi = 0;
-            c1.lo = reduce128(c1.lo, c1.hi, RD); c1.hi = 0;
+        const Split30 v = split30(ex[(size_t)j * per_r]);
+        acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j) * K * N)));
+        acc3_mac(a1, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N)));
+        if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
+            acc3_fold(c0, a0);
+            acc3_fold(c1, a1);
         }
     }
+    acc3_fold(c0, a0);
+    acc3_fold(c1, a1);
     acc[(((size_t)r * 2 + 0) * E + t) * N + n] = reduce128(c0.lo, c0.hi, RD);
     acc[(((size_t)r * 2 + 1) * E + t) * N + n] = reduce128(c1.lo, c1.hi, RD);
 }
@@ -675,58 +686,100 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
 // Block = 4 waves sharing one 64-coefficient slice of limb i: the slice of all G baby steps
 // (both components) is staged once in LDS, each wave then streams the diagonals of its giant
 // groups (g = wave, wave+4, ...) from HBM with lazy 128-bit accumulation.
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+template <int VEC>
+__device__ __forceinline__ void ld_diag(const u64* p, u64* out) {
+    if constexpr (VEC == 2) {
+        const u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p));
+        out[0] = t.x;
+        out[1] = t.y;
+    } else {
+        out[0] = __builtin_nontemporal_load(p);
+    }
+}
+template <int VEC>
 __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
                                                     const u64* const* __restrict__ pts, int G, int B, int D, int l,
                                                     u64* __restrict__ inner) {
-    extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][64]
+    extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][W], split-30 packed
+    constexpr int W = 64 * VEC;
     const int N = T.N;
-    const int i = blockIdx.y, n0 = blockIdx.x * 64, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t S = (size_t)l * N;
-    for (int idx = tid; idx < G * 128; idx += 64 * FHS_INNER_WAVES) {
-        const int b = idx >> 7, comp = (idx >> 6) & 1, c = idx & 63;
-        sb[idx] = baby[b][comp * S + (size_t)i * N + n0 + c];
+    for (int idx = tid; idx < G * 2 * W; idx += 64 * FHS_INNER_WAVES) {
+        const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
+        sb[idx] = pack30(baby[b][comp * S + (size_t)i * N + n0 + c]);
     }
     __syncthreads();
-    const PrimeK& P = PK(T, i);
-    const u64 q = P.q;
-    const size_t off = (size_t)i * N + n0 + lane;
+    const RedU R = redu(PK(T, i));
+    const size_t off = (size_t)i * N + n0 + lane * VEC;
     for (int g = wave; g < B; g += FHS_INNER_WAVES) {
         const int bmax = min(G, D - g * G);
         if (bmax <= 0) continue;
-        u128 c0 = {0, 0}, c1 = {0, 0};
+        u128 c0[VEC], c1[VEC];
+        Acc3 a0[VEC], a1[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+            c0[v] = c1[v] = u128{0, 0};
+            a0[v] = a1[v] = Acc3{0, 0, 0};
+        }
         const u64* const* pg = pts + (size_t)g * G;
         int b = 0;
-        // 8 diagonal loads in flight per wave-iteration; lazy sums reduced every 32 products so
-        // they stay < 2^128 for any prime < 2^61
+        // 8 diagonal loads in flight per wave-iteration, folded into the 128-bit sums every 8
         for (; b + 8 <= bmax; b += 8) {
-            if (b && (b & 31) == 0) {
-                c0.lo = reduce128(c0.lo, c0.hi, P); c0.hi = 0;
-                c1.lo = reduce128(c1.lo, c1.hi, P); c1.hi = 0;
-            }
-            u64 p[8];
+            u64 p[8][VEC];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) p[u] = __builtin_nontemporal_load(pg[b + u] + off);
+            for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + off, p[u]);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                mac128(c0, sb[((b + u) * 2 + 0) * 64 + lane], p[u]);
-                mac128(c1, sb[((b + u) * 2 + 1) * 64 + lane], p[u]);
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) {
+                    const Split30 y = split30(p[u][v]);
+                    acc3_mac(a0[v], unpack30(sb[((b + u) * 2 + 0) * W + lane * VEC + v]), y);
+                    acc3_mac(a1[v], unpack30(sb[((b + u) * 2 + 1) * W + lane * VEC + v]), y);
+                }
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+                acc3_fold(c0[v], a0[v]);
+                acc3_fold(c1[v], a1[v]);
             }
         }
-        for (; b < bmax; ++b) {
-            const u64 p = __builtin_nontemporal_load(pg[b] + off);
-            mac128(c0, sb[(b * 2 + 0) * 64 + lane], p);
-            mac128(c1, sb[(b * 2 + 1) * 64 + lane], p);
+        for (; b < bmax; ++b) {   // < 8 left: Acc3 capacity holds
+            u64 p[VEC];
+            ld_diag<VEC>(pg[b] + off, p);
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) {
+                const Split30 y = split30(p[v]);
+                acc3_mac(a0[v], unpack30(sb[(b * 2 + 0) * W + lane * VEC + v]), y);
+                acc3_mac(a1[v], unpack30(sb[(b * 2 + 1) * W + lane * VEC + v]), y);
+            }
         }
-        inner[(size_t)g * 2 * S + off] = reduce128(c0.lo, c0.hi, P);
-        inner[(size_t)g * 2 * S + S + off] = reduce128(c1.lo, c1.hi, P);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+            acc3_fold(c0[v], a0[v]);
+            acc3_fold(c1[v], a1[v]);
+        }
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+            inner[(size_t)g * 2 * S + off + v] = reduce128(c0[v].lo, c0[v].hi, R);
+            inner[(size_t)g * 2 * S + S + off + v] = reduce128(c1[v].lo, c1[v].hi, R);
+        }
     }
 }
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
                              int D, int l, u64* inner, hipStream_t st, const KTimer* tm) {
-    if (T.N % 64 || G > 64) return hipErrorInvalidValue;
-    const size_t sh = (size_t)G * 128 * 8;
+    constexpr int VEC = FHS_INNER_VEC, W = 64 * VEC;
+    if (T.N % W || G > 64) return hipErrorInvalidValue;
+    const size_t sh = (size_t)G * 2 * W * 8;
+    static bool attr = false;
+    if (!attr) {   // dynamic LDS above 64 KiB must be opted into
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 2 * W * 8);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
     FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-    hipLaunchKernelGGL(k_bsgs_inner, dim3(T.N / 64, l), dim3(64 * FHS_INNER_WAVES), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
+    hipLaunchKernelGGL(k_bsgs_inner<VEC>, dim3(T.N / W, l), dim3(64 * FHS_INNER_WAVES), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
     FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
     return hipGetLastError();
 }

@@ -105,6 +105,40 @@ __host__ __device__ __forceinline__ u64 pm_reduce128(u64 lo, u64 hi, u64 q, unsi
 __device__ __forceinline__ u64 addmod(u64 a, u64 b, u64 q) { return csub(a + b, q); }
 __device__ __forceinline__ u64 submod(u64 a, u64 b, u64 q) { return a >= b ? a - b : a + q - b; }
 
+// Split-30 lazy accumulation of sums of 64x64 products for residues < 2^60 (every context prime
+// is < 2^60): x = x1 2^30 + x0 with x0, x1 < 2^30, so each partial product is < 2^60 and a plain
+// v_mad_u64_u32 accumulates it in 64 bits.  L, H take one partial per product, M two, so up to 8
+// products fit before acc3_fold must move the sums into a 128-bit accumulator: 4 multiply-adds per
+// product instead of a full 128-bit product and carry chain (~15 instructions).
+struct Acc3 {
+    u64 L, M, H;
+};
+struct Split30 {
+    uint32_t lo, hi;
+};
+__device__ __forceinline__ Split30 split30(u64 x) { return Split30{(uint32_t)x & 0x3FFFFFFFu, (uint32_t)(x >> 30)}; }
+__device__ __forceinline__ u64 pack30(u64 x) { return (u64)(((uint32_t)x) & 0x3FFFFFFFu) | ((x >> 30) << 32); }
+__device__ __forceinline__ Split30 unpack30(u64 p) { return Split30{(uint32_t)p, (uint32_t)(p >> 32)}; }
+__device__ __forceinline__ void acc3_mac(Acc3& a, Split30 x, Split30 y) {
+    a.L += mul32w(x.lo, y.lo);
+    a.M += mul32w(x.lo, y.hi);
+    a.M += mul32w(x.hi, y.lo);
+    a.H += mul32w(x.hi, y.hi);
+}
+// c += L + M 2^30 + H 2^60 (< 2^123 for 8 products), then clear
+__device__ __forceinline__ void acc3_fold(u128& c, Acc3& a) {
+    u64 lo = a.L, hi = 0;
+    u64 t = a.M << 30;
+    lo += t;
+    hi += (lo < t) + (a.M >> 34);
+    t = a.H << 60;
+    lo += t;
+    hi += (lo < t) + (a.H >> 4);
+    c.lo += lo;
+    c.hi += hi + (c.lo < lo);
+    a = Acc3{0, 0, 0};
+}
+
 // Per-prime constants, 64 B, kept in a device table indexed by key-level prime index.
 struct PrimeK {
     u64 q;

@@ -26,3 +26,17 @@ for name in names:
               f"smem {sum(v for k, v in c.items() if k.startswith('s_load'))} lds {sum(v for k, v in c.items() if k.startswith('ds_'))}")
         if "-v" in sys.argv:
             print("   ", c.most_common(30))
+
+if "-loops" in sys.argv:
+    for name in names:
+        for m in re.finditer(r"^(_Z\S*%s\S*):" % re.escape(name), s, re.M):
+            j = s.find("s_endpgm", m.end())
+            body = s[m.end():j].splitlines()
+            labels = [(i, l) for i, l in enumerate(body) if l.startswith(".LBB")] + [(len(body), "end")]
+            for (i, l), (i2, _) in zip(labels, labels[1:]):
+                seg = [x.strip().split()[0] for x in body[i + 1:i2] if x.strip() and not x.strip().startswith((".", ";"))]
+                c = collections.Counter(seg)
+                v = sum(n for k, n in c.items() if k.startswith("v_"))
+                if v >= 20:
+                    print(f"  {l.split()[0]:12s} valu {v:4d} mad64 {c['v_mad_u64_u32']:3d} mov {c['v_mov_b32_e32']:3d} "
+                          f"lds {sum(n for k, n in c.items() if k.startswith('ds_'))} vmem {sum(n for k, n in c.items() if k.startswith('global_'))} {l[l.find(';'):][:40] if ';' in l else ''}")
