@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <set>
@@ -209,6 +210,16 @@ struct fhs_context {
     std::vector<hipEvent_t> timer_open;                              // begin event per id
     std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> timer_pairs;
     fhs::KTimer ktimer{};
+    // pinned staging ring for launch descriptors (stage_h2d); wraps after a stream sync
+    unsigned char* ring = nullptr;
+    size_t ring_head = 0;
+    static constexpr size_t kRingBytes = 16u << 20;
+    fhs::Stager stager{};
+    // grow-only scratch buffers reused across calls (stream order makes reuse safe): a large
+    // hipMallocAsync costs ~0.7 ms/GB of host time and can wait on earlier frees
+    enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_COUNT };
+    uint64_t* scr[SCR_COUNT] = {};
+    size_t scr_bytes[SCR_COUNT] = {};
     static constexpr int kMaxItems = 512;
     static constexpr int kMaxPtrs = 1 << 16;
 };
@@ -263,6 +274,19 @@ static void dfree(fhs_context* c, void* p, size_t bytes) {
     c->bytes_live -= bytes;
 }
 
+static hipError_t scratch(fhs_context* c, int slot, size_t bytes, uint64_t** p) {
+    if (bytes > c->scr_bytes[slot]) {
+        if (c->scr[slot]) dfree(c, c->scr[slot], c->scr_bytes[slot]);
+        c->scr[slot] = nullptr;
+        c->scr_bytes[slot] = 0;
+        hipError_t e = dalloc(c, &c->scr[slot], bytes);
+        if (e != hipSuccess) return e;
+        c->scr_bytes[slot] = bytes;
+    }
+    *p = c->scr[slot];
+    return hipSuccess;
+}
+
 static fhs_status new_ct(fhs_context* c, int ncomp, int ci, double scale, fhs_ciphertext** out) {
     const int l = c->L0 + 1 - ci;
     if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
@@ -290,6 +314,43 @@ static fhs_status new_pt(fhs_context* c, int ci, double scale, fhs_plaintext** o
 static size_t ct_bytes(const fhs_ciphertext* ct) { return 8ull * ct->ncomp * ct->l * ct->ctx->N; }
 static size_t pt_bytes(const fhs_plaintext* pt) { return 8ull * pt->l * pt->ctx->N; }
 
+// ---------------------------------------------------------------- host-side latency trace
+// FHESPEAR_HOST_TRACE=1 prints the host time of each section of the BSGS entry point (stderr); used
+// to check that no call blocks on the GPU queue (tools/debug/host_timing.py).
+struct HostTrace {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    HostTrace() : on(getenv("FHESPEAR_HOST_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+    void mark(const char* what) {
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[fhs host] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+
+// ---------------------------------------------------------------- staging
+// Small host->device copies on the context stream.  A pageable-source hipMemcpyAsync returns only
+// once the copy has run, i.e. once the stream has drained up to it, which would serialise the host
+// with the GPU on every launch; staging through a pinned ring keeps the host ahead of the queue.
+// The ring is reused after one stream synchronisation per wrap (every few hundred BSGS steps).
+static hipError_t stage_h2d(void* user, void* dst, const void* src, size_t bytes) {
+    fhs_context* c = static_cast<fhs_context*>(user);
+    if (!c->ring || bytes > fhs_context::kRingBytes / 4) {
+        hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->st);
+        return e == hipSuccess ? hipStreamSynchronize(c->st) : e;
+    }
+    if (c->ring_head + bytes > fhs_context::kRingBytes) {
+        hipError_t e = hipStreamSynchronize(c->st);
+        if (e != hipSuccess) return e;
+        c->ring_head = 0;
+    }
+    unsigned char* p = c->ring + c->ring_head;
+    memcpy(p, src, bytes);
+    c->ring_head += (bytes + 255) & ~(size_t)255;
+    return hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, c->st);
+}
+
 // ---------------------------------------------------------------- deferred rotations
 static fhs_status flush(fhs_context* c) {
     if (c->pending.empty()) return FHS_OK;
@@ -307,11 +368,13 @@ static fhs_status flush(fhs_context* c) {
     const int U = (int)uniq.size();
     const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, U, l);
     uint64_t* ws = nullptr;
-    hipError_t e = dalloc(c, &ws, wsb);
+    HostTrace ht;
+    hipError_t e = scratch(c, fhs_context::SCR_KS, wsb, &ws);
+    ht.mark("flush: workspace");
     if (e != hipSuccess) return hip_fail(e, "key-switch workspace");
     e = fhs::launch_keyswitch(c->T, items.data(), R, reinterpret_cast<const fhs::u64* const*>(uniq.data()), U, l, ws,
-                              wsb, c->items_dev, c->st, c->timer_mask ? &c->ktimer : nullptr);
-    dfree(c, ws, wsb);
+                              wsb, c->items_dev, c->stager, c->st, c->timer_mask ? &c->ktimer : nullptr);
+    ht.mark("flush: launch keyswitch");
     c->pending.clear();
     c->pending_refs.clear();
     c->pending_outs.clear();
@@ -531,6 +594,9 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
     HIPCHK(up(rs.data(), 8 * rs.size(), (const void**)&T.rescale), "tables");
     HIPCHK(up(pow2.data(), 8 * pow2.size(), (const void**)&T.pow2), "tables");
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->ring), fhs_context::kRingBytes, hipHostMallocDefault),
+           "staging ring");
+    c->stager = fhs::Stager{c.get(), stage_h2d};
     HIPCHK(hipMalloc(&c->items_dev, (sizeof(KsItem) + sizeof(void*)) * fhs_context::kMaxItems), "items buffer");
     c->tables.push_back(c->items_dev);
     HIPCHK(hipMalloc(&c->ptrs_dev, sizeof(void*) * 2 * fhs_context::kMaxPtrs), "pointer buffer");
@@ -555,6 +621,9 @@ extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
         flush(c);
         hipStreamSynchronize(c->st);
         for (void* p : c->tables) hipFree(p);
+        for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
+            if (c->scr[k]) hipFree(c->scr[k]);
+        if (c->ring) hipHostFree(c->ring);
         for (auto& v : c->timer_pairs)
             for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
         hipStreamDestroy(c->st);
@@ -1228,10 +1297,9 @@ static fhs_status run_keyswitch(fhs_context* c, std::vector<KsItem>& items, int 
     }
     const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, R, l);
     uint64_t* ws = nullptr;
-    HIPCHK(dalloc(c, &ws, wsb), "key-switch workspace");
+    HIPCHK(scratch(c, fhs_context::SCR_KS, wsb, &ws), "key-switch workspace");
     hipError_t e = fhs::launch_keyswitch(c->T, items.data(), R, reinterpret_cast<const fhs::u64* const*>(uniq.data()), R,
-                                         l, ws, wsb, c->items_dev, c->st, nullptr);
-    dfree(c, ws, wsb);
+                                         l, ws, wsb, c->items_dev, c->stager, c->st, nullptr);
     if (e != hipSuccess) return hip_fail(e, "key-switch");
     return FHS_OK;
 }
@@ -1259,10 +1327,9 @@ extern "C" fhs_status fhs_rescale_to_next(fhs_context* c, const fhs_ciphertext* 
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, a->ncomp, a->ci + 1, a->scale / (double)c->q[a->l - 1], &r);
     if (s != FHS_OK) return s;
-    uint64_t* scratch = nullptr;
-    HIPCHK(dalloc(c, &scratch, 8ull * a->ncomp * c->N), "rescale");
-    HIPCHK(fhs::launch_rescale(c->T, a->d, r->d, scratch, a->ncomp, a->l, c->st), "rescale");
-    dfree(c, scratch, 8ull * a->ncomp * c->N);
+    uint64_t* scr = nullptr;
+    HIPCHK(scratch(c, fhs_context::SCR_RESCALE, 8ull * a->ncomp * c->N, &scr), "rescale");
+    HIPCHK(fhs::launch_rescale(c->T, a->d, r->d, scr, a->ncomp, a->l, c->st), "rescale");
     *out = r;
     return FHS_OK;
 }
@@ -1373,6 +1440,7 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
             return fail(FHS_ERR_LEVEL, "bsgs: baby steps and diagonals must share one chain index");
     }
     if (l < 2) return fail(FHS_ERR_LEVEL, "bsgs: no level left for the final rescale");
+    HostTrace ht;
     std::vector<const uint64_t*> keys(Beff, nullptr);
     for (int g = 1; g < Beff; ++g) {
         const uint64_t elt = fhs_galois_elt_from_step(g * G, c->N);
@@ -1385,30 +1453,33 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     std::vector<const uint64_t*> ptrs(G + D);
     for (int b = 0; b < G; ++b) ptrs[b] = baby[b]->d;
     for (int k = 0; k < D; ++k) ptrs[G + k] = pt_ptrs[k];
-    HIPCHK(hipMemcpyAsync(c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D), hipMemcpyHostToDevice, c->st), "bsgs");
+    ht.mark("keys+ptrs");
+    HIPCHK(stage_h2d(c, c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D)), "bsgs");
+    ht.mark("stage ptrs");
     const uint64_t* const* dbaby = reinterpret_cast<const uint64_t* const*>(c->ptrs_dev);
     const uint64_t* const* dpts = dbaby + G;
     uint64_t* inner = nullptr;
-    HIPCHK(dalloc(c, &inner, 8ull * Beff * 2 * S), "bsgs inner products");
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * Beff * 2 * S, &inner), "bsgs inner products");
     const fhs::KTimer* tm = c->timer_mask ? &c->ktimer : nullptr;
+    ht.mark("dalloc inner");
     HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dpts, G, Beff, D, l, inner, c->st, tm), "bsgs inner");
+    ht.mark("launch inner");
     const size_t wsb = fhs::bsgs_giant_workspace_bytes(c->T, Beff - 1, l);
     uint64_t* ws = nullptr;
-    HIPCHK(dalloc(c, &ws, wsb), "bsgs workspace");
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_WS, wsb, &ws), "bsgs workspace");
     uint64_t* sum = nullptr;
-    HIPCHK(dalloc(c, &sum, 16 * S), "bsgs sum");
-    HIPCHK(fhs::launch_bsgs_giant(c->T, inner, G, Beff, l, keys.data(), sum, ws, wsb, c->items_dev, c->st, tm),
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_SUM, 16 * S, &sum), "bsgs sum");
+    ht.mark("dalloc ws");
+    HIPCHK(fhs::launch_bsgs_giant(c->T, inner, G, Beff, l, keys.data(), sum, ws, wsb, c->items_dev, c->stager, c->st, tm),
            "bsgs giant");
-    dfree(c, ws, wsb);
-    dfree(c, inner, 8ull * Beff * 2 * S);
+    ht.mark("launch giant");
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, 2, ci + 1, baby[0]->scale * pt_scale / (double)c->q[l - 1], &r);
     if (s != FHS_OK) return s;
-    uint64_t* scratch = nullptr;
-    HIPCHK(dalloc(c, &scratch, 16ull * c->N), "bsgs rescale");
-    HIPCHK(fhs::launch_rescale(c->T, sum, r->d, scratch, 2, l, c->st, tm), "bsgs rescale");
-    dfree(c, scratch, 16ull * c->N);
-    dfree(c, sum, 16 * S);
+    uint64_t* scr = nullptr;
+    HIPCHK(scratch(c, fhs_context::SCR_RESCALE, 16ull * c->N, &scr), "bsgs rescale");
+    HIPCHK(fhs::launch_rescale(c->T, sum, r->d, scr, 2, l, c->st, tm), "bsgs rescale");
+    ht.mark("rescale+frees");
     *out = r;
     return FHS_OK;
 }

@@ -58,16 +58,24 @@ hipError_t launch_eltwise(const DevTables& T, int op, const u64* a, const u64* b
 hipError_t launch_tensor(const DevTables& T, const u64* a, const u64* b, u64* out3, int l, hipStream_t st);
 hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
                           hipStream_t st, const KTimer* tm = nullptr);
+// Stream-ordered host->device copy of small launch descriptors (item lists, pointer arrays).  The
+// host side stages through pinned memory so the copy never blocks the calling thread on the GPU
+// queue; `src` may be reused as soon as the call returns.
+struct Stager {
+    void* user;
+    hipError_t (*h2d)(void* user, void* dst, const void* src, size_t bytes);
+};
 // items_host[r].src must index uniq_host (U distinct inputs); items_dev holds >= R items + U pointers
 hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, const u64* const* uniq_host, int U,
-                            int l, u64* workspace, size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm);
+                            int l, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
+                            const KTimer* tm);
 size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l);
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
                              int D, int l, u64* inner, hipStream_t st, const KTimer* tm);
 // giant-step key-switches of inner[1..B-1] (rotation by g*G), summed with inner[0]; output 2 x l limbs
 hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
-                             u64* out, u64* workspace, size_t ws_bytes, void* items_dev, hipStream_t st,
-                             const KTimer* tm);
+                             u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg,
+                             hipStream_t st, const KTimer* tm);
 size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l);
 hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,

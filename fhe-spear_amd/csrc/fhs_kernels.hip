@@ -651,25 +651,26 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     *ycoef_out = ycoef;
 }
 
-static hipError_t upload_items(const KsItem* items, int R, const u64* const* uniq, int U, void* dev, hipStream_t st,
+static hipError_t upload_items(const KsItem* items, int R, const u64* const* uniq, int U, void* dev, const Stager& sg,
                                const KsItem** it_dev, const u64* const** uniq_dev) {
-    // one staging copy: [R items][U pointers]
+    // one staged copy: [R items][U pointers]
     static thread_local std::vector<unsigned char> buf;
     buf.resize(sizeof(KsItem) * R + sizeof(u64*) * U);
     memcpy(buf.data(), items, sizeof(KsItem) * R);
     memcpy(buf.data() + sizeof(KsItem) * R, uniq, sizeof(u64*) * U);
-    hipError_t e = hipMemcpyAsync(dev, buf.data(), buf.size(), hipMemcpyHostToDevice, st);
+    hipError_t e = sg.h2d(sg.user, dev, buf.data(), buf.size());
     *it_dev = reinterpret_cast<const KsItem*>(dev);
     *uniq_dev = reinterpret_cast<const u64* const*>(static_cast<unsigned char*>(dev) + sizeof(KsItem) * R);
     return e;
 }
 
 hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, const u64* const* uniq_host, int U,
-                            int l, u64* ws, size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm) {
+                            int l, u64* ws, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
+                            const KTimer* tm) {
     if (keyswitch_workspace_bytes(T, R, U, l) > ws_bytes) return hipErrorInvalidValue;
     const KsItem* it;
     const u64* const* uq;
-    hipError_t e = upload_items(items_host, R, uniq_host, U, items_dev, st, &it, &uq);
+    hipError_t e = upload_items(items_host, R, uniq_host, U, items_dev, sg, &it, &uq);
     if (e != hipSuccess) return e;
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
@@ -845,7 +846,8 @@ size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
 }
 
 hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
-                             u64* out, u64* ws, size_t ws_bytes, void* items_dev, hipStream_t st, const KTimer* tm) {
+                             u64* out, u64* ws, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
+                             const KTimer* tm) {
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
     if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
@@ -864,7 +866,7 @@ hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B,
     }
     const KsItem* it;
     const u64* const* uq;
-    hipError_t e = upload_items(items, R, uniq, R, items_dev, st, &it, &uq);
+    hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
     if (e != hipSuccess) return e;
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
