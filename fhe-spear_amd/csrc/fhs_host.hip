@@ -188,6 +188,10 @@ struct PendingRot {
 struct fhs_context {
     int device = 0;
     hipStream_t st = nullptr;
+    hipStream_t st_aux = nullptr;          // second stream of the pipelined BSGS (memory-bound kernels)
+    std::vector<hipEvent_t> bsgs_ev;       // cross-stream ordering events of launch_bsgs
+    int bsgs_chunks = 1;                   // FHESPEAR_BSGS_CHUNKS (overlap measured slower)
+    int bsgs_split_h = 0;                  // FHESPEAR_BSGS_SPLIT_H
     std::recursive_mutex mu;
     uint64_t N = 0;
     int logN = 0, L0 = 0, P = 0, K = 0, dnum = 0;
@@ -596,6 +600,11 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(pow2.data(), 8 * pow2.size(), (const void**)&T.pow2), "tables");
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->ring), fhs_context::kRingBytes, hipHostMallocDefault),
            "staging ring");
+    HIPCHK(hipStreamCreateWithFlags(&c->st_aux, hipStreamNonBlocking), "aux stream");
+    c->bsgs_ev.resize(2 + 2 * 16);
+    for (auto& ev : c->bsgs_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "bsgs events");
+    if (const char* ch = getenv("FHESPEAR_BSGS_CHUNKS")) c->bsgs_chunks = std::max(1, std::min(16, atoi(ch)));
+    if (const char* sh = getenv("FHESPEAR_BSGS_SPLIT_H")) c->bsgs_split_h = atoi(sh) != 0;
     c->stager = fhs::Stager{c.get(), stage_h2d};
     HIPCHK(hipMalloc(&c->items_dev, (sizeof(KsItem) + sizeof(void*)) * fhs_context::kMaxItems), "items buffer");
     c->tables.push_back(c->items_dev);
@@ -620,6 +629,9 @@ extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
         Guard g(c);
         flush(c);
         hipStreamSynchronize(c->st);
+        if (c->st_aux) hipStreamSynchronize(c->st_aux);
+        for (auto ev : c->bsgs_ev) hipEventDestroy(ev);
+        if (c->st_aux) hipStreamDestroy(c->st_aux);
         for (void* p : c->tables) hipFree(p);
         for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
             if (c->scr[k]) hipFree(c->scr[k]);
@@ -1461,18 +1473,18 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     uint64_t* inner = nullptr;
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * Beff * 2 * S, &inner), "bsgs inner products");
     const fhs::KTimer* tm = c->timer_mask ? &c->ktimer : nullptr;
-    ht.mark("dalloc inner");
-    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dpts, G, Beff, D, l, inner, c->st, tm), "bsgs inner");
-    ht.mark("launch inner");
-    const size_t wsb = fhs::bsgs_giant_workspace_bytes(c->T, Beff - 1, l);
+    const size_t wsb = std::max<size_t>(8, fhs::bsgs_workspace_bytes(c->T, Beff - 1, l));
     uint64_t* ws = nullptr;
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_WS, wsb, &ws), "bsgs workspace");
     uint64_t* sum = nullptr;
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_SUM, 16 * S, &sum), "bsgs sum");
-    ht.mark("dalloc ws");
-    HIPCHK(fhs::launch_bsgs_giant(c->T, inner, G, Beff, l, keys.data(), sum, ws, wsb, c->items_dev, c->stager, c->st, tm),
-           "bsgs giant");
-    ht.mark("launch giant");
+    ht.mark("workspaces");
+    const fhs::BsgsStreams ss{c->st, c->st_aux, c->bsgs_ev.data(), (int)c->bsgs_ev.size(), c->bsgs_chunks,
+                              c->bsgs_split_h};
+    HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), inner, sum, ws, wsb, c->items_dev,
+                            c->stager, ss, tm),
+           "bsgs");
+    ht.mark("launch bsgs");
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, 2, ci + 1, baby[0]->scale * pt_scale / (double)c->q[l - 1], &r);
     if (s != FHS_OK) return s;

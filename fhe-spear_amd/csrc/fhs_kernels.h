@@ -77,6 +77,19 @@ hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B,
                              u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg,
                              hipStream_t st, const KTimer* tm);
 size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l);
+// Two-stream pipelined Hadamard + giant steps (fhs_kernels.hip launch_bsgs).  ev holds nev >= 4
+// events (2 + 2 * chunks used); the result is ordered on `main` when the call returns.
+struct BsgsStreams {
+    hipStream_t main, aux;
+    const hipEvent_t* ev;
+    int nev;
+    int chunks;
+    int split_hadamard;   // 1: Hadamard per chunk on the aux stream; 0: one Hadamard launch on main
+};
+size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
+hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
+                       int l, const u64* const* keys_host, u64* inner, u64* out, u64* workspace, size_t ws_bytes,
+                       void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
 hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st);

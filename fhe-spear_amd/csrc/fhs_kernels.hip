@@ -15,6 +15,7 @@
 
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 // build-time tuning knobs (A/B variants are built with -D...; defaults are the shipped choice)
 #ifndef FHS_INNER_WAVES
@@ -33,7 +34,7 @@
 #define FHS_MODUP_CH 4
 #endif
 #ifndef FHS_MODUP_RL
-#define FHS_MODUP_RL 3         // radix (log2) of the register passes in k_modup's NTT
+#define FHS_MODUP_RL 4         // radix (log2) of the register passes in k_modup's NTT
 #endif
 #ifndef FHS_NTT_RL
 #define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
@@ -700,8 +701,8 @@ __device__ __forceinline__ void ld_diag(const u64* p, u64* out) {
 }
 template <int VEC>
 __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
-                                                    const u64* const* __restrict__ pts, int G, int B, int D, int l,
-                                                    u64* __restrict__ inner) {
+                                                    const u64* const* __restrict__ pts, int G, int g0, int g1, int D,
+                                                    int l, u64* __restrict__ inner) {
     extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][W], split-30 packed
     constexpr int W = 64 * VEC;
     const int N = T.N;
@@ -714,7 +715,7 @@ __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T
     __syncthreads();
     const RedU R = redu(PK(T, i));
     const size_t off = (size_t)i * N + n0 + lane * VEC;
-    for (int g = wave; g < B; g += FHS_INNER_WAVES) {
+    for (int g = g0 + wave; g < g1; g += FHS_INNER_WAVES) {
         const int bmax = min(G, D - g * G);
         if (bmax <= 0) continue;
         u128 c0[VEC], c1[VEC];
@@ -780,7 +781,7 @@ hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, con
         attr = true;
     }
     FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-    hipLaunchKernelGGL(k_bsgs_inner<VEC>, dim3(T.N / W, l), dim3(64 * FHS_INNER_WAVES), sh, st, T, baby_dev, pts_dev, G, B, D, l, inner);
+    hipLaunchKernelGGL(k_bsgs_inner<VEC>, dim3(T.N / W, l), dim3(64 * FHS_INNER_WAVES), sh, st, T, baby_dev, pts_dev, G, 0, B, D, l, inner);
     FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
     return hipGetLastError();
 }
@@ -790,7 +791,7 @@ hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, con
 // is bit-identical to rotating and adding one giant step at a time (bg:478-483).
 // base_c = (sum_r acc_r,c) P^-1 + [c==0] sum_r galois_r(inner_r.c0) + inner_0.c ;  convsum_c = sum_r conv(y_r,c)
 __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, const u64* ycoef, const u64* inner0,
-                            u64* base, u64* convsum, int l, int R) {
+                            u64* base, u64* convsum, int l, int R, int first) {
     const int N = T.N, P_ = T.P, E = l + P_;
     const size_t S = (size_t)l * N;
     const size_t total = 2 * S;
@@ -801,7 +802,7 @@ __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, co
         const PrimeK& P = PK(T, i);
         const u64 q = P.q;
         u128 cs = {0, 0};
-        u64 as = 0, add = inner0[(size_t)comp * S + (size_t)i * N + n];
+        u64 as = 0, add = first ? inner0[(size_t)comp * S + (size_t)i * N + n] : 0;
         int cnt = 0;
         for (int r = 0; r < R; ++r) {
             const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N + n;
@@ -815,8 +816,15 @@ __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, co
                 add = addmod(add, it.add0[(size_t)i * N + galois_src(n, it.elt, T.logN)], q);
             }
         }
-        convsum[idx] = reduce128(cs.lo, cs.hi, P);
-        base[idx] = addmod(shoup(as, T.md_pinv[2 * i], T.md_pinv[2 * i + 1], q), add, q);
+        // chunks of rotations accumulate mod q: both sums are linear in the rotations
+        u64 cv = reduce128(cs.lo, cs.hi, P);
+        u64 bv = addmod(shoup(as, T.md_pinv[2 * i], T.md_pinv[2 * i + 1], q), add, q);
+        if (!first) {
+            cv = addmod(cv, convsum[idx], q);
+            bv = addmod(bv, base[idx], q);
+        }
+        convsum[idx] = cv;
+        base[idx] = bv;
     }
 }
 template <int LOGN>
@@ -839,6 +847,153 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_giant_final(DevTables T, c
         const u64 v = fwd_canon(lds[lds_pad(e)], RU);
         out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, P.q), P.q);
     }
+}
+
+// ---- key-switch stages on explicit buffers (the pipelined BSGS launcher runs them per chunk)
+struct KsBufs {
+    u64 *acoef, *ext, *acc, *ycoef;
+    unsigned char* vcnt;
+};
+static KsBufs ks_carve(const DevTables& T, u64* ws, int R, int U, int l) {
+    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
+    KsBufs b;
+    b.acoef = ws;
+    b.ext = b.acoef + (size_t)U * l * N;
+    b.acc = b.ext + (size_t)U * dn * E * N;
+    b.ycoef = b.acc + (size_t)R * 2 * E * N;
+    b.vcnt = reinterpret_cast<unsigned char*>(b.ycoef + (size_t)R * 2 * T.P * N);
+    return b;
+}
+// view of items [r0, ..) with inputs [u0, ..): items' src must then be relative to u0
+static KsBufs ks_at(const DevTables& T, const KsBufs& b, int r0, int u0, int l) {
+    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
+    return KsBufs{b.acoef + (size_t)u0 * l * N, b.ext + (size_t)u0 * dn * E * N, b.acc + (size_t)r0 * 2 * E * N,
+                  b.ycoef + (size_t)r0 * 2 * T.P * N, b.vcnt + (size_t)u0 * dn * N};
+}
+template <int LOGN>
+static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, int l, const KsBufs& b, hipStream_t st,
+                           const KTimer* tm) {
+    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
+    const dim3 blk((1 << LOGN) / 16);
+    FHS_TMARK(tm, KID_KS_INTT, 1, st);
+    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, b.acoef, l, U);
+    hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, b.acoef, b.vcnt, l, U);
+    FHS_TMARK(tm, KID_KS_INTT, 0, st);
+    FHS_TMARK(tm, KID_MODUP, 1, st);
+    hipLaunchKernelGGL((k_modup<LOGN>), dim3(FHS_MODUP_MAP == 1 ? xcd_grid((int)E, (int)(dn * U)) : FHS_MODUP_MAP == 2 ? xcd_grid_m((int)E, (int)(dn * U)) : (int)(E * dn * U)),
+                       blk, 0, st, T, uniq, b.acoef, b.vcnt, b.ext, l, U);
+    FHS_TMARK(tm, KID_MODUP, 0, st);
+}
+template <int LOGN>
+static void ks_ip_stage(const DevTables& T, const KsItem* it, int R, int l, const KsBufs& b, hipStream_t st,
+                        const KTimer* tm) {
+    const size_t N = T.N, E = l + T.P;
+    FHS_TMARK(tm, KID_KS_IP, 1, st);
+    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid((int)E, R * (int)(N >> 8))), dim3(256), 0, st, T, it, b.ext, b.acc, l, R);
+    FHS_TMARK(tm, KID_KS_IP, 0, st);
+    FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
+    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3((1 << LOGN) / 16), 0, st, T, b.acc, b.ycoef, l, R);
+    FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
+}
+
+// Pipelined BSGS (Hadamard + giant steps) on two streams.  The giant rotations are cut into
+// `chunks` groups; the aux stream runs the memory-bound kernels (Hadamard chunk c, then key inner
+// products + giant sums), the main stream the VALU-bound ones (INTT, centred ModUp + NTT), so one
+// chunk's ModUp overlaps the next chunk's Hadamard and the previous chunk's inner product.  Chunks
+// only reorder independent work: the limbs are identical to the serial schedule.
+size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) { return bsgs_giant_workspace_bytes(T, R, l); }
+hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
+                       int l, const u64* const* keys_host, u64* inner, u64* out, u64* ws, size_t ws_bytes,
+                       void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm) {
+    constexpr int VEC = FHS_INNER_VEC, W = 64 * VEC;
+    const int R = B - 1;
+    const size_t N = T.N, S = (size_t)l * N;
+    if (T.N % W || G > 64 || R > 512) return hipErrorInvalidValue;
+    if (R > 0 && bsgs_giant_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
+    const int C = R > 0 ? std::max(1, std::min(ss.chunks, std::min(R, (ss.nev - 2) / 2))) : 1;
+    hipStream_t sm = ss.main, sa = ss.aux;
+    hipEvent_t ev_start = ss.ev[0], ev_end = ss.ev[1];
+    const hipEvent_t* evH = ss.ev + 2;
+    const hipEvent_t* evF = ss.ev + 2 + C;
+    // chunk c covers giant rotations r in [rb(c), rb(c+1)), i.e. giant groups g = r + 1
+    auto rb = [&](int c) { return (int)((long long)c * R / C); };
+    KsItem items[512];
+    const u64* uniq[512];
+    for (int c = 0; c < C; ++c)
+        for (int r = rb(c); r < rb(c + 1); ++r) {
+            const int g = r + 1;
+            const u64* ct = inner + (size_t)g * 2 * S;
+            u64 elt = 1;
+            for (int s2 = 0; s2 < g * G; ++s2) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
+            items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)(r - rb(c))};
+            uniq[r] = ct + S;
+        }
+    const KsItem* it = nullptr;
+    const u64* const* uq = nullptr;
+    if (R > 0) {
+        hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
+        if (e != hipSuccess) return e;
+    }
+    const size_t sh = (size_t)G * 2 * W * 8;
+    static bool attr = false;
+    if (!attr) {   // dynamic LDS above 64 KiB must be opted into
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 2 * W * 8);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    // Hadamard: either one launch on the main stream, or (split_hadamard) one launch per chunk on
+    // the aux stream (chunk 0 also produces g = 0, which needs no rotation)
+    hipStream_t sh_st = ss.split_hadamard ? sa : sm;
+    if (ss.split_hadamard) {
+        hipEventRecord(ev_start, sm);
+        hipStreamWaitEvent(sa, ev_start, 0);
+    }
+    for (int c = 0; c < (ss.split_hadamard ? C : 1); ++c) {
+        const int g0 = c == 0 ? 0 : rb(c) + 1, g1 = (R > 0 && ss.split_hadamard) ? rb(c + 1) + 1 : B;
+        FHS_TMARK(tm, KID_BSGS_INNER, 1, sh_st);
+        hipLaunchKernelGGL(k_bsgs_inner<VEC>, dim3(T.N / W, l), dim3(64 * FHS_INNER_WAVES), sh, sh_st, T, baby_dev,
+                           pts_dev, G, g0, g1, D, l, inner);
+        FHS_TMARK(tm, KID_BSGS_INNER, 0, sh_st);
+        hipEventRecord(evH[c], sh_st);
+    }
+    if (!ss.split_hadamard)
+        for (int c = 1; c < C; ++c) hipEventRecord(evH[c], sm);
+    hipEventRecord(ev_start, sm);
+    hipStreamWaitEvent(sa, ev_start, 0);
+    if (R <= 0) {
+        hipEventRecord(ev_end, sa);
+        hipStreamWaitEvent(sm, ev_end, 0);
+        return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, sm);
+    }
+    u64* base = ws + keyswitch_workspace_bytes(T, R, R, l) / 8;
+    u64* convsum = base + 2 * S;
+    FHS_DISPATCH_LOGN(T.logN, {
+        const KsBufs all = ks_carve(T, ws, R, R, l);
+        // main: INTT + centred ModUp + NTT per chunk, as soon as its inner products exist
+        for (int c = 0; c < C; ++c) {
+            hipStreamWaitEvent(sm, evH[c], 0);
+            ks_modup_stage<LOGN>(T, uq + rb(c), rb(c + 1) - rb(c), l, ks_at(T, all, rb(c), rb(c), l), sm, tm);
+            hipEventRecord(evF[c], sm);
+        }
+        // aux: key inner product, special-limb INTT and the running giant sum per chunk
+        for (int c = 0; c < C; ++c) {
+            const int Rc = rb(c + 1) - rb(c);
+            const KsBufs bc = ks_at(T, all, rb(c), rb(c), l);
+            hipStreamWaitEvent(sa, evF[c], 0);
+            ks_ip_stage<LOGN>(T, it + rb(c), Rc, l, bc, sa, tm);
+            FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
+            hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, it + rb(c), bc.acc, bc.ycoef,
+                               inner, base, convsum, l, Rc, c == 0 ? 1 : 0);
+            FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
+        }
+        hipEventRecord(ev_end, sa);
+        hipStreamWaitEvent(sm, ev_end, 0);
+        FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
+        hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3((1 << LOGN) / 16), 0, sm, T, base, convsum, out, l);
+        FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
+    });
+    return hipGetLastError();
 }
 
 size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
@@ -873,7 +1028,7 @@ hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B,
         ks_front<LOGN>(T, it, uq, R, R, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_GIANT_SUM, 1, st);
         hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, st, T, it, acc, ycoef, inner, base,
-                           convsum, l, R);
+                           convsum, l, R, 1);
         FHS_TMARK(tm, KID_GIANT_SUM, 0, st);
         FHS_TMARK(tm, KID_GIANT_FINAL, 1, st);
         hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3((1 << LOGN) / 16), 0, st, T, base, convsum, out, l);
