@@ -70,12 +70,7 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
                             int l, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
                             const KTimer* tm);
 size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l);
-hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
-                             int D, int l, u64* inner, hipStream_t st, const KTimer* tm);
-// giant-step key-switches of inner[1..B-1] (rotation by g*G), summed with inner[0]; output 2 x l limbs
-hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
-                             u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg,
-                             hipStream_t st, const KTimer* tm);
+
 size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l);
 // Two-stream pipelined Hadamard + giant steps (fhs_kernels.hip launch_bsgs).  ev holds nev >= 4
 // events (2 + 2 * chunks used); the result is ordered on `main` when the call returns.

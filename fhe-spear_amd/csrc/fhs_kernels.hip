@@ -452,12 +452,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     const int j = mi % dn, u = mi / dn;
     const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
     u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
-    if (t >= s0 && t < s1) {   // own limb: plain copy (whole block takes this branch)
-        const u64* src = uniq[u] + (size_t)t * N;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) o[tid + c * TH] = src[tid + c * TH];
-        return;
-    }
+    if (t >= s0 && t < s1) return;   // own limb: k_ks_ip reads it from the input itself
     const int pt = t < l ? t : T.L0 + (t - l);
     const PrimeK& PM = PK(T, pt);
     const u64 m = PM.q;
@@ -518,12 +513,18 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 // (bit-reversed order: the low 6 bits of the slot index are the top 6 bits of the evaluation
 // exponent, which k * (.) permutes among themselves), so each wave's gather touches exactly one
 // 512-byte region: four whole cache lines, no amplification.
-__global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items, const u64* ext, u64* acc, int l,
-                                                int R) {
+// Limbs t >= t0 only (the giant-step path sums limbs t < l over rotations in k_ks_ip_sum).  A digit's
+// own limbs were not extended (k_modup skips them): they are read from the input itself.
+__device__ __forceinline__ const u64* ks_src(const u64* ext_tj, const u64* own_t, int t, int j, int P_, int l) {
+    return (t >= j * P_ && t < min(j * P_ + P_, l)) ? own_t : ext_tj;
+}
+__global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items, const u64* const* uniq, const u64* ext,
+                                                u64* acc, int l, int R, int t0) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
     int t, m;
-    if (!xcd_touter(E, R * NB, t, m)) return;   // rotations of one limb t run together on one XCD
+    if (!xcd_touter(E - t0, R * NB, t, m)) return;   // rotations of one limb t run together on one XCD
+    t += t0;
     const int r = m / NB, n = ((m % NB) << 8) + threadIdx.x;
     const size_t per_r = (size_t)E * N;
     const int pt = t < l ? t : T.L0 + (t - l);
@@ -531,12 +532,13 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     const KsItem it = items[r];
     const int sn = galois_src(n, it.elt, T.logN);
     const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
+    const u64* own = uniq[it.src] + (size_t)t * N + sn;
     const u64* key = it.key + (size_t)pt * N + n;
     u128 c0 = {0, 0}, c1 = {0, 0};
     Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
 #pragma unroll 4
     for (int j = 0; j < dn; ++j) {
-        const Split30 v = split30(ex[(size_t)j * per_r]);
+        const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
         acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j) * K * N)));
         acc3_mac(a1, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N)));
         if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
@@ -548,6 +550,50 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     acc3_fold(c1, a1);
     acc[(((size_t)r * 2 + 0) * E + t) * N + n] = reduce128(c0.lo, c0.hi, RD);
     acc[(((size_t)r * 2 + 1) * E + t) * N + n] = reduce128(c1.lo, c1.hi, RD);
+}
+
+// Giant steps, limbs t < l: the key inner products of all R rotations summed in place, already
+// scaled by P^-1 and with the rotated c0's added (comp 0) -- the t < l part of
+// sum_r ModDown(acc_r) + sigma_r(c0_r) (k_giant_sum adds the special-limb conversion).  Writes
+// bpart[c][t][n] into the r = 0 slot of acc (acc[0][c][t], t < l), which nothing else uses.
+__global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* items, const u64* const* uniq,
+                                                    const u64* ext, u64* acc, int l, int R) {
+    const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    const int NB = N >> 8;
+    int t, m;
+    if (!xcd_touter(l, NB, t, m)) return;
+    const int n = (m << 8) + threadIdx.x;
+    const size_t per_r = (size_t)E * N;
+    const RedU RD = redu(PK(T, t));
+    const u64 q = RD.q;
+    u64 s0 = 0, s1 = 0, sadd = 0;
+    for (int r = 0; r < R; ++r) {
+        const KsItem it = items[r];
+        const int sn = galois_src(n, it.elt, T.logN);
+        const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
+        const u64* own = uniq[it.src] + (size_t)t * N + sn;
+        const u64* key = it.key + (size_t)t * N + n;
+        u128 c0 = {0, 0}, c1 = {0, 0};
+        Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
+#pragma unroll 4
+        for (int j = 0; j < dn; ++j) {
+            const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
+            acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j) * K * N)));
+            acc3_mac(a1, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N)));
+            if ((j & 7) == 7) {
+                acc3_fold(c0, a0);
+                acc3_fold(c1, a1);
+            }
+        }
+        acc3_fold(c0, a0);
+        acc3_fold(c1, a1);
+        s0 = addmod(s0, reduce128(c0.lo, c0.hi, RD), q);
+        s1 = addmod(s1, reduce128(c1.lo, c1.hi, RD), q);
+        sadd = addmod(sadd, it.add0[(size_t)t * N + sn], q);
+    }
+    const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
+    acc[((size_t)0 * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
+    acc[((size_t)1 * E + t) * N + n] = shoup(s1, pinv, pinv_s, q);
 }
 
 // (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
@@ -643,7 +689,8 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     hipLaunchKernelGGL((k_modup<LOGN>), dim3(FHS_MODUP_MAP == 1 ? xcd_grid((int)E, (int)(dn * U)) : FHS_MODUP_MAP == 2 ? xcd_grid_m((int)E, (int)(dn * U)) : (int)(E * dn * U)), blk, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     FHS_TMARK(tm, KID_MODUP, 0, st);
     FHS_TMARK(tm, KID_KS_IP, 1, st);
-    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid((int)E, R * (int)(N >> 8))), dim3(256), 0, st, T, it, ext, acc, l, R);
+    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid((int)E, R * (int)(N >> 8))), dim3(256), 0, st, T, it, uniq, ext, acc, l, R,
+                       0);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
     hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), blk, 0, st, T, acc, ycoef, l, R);
@@ -768,30 +815,13 @@ __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T
         }
     }
 }
-hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B,
-                             int D, int l, u64* inner, hipStream_t st, const KTimer* tm) {
-    constexpr int VEC = FHS_INNER_VEC, W = 64 * VEC;
-    if (T.N % W || G > 64) return hipErrorInvalidValue;
-    const size_t sh = (size_t)G * 2 * W * 8;
-    static bool attr = false;
-    if (!attr) {   // dynamic LDS above 64 KiB must be opted into
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 2 * W * 8);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-    hipLaunchKernelGGL(k_bsgs_inner<VEC>, dim3(T.N / W, l), dim3(64 * FHS_INNER_WAVES), sh, st, T, baby_dev, pts_dev, G, 0, B, D, l, inner);
-    FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
-    return hipGetLastError();
-}
 
 // Giant steps.  Exactness: every output limb is a sum of exact residues, so
 //   sum_r ModDown(acc_r) = (sum_r acc_r - NTT(sum_r conv(y_r))) * P^-1   (mod q_i)
 // is bit-identical to rotating and adding one giant step at a time (bg:478-483).
 // base_c = (sum_r acc_r,c) P^-1 + [c==0] sum_r galois_r(inner_r.c0) + inner_0.c ;  convsum_c = sum_r conv(y_r,c)
-__global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, const u64* ycoef, const u64* inner0,
-                            u64* base, u64* convsum, int l, int R, int first) {
+__global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, const u64* inner0, u64* base,
+                            u64* convsum, int l, int R, int first) {
     const int N = T.N, P_ = T.P, E = l + P_;
     const size_t S = (size_t)l * N;
     const size_t total = 2 * S;
@@ -802,7 +832,6 @@ __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, co
         const PrimeK& P = PK(T, i);
         const u64 q = P.q;
         u128 cs = {0, 0};
-        u64 as = 0, add = first ? inner0[(size_t)comp * S + (size_t)i * N + n] : 0;
         int cnt = 0;
         for (int r = 0; r < R; ++r) {
             const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N + n;
@@ -810,16 +839,13 @@ __global__ void k_giant_sum(DevTables T, const KsItem* items, const u64* acc, co
                 mac128(cs, y[(size_t)k * N], T.md_hat[(size_t)k * T.L0 + i]);
                 if (++cnt == 48) { cs.lo = reduce128(cs.lo, cs.hi, P); cs.hi = 0; cnt = 0; }
             }
-            as = addmod(as, acc[(((size_t)r * 2 + comp) * E + i) * N + n], q);
-            if (comp == 0) {
-                const KsItem it = items[r];
-                add = addmod(add, it.add0[(size_t)i * N + galois_src(n, it.elt, T.logN)], q);
-            }
         }
         // chunks of rotations accumulate mod q: both sums are linear in the rotations
         u64 cv = reduce128(cs.lo, cs.hi, P);
-        u64 bv = addmod(shoup(as, T.md_pinv[2 * i], T.md_pinv[2 * i + 1], q), add, q);
-        if (!first) {
+        u64 bv = bpart[((size_t)comp * E + i) * N + n];
+        if (first) {
+            bv = addmod(bv, inner0[idx], q);
+        } else {
             cv = addmod(cv, convsum[idx], q);
             bv = addmod(bv, base[idx], q);
         }
@@ -885,11 +911,12 @@ static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, in
     FHS_TMARK(tm, KID_MODUP, 0, st);
 }
 template <int LOGN>
-static void ks_ip_stage(const DevTables& T, const KsItem* it, int R, int l, const KsBufs& b, hipStream_t st,
-                        const KTimer* tm) {
-    const size_t N = T.N, E = l + T.P;
+static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* const* uniq, int R, int l, const KsBufs& b,
+                           hipStream_t st, const KTimer* tm) {
+    const int NB = T.N >> 8;
     FHS_TMARK(tm, KID_KS_IP, 1, st);
-    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid((int)E, R * (int)(N >> 8))), dim3(256), 0, st, T, it, b.ext, b.acc, l, R);
+    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(T.P, R * NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R, l);
+    hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
     hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3((1 << LOGN) / 16), 0, st, T, b.acc, b.ycoef, l, R);
@@ -981,10 +1008,10 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             const int Rc = rb(c + 1) - rb(c);
             const KsBufs bc = ks_at(T, all, rb(c), rb(c), l);
             hipStreamWaitEvent(sa, evF[c], 0);
-            ks_ip_stage<LOGN>(T, it + rb(c), Rc, l, bc, sa, tm);
+            giant_ip_stage<LOGN>(T, it + rb(c), uq + rb(c), Rc, l, bc, sa, tm);
             FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
-            hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, it + rb(c), bc.acc, bc.ycoef,
-                               inner, base, convsum, l, Rc, c == 0 ? 1 : 0);
+            hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, bc.acc, bc.ycoef, inner, base,
+                               convsum, l, Rc, c == 0 ? 1 : 0);
             FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
         }
         hipEventRecord(ev_end, sa);
@@ -1000,42 +1027,6 @@ size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
     return keyswitch_workspace_bytes(T, R, R, l) + 8 * (size_t)T.N * 4 * l;
 }
 
-hipError_t launch_bsgs_giant(const DevTables& T, const u64* inner, int G, int B, int l, const u64* const* keys_host,
-                             u64* out, u64* ws, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
-                             const KTimer* tm) {
-    const int R = B - 1;
-    const size_t N = T.N, S = (size_t)l * N;
-    if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
-    if (bsgs_giant_workspace_bytes(T, R, l) > ws_bytes || R > 512) return hipErrorInvalidValue;
-    u64* base = ws + keyswitch_workspace_bytes(T, R, R, l) / 8;
-    u64* convsum = base + 2 * S;
-    KsItem items[512];
-    const u64* uniq[512];
-    for (int r = 0; r < R; ++r) {
-        const int g = r + 1;
-        const u64* ct = inner + (size_t)g * 2 * S;
-        u64 elt = 1;
-        for (int s = 0; s < g * G; ++s) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
-        items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)r};
-        uniq[r] = ct + S;
-    }
-    const KsItem* it;
-    const u64* const* uq;
-    hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
-    if (e != hipSuccess) return e;
-    FHS_DISPATCH_LOGN(T.logN, {
-        u64 *acc, *ycoef;
-        ks_front<LOGN>(T, it, uq, R, R, l, ws, st, tm, &acc, &ycoef);
-        FHS_TMARK(tm, KID_GIANT_SUM, 1, st);
-        hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, st, T, it, acc, ycoef, inner, base,
-                           convsum, l, R, 1);
-        FHS_TMARK(tm, KID_GIANT_SUM, 0, st);
-        FHS_TMARK(tm, KID_GIANT_FINAL, 1, st);
-        hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3((1 << LOGN) / 16), 0, st, T, base, convsum, out, l);
-        FHS_TMARK(tm, KID_GIANT_FINAL, 0, st);
-    });
-    return hipGetLastError();
-}
 
 // ============================================================================ sampling / keys
 __device__ __forceinline__ u64 sm64(u64 x) {
