@@ -80,8 +80,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rotations", type=int, default=24)
-    ap.add_argument("--cpu-sample-diagonals", type=int, default=512)
+    ap.add_argument("--cpu-sample-rotations", type=int, default=32)
+    ap.add_argument("--cpu-sample-diagonals", type=int, default=768)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -188,6 +188,11 @@ def main():
                 rows[name] = {"ms_per_step": round(ms / prof_steps, 3), "launches_per_step": n // prof_steps,
                               "share": round(ms / sum(v[0] for v in kprof.values()), 3)}
 
+        traffic = {}
+        tpath = REPO / "profiles" / "r01" / "pmc_traffic_cfg2.json"
+        if args.config == "cfg2" and tpath.exists():
+            traffic = json.loads(tpath.read_text())["kernels"]
+
         def roofline_of(name):
             ms, n = ktimes[name]
             ab = algorithmic_bytes_per_matvec(name, cfg, l)
@@ -195,8 +200,12 @@ def main():
                 return None
             launches = n // args.steps
             ach = ab / (ms / args.steps * 1e-3) / 1e9
+            # traffic: HBM-side bytes per launch from the committed rocprofv3 PMC passes of this
+            # workload (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py); null when absent
+            tr = traffic.get(name)
+            tr_b = int(tr["traffic_bytes_per_step"] / max(tr["launches_per_step"], 1)) if tr else None
             return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr_b,
                     "bytes_per_launch": ab // max(launches, 1), "ms_per_launch": round(ms / n, 4)}
 
         roof = roofline_of(dom)
