@@ -24,6 +24,15 @@
 #ifndef FHS_INNER_VEC
 #define FHS_INNER_VEC 2       // consecutive coefficients per lane in k_bsgs_inner (2: 16-byte loads)
 #endif
+#ifndef FHS_MODUP_HALF
+#define FHS_MODUP_HALF 1      // k_modup_h: half-limb LDS, two workgroups per CU
+#endif
+#ifndef FHS_MODUPH_CH
+#define FHS_MODUPH_CH 2
+#endif
+#ifndef FHS_MODUPH_RL
+#define FHS_MODUPH_RL 3
+#endif
 #ifndef FHS_MODUP_MAP
 #define FHS_MODUP_MAP 2     // block->(limb, input) map of k_modup: 0 plain, 1 XCD t-inner, 2 XCD m-major
 #endif
@@ -498,13 +507,121 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     }
     __syncthreads();
 #ifndef FHS_EXP_NONTT
+#ifdef FHS_EXP_TW0
+    ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd, m, R.lazy);   // experiment: one shared table
+#else
     ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m, R.lazy);
+#endif
 #endif
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
         o[e] = fwd_canon(lds[lds_pad(e)], R);
     }
+}
+
+// (b1') ModUp + NTT with half the limb in LDS (68 KiB at N = 16384): two workgroups share a CU,
+// so one's loads and base conversion overlap the other's NTT.  Stage 0 of the forward NTT pairs
+// coefficient e with e + N/2; each thread converts both, applies that butterfly in registers, keeps
+// the upper half in registers while the lower half is transformed in LDS, then transforms it.
+// Same values as k_modup (same butterflies, same lazy bounds: < q + 2 q log N).
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
+                                                                 const u64* acoef, const unsigned char* vcnt, u64* ext,
+                                                                 int l, int U) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;   // 16 coefficient pairs per thread
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
+    const int tid = threadIdx.x;
+    const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    int t, mi;
+#if FHS_MODUP_MAP == 1
+    if (!xcd_tinner(E, dn * U, t, mi)) return;
+#elif FHS_MODUP_MAP == 2
+    if (!xcd_mmajor(E, dn * U, t, mi)) return;
+#else
+    if (!plain_tm(E, dn * U, t, mi)) return;
+#endif
+    const int j = mi % dn, u = mi / dn;
+    const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
+    u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
+    if (t >= s0 && t < s1) return;   // own limb: k_ks_ip reads it from the input itself
+    const int pt = t < l ? t : T.L0 + (t - l);
+    const PrimeK& PM = PK(T, pt);
+    const u64 m = PM.q;
+    const u64* yb = acoef + ((size_t)u * l + s0) * N;
+    const u64* hat = T.modup_hat + (((size_t)l * T.dnum + j) * P_) * K + pt;
+    const u64* qv = T.modup_Q + (((size_t)l * T.dnum + j) * K + pt) * 2;
+    const u64 Qm = qv[0], nsQm = qv[1];
+    const unsigned char* vb = vcnt + ((size_t)u * dn + j) * N;
+    const RedU R = redu(PM);
+    const u64* tw = T.tw_fwd + (size_t)pt * N * 2;
+    u64 w0, w0p;
+    ld_tw(tw, 1, w0, w0p);
+    const u64 q2 = 2 * m;
+    constexpr int CH = FHS_MODUPH_CH;   // coefficient pairs per conversion chunk
+    u64 hi[16];
+#pragma unroll
+    for (int ch = 0; ch < 16 / CH; ++ch) {
+        Acc3 a3[2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) a3[k] = Acc3{0, 0, 0};
+#pragma unroll 1
+        for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
+            const Split30 hw = split30(hat[(size_t)w * K]);
+            const u64* yw = yb + (size_t)w * N + tid;
+            u64 y[2 * CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                y[k] = yw[(ch * CH + k) * TH];
+                y[CH + k] = yw[(ch * CH + k) * TH + NH];
+            }
+#pragma unroll
+            for (int k = 0; k < 2 * CH; ++k) acc3_mac(a3[k], split30(y[k]), hw);
+        }
+        u64 x[2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) {
+            const int e = tid + (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);
+            u128 acc = {0, 0};
+            acc3_fold(acc, a3[k]);
+            mac128(acc, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
+            x[k] = submod(reduce128(acc.lo, acc.hi, R), nsQm, m);
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {   // global stage 0: (e, e + N/2), twiddle psi^rev(1)
+            const int e = tid + (ch * CH + k) * TH;
+            const u64 tt = shoup_lazy(x[CH + k], w0, w0p, m);
+            lds[lds_pad(e)] = x[k] + tt;
+            hi[ch * CH + k] = x[k] + (q2 - tt);
+        }
+    }
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+        if (h) {   // lower half written out: the upper half moves from registers into LDS
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = hi[c];
+        }
+        __syncthreads();
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, m, R.lazy, 1 + h);
+        u64* oh = o + h * NH;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int e = tid + c * TH;
+            oh[e] = fwd_canon(lds[lds_pad(e)], R);
+        }
+    }
+}
+
+template <int LOGN>
+static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* acoef, const unsigned char* vcnt,
+                         u64* ext, int l, int U, hipStream_t st) {
+    const int E = l + T.P, dn = (l + T.P - 1) / T.P;
+    const int mgrid = FHS_MODUP_MAP == 1 ? xcd_grid(E, dn * U) : FHS_MODUP_MAP == 2 ? xcd_grid_m(E, dn * U) : E * dn * U;
+    if (FHS_MODUP_HALF && LOGN >= 9)
+        hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    else
+        hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
 }
 
 // (b2) key inner product with the automorphism applied on the fly, lazy 128-bit over digits:
@@ -686,7 +803,7 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, acoef, vcnt, l, U);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
-    hipLaunchKernelGGL((k_modup<LOGN>), dim3(FHS_MODUP_MAP == 1 ? xcd_grid((int)E, (int)(dn * U)) : FHS_MODUP_MAP == 2 ? xcd_grid_m((int)E, (int)(dn * U)) : (int)(E * dn * U)), blk, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    launch_modup<LOGN>(T, uniq, acoef, vcnt, ext, l, U, st);
     FHS_TMARK(tm, KID_MODUP, 0, st);
     FHS_TMARK(tm, KID_KS_IP, 1, st);
     hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid((int)E, R * (int)(N >> 8))), dim3(256), 0, st, T, it, uniq, ext, acc, l, R,
@@ -906,8 +1023,7 @@ static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, in
     hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, b.acoef, b.vcnt, l, U);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
-    hipLaunchKernelGGL((k_modup<LOGN>), dim3(FHS_MODUP_MAP == 1 ? xcd_grid((int)E, (int)(dn * U)) : FHS_MODUP_MAP == 2 ? xcd_grid_m((int)E, (int)(dn * U)) : (int)(E * dn * U)),
-                       blk, 0, st, T, uniq, b.acoef, b.vcnt, b.ext, l, U);
+    launch_modup<LOGN>(T, uniq, b.acoef, b.vcnt, b.ext, l, U, st);
     FHS_TMARK(tm, KID_MODUP, 0, st);
 }
 template <int LOGN>

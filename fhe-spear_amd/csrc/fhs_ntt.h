@@ -34,9 +34,12 @@ __device__ __forceinline__ void ld_tw(const u64* __restrict__ tw, int idx, u64& 
 // B = 4q stay below 32q < 2^64 for q < 2^59 (host flag PrimeK.pm bit 7).
 // When a group's block index is wave-uniform (TL >= 64) it is read through readfirstlane so the
 // twiddle loads become scalar loads.
+// hoff != 0 runs the pass on one half of a twice-larger transform whose first stage was done
+// elsewhere: half h uses the global twiddles of its blocks, index ((2 + h) << s) + block = local
+// index + ((1 + h) << s), so hoff = 1 + h (forward only).
 template <int LOGN, int S, int R, bool FWD, int EPT, bool LAZY = false>
 __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
-                                         u64 s1, u64 s1s) {
+                                         u64 s1, u64 s1s, int hoff = 0) {
     constexpr int N = 1 << LOGN, T = N / EPT;
     constexpr int TF = N >> (S + 1);
     constexpr int TL = TF >> (R - 1);
@@ -63,7 +66,7 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
                 for (int k = 0; k < GS; ++k) {
                     if (k & half) continue;
                     u64 w, wp;
-                    ld_tw(tw, (1 << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
+                    ld_tw(tw, ((1 + hoff) << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
                     u64 X = x[k];
                     if constexpr (!LAZY) X = X >= q2 ? X - q2 : X;
                     const u64 t = shoup_lazy(x[k + half], w, wp, q);
@@ -98,12 +101,12 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
 }
 
 template <int LOGN, int RL, int S, int EPT, bool LAZY>
-__device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q) {
+__device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
     if constexpr (S < LOGN) {
         constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
-        ntt_pass<LOGN, S, R, true, EPT, LAZY>(lds, tid, tw, q, 0, 0, 0, 0);
+        ntt_pass<LOGN, S, R, true, EPT, LAZY>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
         __syncthreads();
-        fwd_from<LOGN, RL, S + R, EPT, LAZY>(lds, tid, tw, q);
+        fwd_from<LOGN, RL, S + R, EPT, LAZY>(lds, tid, tw, q, hoff);
     }
 }
 // inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first
@@ -122,16 +125,17 @@ __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restric
 // Exit: bit-reversed-order output, after a barrier: < 4q (Harvey) or < (4 + 2 LOGN) q when
 // `lazy` (wave-uniform; RedU::lazy); fwd_canon() maps either to [0, q).
 template <int LOGN, int RL = 3, int EPT = 16>
-__device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, bool lazy) {
-    static_assert(LOGN >= 8 && LOGN <= 14, "LDS-resident NTT supports 256 <= N <= 16384");
+__device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, bool lazy,
+                                            int hoff = 0) {
+    static_assert(LOGN >= 7 && LOGN <= 14, "LDS-resident NTT supports 128 <= N <= 16384");
     static_assert(EPT >= 16 && (EPT & (EPT - 1)) == 0, "EPT must be a power of two >= 16");
 #ifdef FHS_NO_LAZY
     lazy = false;
 #endif
     if (lazy)
-        fwd_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q);
+        fwd_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q, hoff);
     else
-        fwd_from<LOGN, RL, 0, EPT, false>(lds, tid, tw, q);
+        fwd_from<LOGN, RL, 0, EPT, false>(lds, tid, tw, q, hoff);
 }
 // Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.
