@@ -64,6 +64,15 @@ def algorithmic_bytes_per_matvec(name, cfg, l):
     return None
 
 
+def matvec_bytes(cfg, l):
+    """SURVEY.md §8(d) algorithmic bytes of one matvec: D diagonals + (G+B-2) Galois keys at level l
+    + ciphertext in and out."""
+    N, P, D = cfg["N"], cfg["P"], cfg["D"]
+    G, B = bsgs_params(D)
+    E, dn = l + P, (l + P - 1) // P
+    return 8 * N * (D * l + (G + B - 2) * dn * 2 * E + 2 * 2 * l)
+
+
 def ntt_butterflies_per_matvec(cfg, l):
     """Forward-NTT butterflies in k_modup per matvec: B ModUps x (dnum (l+P) - l) limbs x N/2 log N."""
     N, P, D = cfg["N"], cfg["P"], cfg["D"]
@@ -80,8 +89,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rotations", type=int, default=32)
-    ap.add_argument("--cpu-sample-diagonals", type=int, default=768)
+    ap.add_argument("--cpu-sample-rotations", type=int, default=24)
+    ap.add_argument("--cpu-sample-diagonals", type=int, default=512)
+    ap.add_argument("--cpu-workers", type=int, default=16)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -218,6 +228,13 @@ def main():
             valu = {"kernel": "k_modup", "bound": "int-valu", "achieved": round(bf / (mu_ms * 1e-3) / 1e9, 1),
                     "peak": BFLY_PEAK_GOPS, "unit": "G butterfly/s (register-only butterfly ceiling)",
                     "frac": round(bf / (mu_ms * 1e-3) / 1e9 / BFLY_PEAK_GOPS, 4)}
+        # the whole matvec as one HBM-bound unit -- diagonals + 89 non-hoisted
+        # Galois keys + ciphertext in/out -- against 8 TB/s
+        mv_bytes = matvec_bytes(cfg, l)
+        matvec_roof = {"bound": "hbm", "bytes_per_matvec": mv_bytes,
+                       "achieved": round(mv_bytes * value / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(mv_bytes * value / 1e9 / HBM_PEAK_GBS, 4),
+                       "floor_matvec_per_s": round(HBM_PEAK_GBS * 1e9 / mv_bytes, 1)}
         res = {
             "metric": "BSGS matvecs/sec at d=2048,N=16384,L0=36; sec/RWKV-block at 1/2/4/8 GPU",
             "value": round(value, 3),
@@ -238,6 +255,7 @@ def main():
             "roofline": roof,
             "hadamard_roofline": had_roof,
             "ntt_valu_roofline": valu,
+            "matvec_roofline": matvec_roof,
             "kernels": rows,
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -249,34 +267,41 @@ def main():
 
 
 def cpu_baseline(cfg, primes, args):
-    """The C oracle (oracle/ckks_oracle.c, one core) on a bounded sample of the same matvec:
-    `r` of the 89 rotations and `d` of the 2048 multiply_plain+add pairs at the same level;
-    extrapolated linearly to one matvec."""
-    from oracle.oracle import Oracle, galois_elt
+    """The C oracle (oracle/ckks_oracle.c) on a bounded sample of the same matvec, one process per
+    core (W = min(16, cpu_count): the box's CPU share): each worker runs `r` rotations (individual,
+    non-hoisted, as the reference's CPU path issues them) and `d` multiply_plain+add pairs at the
+    same level; the slowest worker's times are extrapolated to one matvec's 89 rotations and 2048
+    products spread over W cores."""
+    import multiprocessing as mp
     N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
-    o = Oracle(N, primes, P)
-    s = o.gen_secret(5)
-    key = o.gen_galois_key(5, s, galois_elt(G, N))
-    rng = np.random.default_rng(9)
-    ct = np.stack([np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)]) for _ in range(2)])
-    pt = np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)])
+    W = max(1, min(args.cpu_workers, os.cpu_count() or 1))
     nr = max(1, min(args.cpu_sample_rotations, (G - 1) + (B - 1)))
     nd = max(1, min(args.cpu_sample_diagonals, D))
-    t0 = time.perf_counter()
-    for _ in range(nr):
-        o.rotate(ct, key, G)
-    t1 = time.perf_counter()
-    acc = o.multiply_plain(ct, pt)
-    for _ in range(nd - 1):
-        acc = o.add(acc, o.multiply_plain(ct, pt))
-    t2 = time.perf_counter()
-    per_matvec = (t1 - t0) / nr * ((G - 1) + (B - 1)) + (t2 - t1) / nd * D
-    return {"value": round(1.0 / per_matvec, 5), "unit": "matvec/s", "cores": 1, "kind": "port",
-            "sample": f"{nr} of {(G - 1) + (B - 1)} rotations + {nd} of {D} multiply_plain/add at L0={L0}, "
-                      f"N={N}, oracle/ckks_oracle.c single thread, extrapolated to one matvec "
-                      f"({t2 - t0:.1f} s sampled)",
-            "sec_per_matvec": round(per_matvec, 2)}
+    ctx = mp.get_context("spawn")
+    barrier = ctx.Barrier(W)
+    out = ctx.Queue()
+    from oracle.cpu_bench import worker
+    procs = [ctx.Process(target=worker, args=(N, [int(q) for q in primes], P, G, nr, nd, w, barrier, out))
+             for w in range(W)]
+    for p in procs:
+        p.start()
+    try:
+        res = [out.get(timeout=900) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.terminate()
+    t_rot = max(r[0] for r in res)
+    t_dia = max(r[1] for r in res)
+    rot = (G - 1) + (B - 1)
+    per_matvec = t_rot * rot / (W * nr) + t_dia * D / (W * nd)
+    return {"value": round(1.0 / per_matvec, 5), "unit": "matvec/s", "cores": W, "kind": "port",
+            "sample": f"{W} processes x ({nr} of {rot} rotations + {nd} of {D} multiply_plain/add) at "
+                      f"L0={L0}, N={N}, oracle/ckks_oracle.c, non-hoisted rotations as the reference issues "
+                      f"them; slowest worker extrapolated to one matvec ({t_rot + t_dia:.1f} s wall sampled)",
+            "sec_per_matvec": round(per_matvec, 3)}
 
 
 if __name__ == "__main__":
