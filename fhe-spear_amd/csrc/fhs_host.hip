@@ -3,7 +3,7 @@
 //
 // Runtime model (MI355X-first):
 //  - one context = one device + one HIP stream; all device memory comes from the stream-ordered
-//    pool (hipMallocAsync / hipFreeAsync), so a free never synchronises the host;
+//    pool (hipMallocAsync) behind a per-size caching free list, so a free never synchronises the host;
 //  - calls on a context are serialised by a mutex (ctypes drops the GIL; bg:223-249 may call
 //    from a thread pool);
 //  - rotations are DEFERRED and batched: fhs_rotate allocates the output and queues the
@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_map>
 #include <chrono>
 #include <memory>
 #include <mutex>
@@ -208,6 +209,13 @@ struct fhs_context {
     std::vector<std::complex<double>> fft_w;   // exp(2 pi i k / N), k < N
     std::vector<uint64_t> slot_index;          // (5^j mod 2N - 1)/2, j < N/2
     std::atomic<uint64_t> bytes_live{0};
+    // caching allocator: freed device blocks are kept per exact size and reused in stream order
+    // (every use of a block is ordered on `st`, aux-stream work is joined back into `st`).  A large
+    // hipMallocAsync costs ~0.35 ms/GB of host time and each hipFreeAsync ~8 us (tools/microbench/
+    // alloc.hip); ciphertexts and plaintexts come in a handful of sizes, so almost every allocation
+    // after warm-up is a free-list pop.  Trimmed on out-of-memory and at context destruction.
+    std::unordered_map<size_t, std::vector<void*>> free_blocks;
+    size_t cached_bytes = 0;
     // kernel timer (bench): events around the timed kernel launches
     // per-kernel event timer (fhs_kernel_timer): bitmask of fhs::KernelId, completed pairs per id
     uint32_t timer_mask = 0;
@@ -221,7 +229,7 @@ struct fhs_context {
     fhs::Stager stager{};
     // grow-only scratch buffers reused across calls (stream order makes reuse safe): a large
     // hipMallocAsync costs ~0.7 ms/GB of host time and can wait on earlier frees
-    enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_COUNT };
+    enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_ENC_PTRS, SCR_COUNT };
     uint64_t* scr[SCR_COUNT] = {};
     size_t scr_bytes[SCR_COUNT] = {};
     static constexpr int kMaxItems = 512;
@@ -263,9 +271,32 @@ struct fhs_galois_keys {
 
 static size_t key_words(const fhs_context* c) { return (size_t)c->dnum * 2 * c->K * c->N; }
 
+static void trim_cache(fhs_context* c) {
+    if (c->free_blocks.empty()) return;
+    if (c->st_aux) hipStreamSynchronize(c->st_aux);
+    for (auto& kv : c->free_blocks)
+        for (void* p : kv.second) (void)hipFreeAsync(p, c->st);
+    hipStreamSynchronize(c->st);
+    c->free_blocks.clear();
+    c->cached_bytes = 0;
+}
 static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
+    bytes = bytes ? bytes : 8;
+    auto it = c->free_blocks.find(bytes);
+    if (it != c->free_blocks.end() && !it->second.empty()) {
+        *p = static_cast<uint64_t*>(it->second.back());
+        it->second.pop_back();
+        c->cached_bytes -= bytes;
+        c->bytes_live += bytes;
+        return hipSuccess;
+    }
     void* v = nullptr;
-    hipError_t e = hipMallocAsync(&v, bytes ? bytes : 8, c->st);
+    hipError_t e = hipMallocAsync(&v, bytes, c->st);
+    if (e == hipErrorOutOfMemory && c->cached_bytes) {   // give the cache back and retry once
+        (void)hipGetLastError();
+        trim_cache(c);
+        e = hipMallocAsync(&v, bytes, c->st);
+    }
     if (e == hipSuccess) {
         *p = (uint64_t*)v;
         c->bytes_live += bytes;
@@ -274,7 +305,9 @@ static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
 }
 static void dfree(fhs_context* c, void* p, size_t bytes) {
     if (!p) return;
-    (void)hipFreeAsync(p, c->st);
+    bytes = bytes ? bytes : 8;
+    c->free_blocks[bytes].push_back(p);
+    c->cached_bytes += bytes;
     c->bytes_live -= bytes;
 }
 
@@ -598,6 +631,28 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
     HIPCHK(up(rs.data(), 8 * rs.size(), (const void**)&T.rescale), "tables");
     HIPCHK(up(pow2.data(), 8 * pow2.size(), (const void**)&T.pow2), "tables");
+    {   // GPU encoder tables (fhs_kernels.hip k_encode)
+        const size_t H = N / 2;
+        const int logH = c->logN - 1;
+        std::vector<double> ew(2 * H), et(2 * H);
+        std::vector<unsigned> ep(H);
+        for (size_t k = 0; k < H; ++k) {
+            const double th = -2.0 * M_PI * (double)k / (double)H;
+            ew[2 * k] = std::cos(th);
+            ew[2 * k + 1] = std::sin(th);
+            const double tz = -M_PI * (double)k / (double)N;
+            et[2 * k] = 2.0 / (double)N * std::cos(tz);
+            et[2 * k + 1] = 2.0 / (double)N * std::sin(tz);
+        }
+        uint64_t e5 = 1;
+        for (size_t j = 0; j < H; ++j) {
+            ep[j] = h_bitrev((uint32_t)((e5 - 1) / 4), logH);
+            e5 = (e5 * 5) & (2 * N - 1);
+        }
+        HIPCHK(up(ew.data(), 8 * ew.size(), (const void**)&T.enc_w), "tables");
+        HIPCHK(up(et.data(), 8 * et.size(), (const void**)&T.enc_twist), "tables");
+        HIPCHK(up(ep.data(), 4 * ep.size(), (const void**)&T.enc_pos), "tables");
+    }
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->ring), fhs_context::kRingBytes, hipHostMallocDefault),
            "staging ring");
     HIPCHK(hipStreamCreateWithFlags(&c->st_aux, hipStreamNonBlocking), "aux stream");
@@ -635,6 +690,9 @@ extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
         for (void* p : c->tables) hipFree(p);
         for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
             if (c->scr[k]) hipFree(c->scr[k]);
+        for (auto& kv : c->free_blocks)
+            for (void* p : kv.second) hipFreeAsync(p, c->st);
+        hipStreamSynchronize(c->st);
         if (c->ring) hipHostFree(c->ring);
         for (auto& v : c->timer_pairs)
             for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
@@ -967,25 +1025,6 @@ static void fft_inplace(std::vector<std::complex<double>>& a, const std::vector<
 }
 
 // values: count vectors of n complex (re,im) (or real when is_real); produces rounded coefficients
-static void encode_coeffs(const fhs_context* c, const double* vals, size_t n, bool is_real, double scale,
-                          double* coef) {
-    const size_t N = c->N, M = 2 * N, slots = N / 2;
-    std::vector<std::complex<double>> v(N, 0.0);
-    for (size_t j = 0; j < slots; ++j) {
-        std::complex<double> z(0.0, 0.0);
-        if (j < n) z = is_real ? std::complex<double>(vals[j], 0.0) : std::complex<double>(vals[2 * j], vals[2 * j + 1]);
-        const size_t t = c->slot_index[j];
-        v[t] = z;
-        v[(M - (2 * t + 1) - 1) / 2] = std::conj(z);
-    }
-    fft_inplace(v, c->fft_w, c->logN, true);    // sum_t v_t w^{-tk}
-    const double invN = 1.0 / (double)N;
-    for (size_t k = 0; k < N; ++k) {
-        const std::complex<double> zk = std::polar(1.0, -M_PI * (double)k / (double)N);
-        const double re = (v[k] * zk).real() * invN;
-        coef[k] = std::round(re * scale);
-    }
-}
 
 static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, size_t n, bool is_real, double scale,
                               int ci, fhs_plaintext** outs) {
@@ -993,34 +1032,41 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
     if (!(scale > 0) || !std::isfinite(scale)) return fail(FHS_ERR_INVALID, "encode: bad scale");
     const int l = c->L0 + 1 - ci;
     if (ci < 1 || l < 1) return fail(FHS_ERR_LEVEL, "encode: chain index out of range");
-    const size_t N = c->N, stride = is_real ? n : 2 * n;
-    const size_t chunk = std::min<size_t>(count, 256);
-    std::vector<double> coef(chunk * N);
-    double* dcoef = nullptr;
-    HIPCHK(hipMalloc(&dcoef, 8 * chunk * N), "encode staging");
+    if (count == 0) return FHS_OK;
+    const size_t stride = is_real ? n : 2 * n;
+    // values -> HBM (the copy completes before returning: the caller's buffer may be reused), then
+    // FFT + exact reduction + NTT on the GPU (k_encode, k_ntt_fwd_ptrs), stream-ordered
+    const size_t chunk = 4096;
+    HostTrace ht;
     for (size_t base = 0; base < count; base += chunk) {
         const size_t cnt = std::min(chunk, count - base);
-        const unsigned nth = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 32));
-        std::vector<std::thread> th;
-        for (unsigned t = 0; t < nth; ++t)
-            th.emplace_back([&, t]() {
-                for (size_t v = t; v < cnt; v += nth)
-                    encode_coeffs(c, vals + (base + v) * stride, n, is_real, scale, coef.data() + v * N);
-            });
-        for (auto& x : th) x.join();
-        hipError_t e = hipMemcpyAsync(dcoef, coef.data(), 8 * cnt * N, hipMemcpyHostToDevice, c->st);
-        for (size_t v = 0; v < cnt && e == hipSuccess; ++v) {
+        uint64_t* dvals = nullptr;
+        HIPCHK(dalloc(c, &dvals, std::max<size_t>(8, 8 * cnt * stride)), "encode staging");
+        if (stride) {
+            hipError_t e = hipMemcpyAsync(dvals, vals + base * stride, 8 * cnt * stride, hipMemcpyHostToDevice, c->st);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+            if (e != hipSuccess) { dfree(c, dvals, 8 * cnt * stride); return hip_fail(e, "encode upload"); }
+        }
+        ht.mark("encode: upload");
+        std::vector<uint64_t*> ptrs(cnt);
+        for (size_t v = 0; v < cnt; ++v) {
             fhs_plaintext* pt = nullptr;
             fhs_status s = new_pt(c, ci, scale, &pt);
-            if (s != FHS_OK) { hipFree(dcoef); return s; }
+            if (s != FHS_OK) { dfree(c, dvals, 8 * cnt * stride); return s; }
             outs[base + v] = pt;
-            e = fhs::launch_encode_reduce(c->T, dcoef + v * N, 1, pt->d, l, c->st);
-            if (e == hipSuccess) e = fhs::launch_ntt_fwd(c->T, pt->d, l, l, 1, 0, c->st);
+            ptrs[v] = pt->d;
         }
-        if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // staging buffers are reused
-        if (e != hipSuccess) { hipFree(dcoef); return hip_fail(e, "encode"); }
+        uint64_t* dptrs = nullptr;
+        hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * cnt, &dptrs);
+        if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * cnt);
+        if (e == hipSuccess)
+            e = fhs::launch_encode(c->T, reinterpret_cast<const double*>(dvals), (int)cnt, n, stride, is_real, scale,
+                                   reinterpret_cast<fhs::u64* const*>(dptrs), l, c->st);
+        dfree(c, dvals, std::max<size_t>(8, 8 * cnt * stride));
+        ht.mark("encode: objects+launch");
+        if (ht.on) { hipStreamSynchronize(c->st); ht.mark("encode: gpu"); }
+        if (e != hipSuccess) return hip_fail(e, "encode");
     }
-    hipFree(dcoef);
     return FHS_OK;
 }
 

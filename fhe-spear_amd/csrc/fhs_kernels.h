@@ -21,6 +21,9 @@ struct DevTables {
     const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup
     const u64* rescale;       // [L0+1][L0][4]  inv(q_{l-1}) mod q_i (+Shoup), half mod q_i, half
     const u64* pow2;          // [K][1088] 2^e mod q_i (exact double reduction)
+    const double* enc_w;      // [N/2][2]  omega^-k, omega = exp(2 pi i / (N/2))   (GPU encoder FFT)
+    const double* enc_twist;  // [N/2][2]  (2/N) zeta^-k, zeta = exp(i pi / N)
+    const unsigned* enc_pos;  // [N/2]     rev_{log N - 1}((5^j mod 2N - 1) / 4): LDS slot of z_j
     int N, logN, L0, P, K, dnum;
 };
 
@@ -85,6 +88,10 @@ size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, u64* inner, u64* out, u64* workspace, size_t ws_bytes,
                        void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
+// CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
+// apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
+hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
+                         double scale, u64* const* outs_dev, int l, hipStream_t st);
 hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st);

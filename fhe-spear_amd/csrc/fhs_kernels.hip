@@ -1256,6 +1256,23 @@ hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u6
 }
 
 // exact residue of integral doubles: coef [count][N] -> out [count][l][N] (coefficient form)
+// exact residue of an integral double (any magnitude) mod prime i
+__device__ __forceinline__ u64 dbl_mod(const DevTables& T, double d, int i) {
+    const PrimeK& P = PK(T, i);
+    const bool neg = d < 0;
+    const double a = neg ? -d : d;
+    u64 r;
+    if (a < 9.2e18) {
+        r = reduce64((u64)a, P);
+    } else {
+        const u64 bits = (u64)__double_as_longlong(a);
+        const int ex = (int)((bits >> 52) & 0x7FF) - 1075;
+        const u64 mant = (bits & ((1ULL << 52) - 1)) | (1ULL << 52);
+        r = mulmod(reduce64(mant, P), T.pow2[(size_t)i * 1088 + ex], P);
+    }
+    return (neg && r) ? P.q - r : r;
+}
+
 __global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64* out, int l) {
     const int N = T.N;
     const size_t total = (size_t)count * l * N;
@@ -1265,22 +1282,89 @@ __global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64*
         const size_t rest = idx / N;
         const int i = (int)(rest % l);
         const size_t v = rest / l;
-        const PrimeK& P = PK(T, i);
-        const double d = coef[v * N + n];
-        const bool neg = d < 0;
-        const double a = neg ? -d : d;
-        u64 r;
-        if (a < 9.2e18) {
-            r = reduce64((u64)a, P);
-        } else {
-            const u64 bits = (u64)__double_as_longlong(a);
-            const int ex = (int)((bits >> 52) & 0x7FF) - 1075;
-            const u64 mant = (bits & ((1ULL << 52) - 1)) | (1ULL << 52);
-            r = mulmod(reduce64(mant, P), T.pow2[(size_t)i * 1088 + ex], P);
-        }
-        out[idx] = (neg && r) ? P.q - r : r;
+        out[idx] = dbl_mod(T, coef[v * N + n], i);
     }
 }
+
+// ---- CKKS encoder (pb:138-156, bg:382, 423 encode_*_vector_batch) ----
+// Canonical embedding inverse with an N/2-point FFT: z_j = m(zeta^{5^j}), 5^j = 4 s_j + 1, so
+// c_k = m_k + i m_{k+N/2} = (2/N) zeta^-k sum_j z_j omega^{-s_j k}, omega = zeta^4.  One workgroup
+// per vector: z_j is scattered to LDS slot rev(s_j) (bit-reversed input), a radix-2 DIT FFT runs in
+// LDS (f64), then each coefficient is scaled, rounded (half away from zero, as the host decoder's
+// inverse) and reduced exactly mod every limb's prime.  The NTT follows (k_ntt_fwd_ptrs).
+template <int LOGN>
+__global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024)
+    k_encode(DevTables T, const double* vals, size_t n, size_t stride, int is_real, double scale, u64* const* outs,
+             int l) {
+    constexpr int N = 1 << LOGN, H = N / 2, LOGH = LOGN - 1;
+    constexpr int TH = (N / 16) < 1024 ? (N / 16) : 1024;
+    __shared__ double2 a[H];
+    const int tid = threadIdx.x;
+    const double* src = vals + (size_t)blockIdx.x * stride;
+    for (int j = tid; j < H; j += TH) {
+        double2 z = {0.0, 0.0};
+        if ((size_t)j < n) z = is_real ? double2{src[j], 0.0} : double2{src[2 * j], src[2 * j + 1]};
+        a[T.enc_pos[j]] = z;
+    }
+    __syncthreads();
+    const double2* W = reinterpret_cast<const double2*>(T.enc_w);
+    for (int s = 0; s < LOGH; ++s) {
+        const int half = 1 << s;
+        for (int b = tid; b < H / 2; b += TH) {
+            const int k = b & (half - 1);
+            const int i = ((b >> s) << (s + 1)) + k, j = i + half;
+            const double2 w = W[(size_t)k << (LOGH - 1 - s)];
+            const double2 x = a[i], y = a[j];
+            const double2 t = {y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x};
+            a[i] = double2{x.x + t.x, x.y + t.y};
+            a[j] = double2{x.x - t.x, x.y - t.y};
+        }
+        __syncthreads();
+    }
+    const double2* Z = reinterpret_cast<const double2*>(T.enc_twist);
+    u64* out = outs[blockIdx.x];
+    for (int k = tid; k < H; k += TH) {
+        const double2 v = a[k], z = Z[k];
+        const double lo = round((v.x * z.x - v.y * z.y) * scale);
+        const double hi = round((v.x * z.y + v.y * z.x) * scale);
+        for (int i = 0; i < l; ++i) {
+            out[(size_t)i * N + k] = dbl_mod(T, lo, i);
+            out[(size_t)i * N + H + k] = dbl_mod(T, hi, i);
+        }
+    }
+}
+
+// forward NTT of `limbs` limbs of each polynomial ptrs[blockIdx.y] (plaintext batches)
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_fwd_ptrs(DevTables T, u64* const* ptrs, int limbs) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    const RedU R = redu(PK(T, b));
+    u64* p = ptrs[blockIdx.y] + (size_t)b * N;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = p[tid + k * TH];
+    __syncthreads();
+    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)b * N * 2, R.q, R.lazy);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        p[e] = fwd_canon(lds[lds_pad(e)], R);
+    }
+}
+
+hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
+                         double scale, u64* const* outs_dev, int l, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    FHS_DISPATCH_LOGN(T.logN, {
+        constexpr int TH = ((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024;
+        hipLaunchKernelGGL((k_encode<LOGN>), dim3(count), dim3(TH), 0, st, T, vals, n, stride, is_real ? 1 : 0, scale,
+                           outs_dev, l);
+        hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3((1 << LOGN) / 16), 0, st, T, outs_dev, l);
+    });
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st) {
     hipLaunchKernelGGL(k_encode_reduce, dim3(eltwise_grid((size_t)count * l * T.N)), dim3(256), 0, st, T, coef, count,
                        out, l);
