@@ -269,7 +269,11 @@ struct fhs_galois_keys {
     std::map<uint64_t, uint64_t*> keys;
 };
 
-static size_t key_words(const fhs_context* c) { return (size_t)c->dnum * 2 * c->K * c->N; }
+// switching key in HBM: b_j [dnum][K][N] then the dnum seeds of the uniform a_j, which the key
+// inner product regenerates on the fly (SAMPLE_SEEDED): half the bytes of storing (b_j, a_j)
+static size_t key_words(const fhs_context* c) { return (size_t)c->dnum * c->K * c->N + (size_t)c->dnum; }
+// exported / oracle layout: [dnum][2][K][N]
+static size_t key_words_full(const fhs_context* c) { return (size_t)c->dnum * 2 * c->K * c->N; }
 
 static void trim_cache(fhs_context* c) {
     if (c->free_blocks.empty()) return;
@@ -726,12 +730,7 @@ extern "C" fhs_status fhs_memory_in_use(fhs_context* c, uint64_t* bytes) {
 }
 
 // ============================================================================ sampling helpers
-static uint64_t sm64(uint64_t x) {
-    x += 0x9E3779B97F4A7C15ULL;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
-    return x ^ (x >> 31);
-}
+// sm64: fhs_modarith.h (host + device)
 static uint64_t stream_key(uint64_t seed, uint64_t stream) { return sm64(seed ^ sm64(stream)); }
 static uint64_t stream_id(uint64_t kind, uint64_t a, uint64_t b) { return (kind << 56) | (a << 16) | b; }
 enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6 };
@@ -767,20 +766,46 @@ static fhs_status gen_switch_key(fhs_context* c, uint64_t seed, uint64_t base, c
     uint64_t* key = nullptr;
     hipError_t e = dalloc(c, &key, 8 * key_words(c));
     if (e != hipSuccess) return hip_fail(e, "switching key");
-    uint64_t* ebuf = nullptr;
-    e = dalloc(c, &ebuf, 8ull * c->K * c->N);
-    if (e != hipSuccess) { dfree(c, key, 8 * key_words(c)); return hip_fail(e, "switching key"); }
     const size_t S = (size_t)c->K * c->N;
+    uint64_t* tmp = nullptr;   // e | a
+    e = dalloc(c, &tmp, 16 * S);
+    if (e != hipSuccess) { dfree(c, key, 8 * key_words(c)); return hip_fail(e, "switching key"); }
+    uint64_t* ebuf = tmp;
+    uint64_t* abuf = tmp + S;
+    std::vector<uint64_t> seeds(c->dnum);
     for (int j = 0; j < c->dnum && e == hipSuccess; ++j) {
-        const uint64_t ka = stream_key(seed, base | (uint64_t)(2 * j));
+        seeds[j] = stream_key(seed, base | (uint64_t)(2 * j));
         const uint64_t ke = stream_key(seed, base | (uint64_t)(2 * j + 1));
-        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, ka, key + ((size_t)j * 2 + 1) * S, c->K, 0, c->st);
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_SEEDED, seeds[j], abuf, c->K, 0, c->st);
         if (e == hipSuccess) e = sample_small_ntt(c, fhs::SAMPLE_CBD, ke, ebuf, c->K);
-        if (e == hipSuccess) e = fhs::launch_switch_key_assemble(c->T, key, ebuf, s, snew, j, c->st);
+        if (e == hipSuccess) e = fhs::launch_switch_key_assemble(c->T, key + (size_t)j * S, abuf, ebuf, s, snew, j, c->st);
     }
-    dfree(c, ebuf, 8ull * c->K * c->N);
+    if (e == hipSuccess) e = hipMemcpyAsync(key + (size_t)c->dnum * S, seeds.data(), 8 * seeds.size(),
+                                            hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // `seeds` is a host temporary
+    dfree(c, tmp, 16 * S);
     if (e != hipSuccess) { dfree(c, key, 8 * key_words(c)); return hip_fail(e, "switching key generation"); }
     *key_out = key;
+    return FHS_OK;
+}
+// [dnum][2][K][N] with the a_j regenerated from their seeds (the oracle's layout)
+static fhs_status export_switch_key(fhs_context* c, const uint64_t* key, uint64_t* host) {
+    const size_t S = (size_t)c->K * c->N;
+    std::vector<uint64_t> seeds(c->dnum);
+    HIPCHK(hipMemcpyAsync(seeds.data(), key + (size_t)c->dnum * S, 8 * seeds.size(), hipMemcpyDeviceToHost, c->st),
+           "key export");
+    HIPCHK(hipStreamSynchronize(c->st), "key export");
+    uint64_t* full = nullptr;
+    HIPCHK(dalloc(c, &full, 8 * key_words_full(c)), "key export");
+    hipError_t e = hipSuccess;
+    for (int j = 0; j < c->dnum && e == hipSuccess; ++j) {
+        e = hipMemcpyAsync(full + (size_t)j * 2 * S, key + (size_t)j * S, 8 * S, hipMemcpyDeviceToDevice, c->st);
+        if (e == hipSuccess) e = fhs::launch_sample(c->T, fhs::SAMPLE_SEEDED, seeds[j], full + ((size_t)j * 2 + 1) * S, c->K, 0, c->st);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(host, full, 8 * key_words_full(c), hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    dfree(c, full, 8 * key_words_full(c));
+    if (e != hipSuccess) return hip_fail(e, "key export");
     return FHS_OK;
 }
 
@@ -868,12 +893,12 @@ extern "C" fhs_status fhs_galois_key_export(fhs_context* c, const fhs_galois_key
     if (!gk || !host) return fail(FHS_ERR_INVALID, "null argument");
     auto it = gk->keys.find(elt);
     if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "galois key not present");
-    return export_dev(c, it->second, 8 * key_words(c), host);
+    return export_switch_key(c, it->second, host);
 }
 extern "C" fhs_status fhs_relin_key_export(fhs_context* c, const fhs_relin_key* rk, uint64_t* host) {
     ENTER(c);
     if (!rk || !host) return fail(FHS_ERR_INVALID, "null argument");
-    return export_dev(c, rk->key, 8 * key_words(c), host);
+    return export_switch_key(c, rk->key, host);
 }
 extern "C" fhs_status fhs_secret_key_export(fhs_context* c, const fhs_secret_key* sk, uint64_t* host) {
     ENTER(c);

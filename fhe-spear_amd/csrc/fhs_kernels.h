@@ -35,7 +35,7 @@ struct KsItem {
     const u64* a;        // poly to switch (NTT form, l limbs), un-permuted
     const u64* add0;     // added to output comp 0 (through `elt`), may be null
     const u64* add1;     // added to output comp 1 (identity), may be null
-    const u64* key;      // [dnum][2][K][N]
+    const u64* key;      // switching key: b [dnum][K][N], then the dnum seeds of the a_j (SAMPLE_SEEDED)
     u64* out0;           // l limbs
     u64* out1;           // l limbs
     u64 elt;             // galois element (1 = identity)
@@ -93,7 +93,8 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
                          double scale, u64* const* outs_dev, int l, hipStream_t st);
 hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
-hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,
+// b_j = e - a_j s + [limb in digit j] (P mod q) s_new  (switching-key component 0 of digit j)
+hipError_t launch_switch_key_assemble(const DevTables& T, u64* b_out, const u64* a, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st);
 hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int limbs, u64 elt, hipStream_t st);
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
@@ -103,6 +104,6 @@ hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int coun
 hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st);
 
 enum EltOp { OP_ADD = 0, OP_SUB = 1, OP_NEG = 2, OP_MULP = 3, OP_ADDP = 4, OP_SUBP = 5, OP_SUBNEG = 6 };
-enum SampleMode { SAMPLE_UNIFORM = 0, SAMPLE_TERNARY = 1, SAMPLE_CBD = 2 };
+enum SampleMode { SAMPLE_UNIFORM = 0, SAMPLE_TERNARY = 1, SAMPLE_CBD = 2, SAMPLE_SEEDED = 3 };
 
 }  // namespace fhs

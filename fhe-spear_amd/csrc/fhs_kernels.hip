@@ -651,13 +651,16 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
     const u64* own = uniq[it.src] + (size_t)t * N + sn;
     const u64* key = it.key + (size_t)pt * N + n;
+    const u64* seeds = it.key + (size_t)T.dnum * K * N;
+    const u64 cx = seeded_ctr_mix(pt, n);
+    const unsigned qb = 64 - __clzll(RD.q);
     u128 c0 = {0, 0}, c1 = {0, 0};
     Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
 #pragma unroll 4
     for (int j = 0; j < dn; ++j) {
         const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
-        acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j) * K * N)));
-        acc3_mac(a1, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N)));
+        acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * K * N)));
+        acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
         if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
             acc3_fold(c0, a0);
             acc3_fold(c1, a1);
@@ -683,6 +686,8 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
     const size_t per_r = (size_t)E * N;
     const RedU RD = redu(PK(T, t));
     const u64 q = RD.q;
+    const u64 cx = seeded_ctr_mix(t, n);
+    const unsigned qb = 64 - __clzll(q);
     u64 s0 = 0, s1 = 0, sadd = 0;
     for (int r = 0; r < R; ++r) {
         const KsItem it = items[r];
@@ -690,13 +695,14 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
         const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
         const u64* own = uniq[it.src] + (size_t)t * N + sn;
         const u64* key = it.key + (size_t)t * N + n;
+        const u64* seeds = it.key + (size_t)T.dnum * K * N;
         u128 c0 = {0, 0}, c1 = {0, 0};
         Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
 #pragma unroll 4
         for (int j = 0; j < dn; ++j) {
             const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
-            acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j) * K * N)));
-            acc3_mac(a1, v, split30(__builtin_nontemporal_load(key + (size_t)(2 * j + 1) * K * N)));
+            acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * K * N)));
+            acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, q, qb)));
             if ((j & 7) == 7) {
                 acc3_fold(c0, a0);
                 acc3_fold(c1, a1);
@@ -1145,12 +1151,6 @@ size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
 
 
 // ============================================================================ sampling / keys
-__device__ __forceinline__ u64 sm64(u64 x) {
-    x += 0x9E3779B97F4A7C15ULL;
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
-    return x ^ (x >> 31);
-}
 __device__ __forceinline__ u64 rnd(u64 key, u64 ctr) { return sm64(key ^ sm64(ctr ^ 0xD1B54A32D192ED03ULL)); }
 
 // mode 0: uniform mod q_i directly (NTT-domain sample); 1: ternary; 2: CBD(21) -- small values
@@ -1165,6 +1165,8 @@ __global__ void k_sample(DevTables T, int mode, u64 key, u64* out, int l) {
         if (mode == SAMPLE_UNIFORM) {
             const u64 ctr = 2 * ((u64)i * N + n);
             v = reduce128(rnd(key, ctr + 1), rnd(key, ctr), P);
+        } else if (mode == SAMPLE_SEEDED) {
+            v = seeded_uniform_x(key + seeded_ctr_mix(i, n), P.q, 64 - __clzll(P.q));
         } else {
             const u64 r = rnd(key, (u64)n);
             long long s;
@@ -1185,26 +1187,24 @@ hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l,
 }
 
 // key_j[0] = e - a s + [i in digit j] (P mod q_i) s_new ; key_j[1] = a (already in place)
-__global__ void k_swk(DevTables T, u64* key, const u64* e, const u64* s, const u64* snew, int j) {
+__global__ void k_swk(DevTables T, u64* b_out, const u64* a, const u64* e, const u64* s, const u64* snew, int j) {
     const int N = T.N, K = T.K;
     const size_t S = (size_t)K * N;
-    u64* k0 = key + (size_t)j * 2 * S;
-    const u64* k1 = k0 + S;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
         const int i = (int)(idx / N);
         const PrimeK& P = PK(T, i);
-        u64 v = submod(e[idx], mulmod(k1[idx], s[idx], P), P.q);
+        u64 v = submod(e[idx], mulmod(a[idx], s[idx], P), P.q);
         if (i < T.L0 && i / T.P == j) {
             const u64 pm = T.md_pinv[2 * T.L0 + i];   // P mod q_i stored after the inverses
             v = addmod(v, mulmod(pm, snew[idx], P), P.q);
         }
-        k0[idx] = v;
+        b_out[idx] = v;
     }
 }
-hipError_t launch_switch_key_assemble(const DevTables& T, u64* key, const u64* e_ntt, const u64* s_ntt,
+hipError_t launch_switch_key_assemble(const DevTables& T, u64* b_out, const u64* a, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st) {
-    hipLaunchKernelGGL(k_swk, dim3(eltwise_grid((size_t)T.K * T.N)), dim3(256), 0, st, T, key, e_ntt, s_ntt, snew_ntt,
-                       digit);
+    hipLaunchKernelGGL(k_swk, dim3(eltwise_grid((size_t)T.K * T.N)), dim3(256), 0, st, T, b_out, a, e_ntt, s_ntt,
+                       snew_ntt, digit);
     return hipGetLastError();
 }
 

@@ -139,6 +139,27 @@ __device__ __forceinline__ void acc3_fold(u128& c, Acc3& a) {
     a = Acc3{0, 0, 0};
 }
 
+// SplitMix64 (the sampling spec shared with oracle/ckks_oracle.c ock_splitmix64).
+__host__ __device__ __forceinline__ u64 sm64(u64 x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+// Seeded uniform residue (switching-key `a` components): the top `bits`
+// bits of sm64(key + ctr * gamma), ctr = m 2^40 | prime 2^20 | n, accepted when < q (rejection
+// sampling: exactly uniform; for SEAL-style primes a retry has probability (2^bits - q) / 2^bits <
+// 2^-32).  `kx` = key + (prime 2^20 | n) * gamma is hoisted by callers that vary only the key.
+__host__ __device__ __forceinline__ u64 seeded_uniform_x(u64 kx, u64 q, unsigned bits) {
+    for (u64 m = 0;; ++m) {
+        const u64 v = sm64(kx + (m << 40) * 0x9E3779B97F4A7C15ULL) >> (64 - bits);
+        if (v < q) return v;
+    }
+}
+__host__ __device__ __forceinline__ u64 seeded_ctr_mix(int prime, int n) {
+    return (((u64)prime << 20) | (u64)n) * 0x9E3779B97F4A7C15ULL;
+}
+
 // Per-prime constants, 64 B, kept in a device table indexed by key-level prime index.
 struct PrimeK {
     u64 q;

@@ -587,6 +587,21 @@ static void sample_uniform_ntt(const ock_ctx* c, uint64_t key, int pi, uint64_t*
         dst[n] = reduce128(ock_rnd(key, ctr), ock_rnd(key, ctr + 1), q);
     }
 }
+/* switching-key `a` components: exactly uniform by rejection from the top bits of one SplitMix64
+ * output per try (spec shared with fhs_modarith.h seeded_uniform_x, regenerated on the GPU inside
+ * the key inner product instead of being stored) */
+uint64_t ock_seeded_uniform(uint64_t key, int pi, uint64_t n, uint64_t q) {
+    const uint64_t G = 0x9E3779B97F4A7C15ULL;
+    const int bits = 64 - __builtin_clzll(q);
+    const uint64_t kx = key + ((((uint64_t)pi) << 20) | n) * G;
+    for (uint64_t m = 0;; m++) {
+        uint64_t v = ock_splitmix64(kx + (m << 40) * G) >> (64 - bits);
+        if (v < q) return v;
+    }
+}
+static void sample_uniform_seeded(const ock_ctx* c, uint64_t key, int pi, uint64_t* dst) {
+    for (uint64_t n = 0; n < c->N; n++) dst[n] = ock_seeded_uniform(key, pi, n, c->q[pi]);
+}
 static void sample_ternary(const ock_ctx* c, uint64_t key, int64_t* dst) {
     for (uint64_t n = 0; n < c->N; n++) { uint64_t t = ock_rnd(key, n) % 3; dst[n] = t == 2 ? -1 : (int64_t)t; }
 }
@@ -623,7 +638,7 @@ void ock_gen_switch_key(const ock_ctx* c, uint64_t seed, uint64_t stream_base,
             uint64_t q = c->q[i];
             uint64_t* k0 = key + (((size_t)j * 2 + 0) * K + i) * N;
             uint64_t* k1 = key + (((size_t)j * 2 + 1) * K + i) * N;
-            sample_uniform_ntt(c, ka, i, k1);
+            sample_uniform_seeded(c, ka, i, k1);
             small_to_ntt(c, e, i, et);
             uint64_t Pm = 1;
             for (int k = 0; k < P; k++) Pm = mulmod(Pm, c->q[L0 + k] % q, q);

@@ -34,6 +34,8 @@ typedef struct ock_ctx ock_ctx;
 uint64_t ock_splitmix64(uint64_t x);
 uint64_t ock_stream_key(uint64_t seed, uint64_t stream);
 uint64_t ock_rnd(uint64_t key, uint64_t ctr);
+/* uniform residue mod q from (key, prime index, coefficient) by rejection (switching-key a_j) */
+uint64_t ock_seeded_uniform(uint64_t key, int pi, uint64_t n, uint64_t q);
 
 /* SEAL/Phantom CoeffModulus::Create (pb:81 create_coeff_modulus). 0 on success. */
 int ock_create_coeff_modulus(uint64_t N, const int* bits, int n, uint64_t* out);

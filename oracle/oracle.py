@@ -65,6 +65,8 @@ def lib():
         L.ock_rotate_hoisted.argtypes = [vp, _u64p, C.POINTER(_u64p), _u64p, C.c_int, C.c_int, C.POINTER(_u64p)]
         L.ock_centered_count_test.argtypes = [_u64p, _u64p, C.c_int]
         L.ock_centered_count_test.restype = C.c_int
+        L.ock_seeded_uniform.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64]
+        L.ock_seeded_uniform.restype = C.c_uint64
         L.ock_bsgs_loop.argtypes = [vp, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p),
                                     C.c_int, C.c_int, C.c_int, C.c_int, _u64p]
         L.ock_gen_secret.argtypes = [vp, C.c_uint64, _u64p]
@@ -100,6 +102,11 @@ def centered_count(y, qs) -> int:
     y = np.ascontiguousarray(np.asarray(y, dtype=np.uint64))
     q = np.ascontiguousarray(np.asarray(qs, dtype=np.uint64))
     return int(lib().ock_centered_count_test(_p(y), _p(q), len(y)))
+
+
+def seeded_uniform(key: int, prime_idx: int, n: int, q: int) -> int:
+    """ock_seeded_uniform: the switching-key `a` sampler (rejection from SplitMix64 top bits)."""
+    return int(lib().ock_seeded_uniform(key, prime_idx, n, q))
 
 
 def galois_elt(step: int, N: int) -> int:

@@ -310,3 +310,35 @@ def test_device_ntt_passes_emulated_match_direct_evaluation(tmp_path):
                     str(REPO / "tools/debug/ntt_emu.cpp"), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
+
+
+def _sm64(x):
+    M = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    return x ^ (x >> 31)
+
+
+def test_seeded_key_sampler_spec(orc):
+    """Switching-key `a` components are regenerated on the GPU from a seed (fhs_modarith.h
+    seeded_uniform_x); the oracle's sampler must follow the written spec exactly, including the
+    rejection path (forced here with q just above a power of two, so about half the tries reject)."""
+    from oracle.oracle import seeded_uniform
+    G, M = 0x9E3779B97F4A7C15, (1 << 64) - 1
+
+    def spec(key, pi, n, q):
+        bits = q.bit_length()
+        kx = (key + (((pi << 20) | n) * G)) & M
+        m = 0
+        while True:
+            v = _sm64((kx + ((m << 40) * G)) & M) >> (64 - bits)
+            if v < q:
+                return v
+            m += 1
+
+    q59 = orc.create_coeff_modulus(16384, [59] * 2)[0]
+    for q in (q59, (1 << 58) + 3, 97):
+        for key in (0, 1, 0xDEADBEEFCAFEF00D):
+            for pi, n in ((0, 0), (3, 1), (38, 16383), (5, 777)):
+                assert seeded_uniform(key, pi, n, q) == spec(key, pi, n, q)
