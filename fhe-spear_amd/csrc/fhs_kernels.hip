@@ -27,6 +27,12 @@
 #ifndef FHS_MODUP_HALF
 #define FHS_MODUP_HALF 1      // k_modup_h: half-limb LDS, two workgroups per CU
 #endif
+#ifndef FHS_INNER_LDS_MIN
+#define FHS_INNER_LDS_MIN 0
+#endif
+#ifndef FHS_INTT_HALF
+#define FHS_INTT_HALF 1       // k_ks_intt_h: half-limb LDS inverse NTT
+#endif
 #ifndef FHS_MODUPH_CH
 #define FHS_MODUPH_CH 2
 #endif
@@ -352,6 +358,46 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const
     u64* dst = acoef + ((size_t)u * l + i) * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
+}
+
+// k_ks_intt with half the limb in LDS (two workgroups per CU, co-resident with the half-limb ModUp
+// and the Hadamard): each half runs every inverse stage but the global last one, whose (e, e+N/2)
+// butterflies (with the N^-1 and ModUp scaling folded in) are done in registers.  Same values.
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, const u64* const* uniq, u64* acoef,
+                                                                   int l, int U) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
+    const int tid = threadIdx.x;
+    int i, u;
+    if (!plain_tm(l, U, i, u)) return;
+    const PrimeK& P = PK(T, i);
+    const u64 q = P.q;
+    const u64* src = uniq[u] + (size_t)i * N;
+    const u64* tw = T.tw_inv + (size_t)i * N * 2;
+    u64 lo[16];
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[h * NH + tid + c * TH];
+        __syncthreads();
+        ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL>(lds, tid, tw, q, 1 + h);
+        if (h == 0) {
+#pragma unroll
+            for (int c = 0; c < 16; ++c) lo[c] = lds[lds_pad(tid + c * TH)];
+        }
+    }
+    const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
+    const u64 s0 = cst[0], s0s = cst[1], s1 = cst[2], s1s = cst[3], q2 = 2 * q;
+    u64* dst = acoef + ((size_t)u * l + i) * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int e = tid + c * TH;
+        const u64 X = lo[c], Y = lds[lds_pad(e)];
+        dst[e] = csub(shoup_lazy(X + Y, s0, s0s, q), q);
+        dst[NH + e] = csub(shoup_lazy(X - Y + q2, s1, s1s, q), q);
+    }
 }
 
 // Exact centred-extension count, slow path (|frac - 1/2| < 2^-58; never seen on random data
@@ -805,7 +851,10 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     unsigned char* vcnt = reinterpret_cast<unsigned char*>(ycoef + (size_t)R * 2 * T.P * N);
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, acoef, l, U);
+    if (FHS_INTT_HALF && LOGN >= 9)
+        hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, l, U);
+    else
+        hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, acoef, l, U);
     hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, acoef, vcnt, l, U);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
@@ -1025,7 +1074,10 @@ static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, in
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, b.acoef, l, U);
+    if (FHS_INTT_HALF && LOGN >= 9)
+        hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, b.acoef, l, U);
+    else
+        hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, b.acoef, l, U);
     hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, b.acoef, b.vcnt, l, U);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
@@ -1083,11 +1135,14 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
         if (e != hipSuccess) return e;
     }
-    const size_t sh = (size_t)G * 2 * W * 8;
+    // FHS_INNER_LDS_MIN pads the dynamic LDS so fewer Hadamard workgroups fit a CU and the
+    // VALU-bound ModUp of the previous chunk (other stream) can be co-resident (experiment knob)
+    const size_t sh = std::max<size_t>((size_t)G * 2 * W * 8, FHS_INNER_LDS_MIN);
     static bool attr = false;
     if (!attr) {   // dynamic LDS above 64 KiB must be opted into
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 2 * W * 8);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)std::max<size_t>(64 * 2 * W * 8, FHS_INNER_LDS_MIN));
         if (e != hipSuccess) return e;
         attr = true;
     }

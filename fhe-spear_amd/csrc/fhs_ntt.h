@@ -37,7 +37,9 @@ __device__ __forceinline__ void ld_tw(const u64* __restrict__ tw, int idx, u64& 
 // hoff != 0 runs the pass on one half of a twice-larger transform whose first stage was done
 // elsewhere: half h uses the global twiddles of its blocks, index ((2 + h) << s) + block = local
 // index + ((1 + h) << s), so hoff = 1 + h (forward only).
-template <int LOGN, int S, int R, bool FWD, int EPT, bool LAZY = false>
+// NOFOLD (inverse only): the transform is one half of a twice-larger inverse, so its last stage is
+// an ordinary stage (twiddle through hoff) and the N^-1 fold happens in the caller's final stage.
+template <int LOGN, int S, int R, bool FWD, int EPT, bool LAZY = false, bool NOFOLD = false>
 __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
                                          u64 s1, u64 s1s, int hoff = 0) {
     constexpr int N = 1 << LOGN, T = N / EPT;
@@ -82,12 +84,12 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
                 for (int k = 0; k < GS; ++k) {
                     if (k & half) continue;
                     const u64 X = x[k], Y = x[k + half];
-                    if (S == 0 && u == 0) {   // last GS stage: fold N^-1 (and any caller scale)
+                    if (!NOFOLD && S == 0 && u == 0) {   // last GS stage: fold N^-1 (and any caller scale)
                         x[k] = shoup_lazy(X + Y, s0, s0s, q);
                         x[k + half] = shoup_lazy(X - Y + q2, s1, s1s, q);
                     } else {
                         u64 w, wp;
-                        ld_tw(tw, (1 << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
+                        ld_tw(tw, ((1 + hoff) << (S + u)) + blk * (1 << u) + (k >> (R - u)), w, wp);
                         const u64 s = X + Y;
                         x[k] = s >= q2 ? s - q2 : s;
                         x[k + half] = shoup_lazy(X - Y + q2, w, wp, q);
@@ -110,13 +112,13 @@ __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restric
     }
 }
 // inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first
-template <int LOGN, int RL, int S, int EPT>
+template <int LOGN, int RL, int S, int EPT, bool NOFOLD = false>
 __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
-                                         u64 s1, u64 s1s) {
+                                         u64 s1, u64 s1s, int hoff = 0) {
     if constexpr (S < LOGN) {
         constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
-        inv_from<LOGN, RL, S + R, EPT>(lds, tid, tw, q, s0, s0s, s1, s1s);
-        ntt_pass<LOGN, S, R, false, EPT>(lds, tid, tw, q, s0, s0s, s1, s1s);
+        inv_from<LOGN, RL, S + R, EPT, NOFOLD>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
+        ntt_pass<LOGN, S, R, false, EPT, false, NOFOLD>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
         __syncthreads();
     }
 }
@@ -139,6 +141,12 @@ __device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __rest
 }
 // Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.
+// Inverse on one half (h = hoff - 1) of a 2^(LOGN+1)-point inverse: all of its stages except the
+// global last one, which the caller applies to the (e, e + 2^LOGN) pairs.  Output in [0, 2q).
+template <int LOGN, int RL = 3, int EPT = 16>
+__device__ __forceinline__ void ntt_inv_half_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
+    inv_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
+}
 template <int LOGN, int RL = 3, int EPT = 16>
 __device__ __forceinline__ void ntt_inv_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
                                             u64 s1, u64 s1s) {
