@@ -101,6 +101,29 @@ static uint64_t pm_word(uint64_t q, int logN) {
     const bool lazy = (hu128)q * (uint64_t)(4 + 2 * logN) < ((hu128)1 << 64);   // fhs_ntt.h LAZY bound
     return (d << 8) | (lazy ? 128u : 0u) | (uint64_t)b;
 }
+
+// Bit 40 of PrimeK.pm: the ModUp conversion may reduce its split-30 sums directly
+// (fhs_modarith.h acc3_reduce_pm): with ns <= P source limbs (< 2^60 each) and the v (Q mod m)
+// correction folded into L, every intermediate of that routine stays in its word and the result is
+// below 2q.  Checked here with exact bounds for this prime.
+static bool conv_pm_ok(uint64_t q, int ns) {
+    const int b = 64 - __builtin_clzll(q);
+    if (b < 40 || b > 60 || ns < 1 || ns > 7) return false;
+    const hu128 d = ((hu128)1 << b) - q;
+    const hu128 p30 = ((hu128)1 << 30) - 1, M64 = ~(hu128)0 >> 64;   // 2^64 - 1
+    const hu128 Lmax = (hu128)ns * p30 * p30 + (hu128)ns * (q - 1);
+    const hu128 Mmax = (hu128)2 * ns * p30 * p30, Hmax = (hu128)ns * p30 * p30;
+    const int sh = b - 30;
+    const hu128 Amax = Lmax + ((((hu128)1 << sh) - 1) << 30);
+    const hu128 Bmax = (Mmax >> sh) + (Hmax << (60 - b));
+    if (Lmax > M64 || Mmax > M64 || Amax > M64 || Bmax > M64) return false;
+    if ((Bmax >> 64) != 0 || d >= ((hu128)1 << 32)) return false;
+    const hu128 Smax = Amax + Bmax * d;   // < 2^96
+    const hu128 Sh = Smax >> b;
+    if (Sh >= ((hu128)1 << 32)) return false;
+    const hu128 rmax = (((hu128)1 << b) - 1) + Sh * d;
+    return rmax < 2 * (hu128)q;
+}
 static bool h_is_prime(uint64_t n) {
     if (n < 2) return false;
     const uint64_t bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
@@ -515,7 +538,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
         }
         const uint64_t ninv = h_inv(N % q, q);
         const uint64_t w1n = h_mulmod(twi[((size_t)i * N + 1) * 2], ninv, q);
-        pk[i] = PrimeK{q, (uint64_t)r, (uint64_t)(r >> 64), ninv, h_shoup(ninv, q), w1n, h_shoup(w1n, q), pm_word(q, c->logN)};
+        pk[i] = PrimeK{q, (uint64_t)r, (uint64_t)(r >> 64), ninv, h_shoup(ninv, q), w1n, h_shoup(w1n, q), pm_word(q, c->logN) | (pm_word(q, c->logN) && conv_pm_ok(q, special) ? (1ull << 40) : 0ull)};
     }
     // ---- ModUp tables per level l: digit j covers [jP, min(jP+P, l))
     std::vector<uint64_t> mu_intt((size_t)(L0 + 1) * L0 * 4, 0), mu_hat((size_t)(L0 + 1) * dnum * P * K, 0);

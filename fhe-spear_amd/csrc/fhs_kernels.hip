@@ -597,7 +597,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
     const u64* yb = acoef + ((size_t)u * l + s0) * N;
     const u64* hat = T.modup_hat + (((size_t)l * T.dnum + j) * P_) * K + pt;
     const u64* qv = T.modup_Q + (((size_t)l * T.dnum + j) * K + pt) * 2;
-    const u64 Qm = qv[0], nsQm = qv[1];
+    const u64 Qm = qv[0], nsQm = qv[1], negQ = Qm ? m - Qm : 0;
     const unsigned char* vb = vcnt + ((size_t)u * dn + j) * N;
     const RedU R = redu(PM);
     const u64* tw = T.tw_fwd + (size_t)pt * N * 2;
@@ -628,10 +628,16 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
 #pragma unroll
         for (int k = 0; k < 2 * CH; ++k) {
             const int e = tid + (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);
-            u128 acc = {0, 0};
-            acc3_fold(acc, a3[k]);
-            mac128(acc, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
-            x[k] = submod(reduce128(acc.lo, acc.hi, R), nsQm, m);
+            if (R.cpm) {   // - v Q_S folded into L as v (m - Q_S mod m); result in [0, 2q)
+                const uint32_t v = vb[e];
+                const u64 vq = mul32w(v, (uint32_t)negQ) + ((u64)(v * (uint32_t)(negQ >> 32)) << 32);
+                x[k] = acc3_reduce_pm(a3[k].L + vq, a3[k].M, a3[k].H, R.b, R.d);
+            } else {
+                u128 acc = {0, 0};
+                acc3_fold(acc, a3[k]);
+                mac128(acc, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
+                x[k] = submod(reduce128(acc.lo, acc.hi, R), nsQm, m);
+            }
         }
 #pragma unroll
         for (int k = 0; k < CH; ++k) {   // global stage 0: (e, e + N/2), twiddle psi^rev(1)

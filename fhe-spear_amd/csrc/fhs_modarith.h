@@ -30,7 +30,7 @@ __host__ __device__ __forceinline__ u64 csub(u64 a, u64 q) { return a >= q ? a -
 // 64x64 products spelled out in 32-bit halves: gfx950 issues v_mad_u64_u32 / v_mul_lo_u32 /
 // v_mul_hi_u32 at about the rate of a 64-bit add (tools/microbench/instrate.hip), so what counts is
 // the instruction total; this form lets the compiler fold the carries into the mad accumulators.
-__device__ __forceinline__ u64 mul32w(uint32_t a, uint32_t b) { return (u64)a * b; }
+__host__ __device__ __forceinline__ u64 mul32w(uint32_t a, uint32_t b) { return (u64)a * b; }
 __device__ __forceinline__ u64 mulhi64x(u64 a, u64 b) {
     const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
     const u64 t = mul32w(a1, b0) + __umulhi(a0, b0);
@@ -125,6 +125,23 @@ __device__ __forceinline__ void acc3_mac(Acc3& a, Split30 x, Split30 y) {
     a.M += mul32w(x.hi, y.lo);
     a.H += mul32w(x.hi, y.hi);
 }
+// (L + M 2^30 + H 2^60) mod q, result in [0, 2q), for q = 2^b - d: the split-30 sums are cut at
+// bit b (A = L + (M mod 2^(b-30)) 2^30, B = M >> (b-30) + H 2^(60-b), x == A + B d) and folded once
+// more.  Valid when the host's conv_pm_ok bounds hold (PrimeK.pm bit 40); ~23 instructions against
+// ~37 for acc3_fold + pm_reduce128.
+__host__ __device__ __forceinline__ u64 acc3_reduce_pm(u64 L, u64 M, u64 H, unsigned b, unsigned d) {
+    const unsigned sh = b - 30;
+    const u64 A = L + ((M & ((1ull << sh) - 1)) << 30);
+    const u64 B = (M >> sh) + (H << (60 - b));
+    const u64 p0 = (u64)(uint32_t)B * d, p1 = (u64)(uint32_t)(B >> 32) * d;
+    u64 lo = A + p0;
+    u64 hi = (lo < p0);
+    const u64 p1l = p1 << 32;
+    lo += p1l;
+    hi += (lo < p1l) + (p1 >> 32);
+    const u64 Sh = (hi << (64 - b)) | (lo >> b);
+    return (lo & ((1ull << b) - 1)) + (u64)(uint32_t)Sh * d;
+}
 // c += L + M 2^30 + H 2^60 (< 2^123 for 8 products), then clear
 __device__ __forceinline__ void acc3_fold(u128& c, Acc3& a) {
     u64 lo = a.L, hi = 0;
@@ -171,7 +188,7 @@ struct PrimeK {
 };
 
 __device__ __forceinline__ u64 reduce128(u64 lo, u64 hi, const PrimeK& P) {
-    if (P.pm) return pm_reduce128(lo, hi, P.q, (unsigned)(P.pm & 127), (unsigned)(P.pm >> 8));
+    if (P.pm) return pm_reduce128(lo, hi, P.q, (unsigned)(P.pm & 127), (unsigned)((P.pm >> 8) & 0xFFFFFFFFu));
     return barrett128(lo, hi, P.q, P.r0, P.r1);
 }
 // Wave-uniform view of a prime's reduction constants (SGPRs): kernels whose prime is uniform per
@@ -185,10 +202,12 @@ struct RedU {
     u64 q, r0, r1;
     unsigned b, d;
     bool lazy;   // forward NTT may skip Harvey's conditional subtraction (PrimeK.pm bit 7)
+    bool cpm;    // ModUp conversion may use acc3_reduce_pm (PrimeK.pm bit 40)
 };
 __device__ __forceinline__ RedU redu(const PrimeK& P) {
     const u64 pm = rfl64(P.pm);
-    return RedU{rfl64(P.q), rfl64(P.r0), rfl64(P.r1), (unsigned)(pm & 127), (unsigned)(pm >> 8), (pm & 128) != 0};
+    return RedU{rfl64(P.q), rfl64(P.r0), rfl64(P.r1), (unsigned)(pm & 127), (unsigned)((pm >> 8) & 0xFFFFFFFFu),
+                (pm & 128) != 0, ((pm >> 40) & 1) != 0};
 }
 __device__ __forceinline__ u64 reduce128(u64 lo, u64 hi, const RedU& R) {
     if (R.b) return pm_reduce128(lo, hi, R.q, R.b, R.d);

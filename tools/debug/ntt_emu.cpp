@@ -69,8 +69,39 @@ static int run(int bits, int RLsel) {
     printf("LOGN=%d bits=%d lazy=%d RL=%d bad=%d\n", LOGN, bits, (int)LAZY, RLsel, bad);
     return bad;
 }
-int main() {
+// acc3_reduce_pm (ModUp conversion reduction) at its extreme inputs: ns = 3 source limbs of
+// 60-bit residues, v = 3, for 59- and 60-bit pseudo-Mersenne primes
+static int test_acc3_reduce() {
     int bad = 0;
+    std::mt19937_64 rng(5);
+    for (int bits : {59, 60}) {
+        const int N = 16384;
+        u64 q = ((1ull << bits) - 1) / (2 * N) * (2 * N) + 1;
+        while (!isprime(q)) q -= 2 * N;
+        const unsigned d = (unsigned)((1ull << bits) - q);
+        const u64 p30 = (1ull << 30) - 1;
+        for (int it = 0; it < 200000; ++it) {
+            u64 L, M, H;
+            if (it < 8) {   // corners
+                L = (it & 1) ? 3 * p30 * p30 + 3 * (q - 1) : 0;
+                M = (it & 2) ? 6 * p30 * p30 : 0;
+                H = (it & 4) ? 3 * p30 * p30 : 0;
+            } else {
+                L = rng() % (3 * p30 * p30 + 3 * (q - 1) + 1);
+                M = rng() % (6 * p30 * p30 + 1);
+                H = rng() % (3 * p30 * p30 + 1);
+            }
+            const u64 r = acc3_reduce_pm(L, M, H, bits, d);
+            const u128h x = (u128h)L + ((u128h)M << 30) + ((u128h)H << 60);
+            if (r >= 2 * q || r % q != (u64)(x % q)) { if (bad < 3) printf("  acc3 bits=%d it=%d\n", bits, it); ++bad; }
+        }
+    }
+    printf("acc3_reduce_pm bad=%d\n", bad);
+    return bad;
+}
+
+int main() {
+    int bad = test_acc3_reduce();
     bad += run<8, false>(59, 3) + run<8, true>(59, 3) + run<10, false>(59, 3) + run<10, true>(59, 3);
     bad += run<10, true>(59, 4) + run<9, true>(58, 3) + run<10, false>(60, 3) + run<11, true>(59, 3);
     printf(bad ? "FAIL\n" : "OK\n");
