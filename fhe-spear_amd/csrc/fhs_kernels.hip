@@ -30,6 +30,9 @@
 #ifndef FHS_INNER_LDS_MIN
 #define FHS_INNER_LDS_MIN 0
 #endif
+#ifndef FHS_MODDOWN_HALF
+#define FHS_MODDOWN_HALF 1
+#endif
 #ifndef FHS_INTT_HALF
 #define FHS_INTT_HALF 1       // k_ks_intt_h: half-limb LDS inverse NTT
 #endif
@@ -837,6 +840,89 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
     }
 }
 
+// k_moddown with half the limb in LDS (see k_modup_h): conversion of both coefficients of each
+// (e, e + N/2) pair, global NTT stage 0 in registers, then each half transformed in LDS and finished
+// ((acc - conv) P^-1 + sigma(c0)).  Same values as k_moddown.
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, const KsItem* items, const u64* acc,
+                                                                   const u64* ycoef, int l, int R) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
+    const int tid = threadIdx.x;
+    const int P_ = T.P, E = l + P_;
+    int i, mm;
+    if (!plain_tm(l, 2 * R, i, mm)) return;
+    const int comp = mm & 1, r = mm >> 1;
+    const PrimeK& P = PK(T, i);
+    const RedU RU = redu(P);
+    const u64 q = RU.q, q2 = 2 * q;
+    const KsItem it = items[r];
+    const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N;
+    const u64* tw = T.tw_fwd + (size_t)i * N * 2;
+    u64 w0, w0p;
+    ld_tw(tw, 1, w0, w0p);
+    u64 hi[16];
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {   // 2 pairs per chunk
+        Acc3 a3[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a3[k] = Acc3{0, 0, 0};
+#pragma unroll 1
+        for (int k = 0; k < P_; ++k) {   // P <= 7 products per Acc3
+            const Split30 hk = split30(T.md_hat[(size_t)k * T.L0 + i]);
+            const u64* yk = y + (size_t)k * N + tid;
+            u64 v[4];
+            v[0] = yk[(ch * 2) * TH];
+            v[1] = yk[(ch * 2 + 1) * TH];
+            v[2] = yk[(ch * 2) * TH + NH];
+            v[3] = yk[(ch * 2 + 1) * TH + NH];
+#pragma unroll
+            for (int z = 0; z < 4; ++z) acc3_mac(a3[z], split30(v[z]), hk);
+        }
+        u64 x[4];
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+            if (RU.cpm) {
+                x[z] = acc3_reduce_pm(a3[z].L, a3[z].M, a3[z].H, RU.b, RU.d);
+            } else {
+                u128 s = {0, 0};
+                acc3_fold(s, a3[z]);
+                x[z] = reduce128(s.lo, s.hi, RU);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {   // global stage 0: (e, e + N/2)
+            const int e = tid + (ch * 2 + k) * TH;
+            const u64 tt = shoup_lazy(x[2 + k], w0, w0p, q);
+            lds[lds_pad(e)] = x[k] + tt;
+            hi[ch * 2 + k] = x[k] + (q2 - tt);
+        }
+    }
+    const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
+    const u64* add = comp == 0 ? it.add0 : it.add1;
+    const u64 aelt = comp == 0 ? it.elt : 1;
+    u64* o = (comp == 0 ? it.out0 : it.out1) + (size_t)i * N;
+    const u64* ac = acc + (((size_t)r * 2 + comp) * E + i) * N;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {
+        if (h) {
+            __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = hi[c];
+        }
+        __syncthreads();
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, q, RU.lazy, 1 + h);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int e = h * NH + tid + c * TH;
+            const u64 v = fwd_canon(lds[lds_pad(tid + c * TH)], RU);
+            u64 res = shoup(submod(ac[e], v, q), pinv, pinv_s, q);
+            if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
+            o[e] = res;
+        }
+    }
+}
+
 size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l) {
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     // acoef | ext | acc | ycoef | centred counts (bytes, rounded up to words)
@@ -902,6 +988,9 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
         u64 *acc, *ycoef;
         ks_front<LOGN>(T, it, uq, R, U, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_MODDOWN, 1, st);
+        if (FHS_MODDOWN_HALF && LOGN >= 9)
+            hipLaunchKernelGGL((k_moddown_h<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc, ycoef, l, R);
+        else
         hipLaunchKernelGGL((k_moddown<LOGN>), dim3(FHS_MODDOWN_MAP == 1 ? xcd_grid(l, 2 * R) : l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
         FHS_TMARK(tm, KID_MODDOWN, 0, st);
     });
