@@ -168,7 +168,9 @@ __host__ __device__ __forceinline__ u64 sm64(u64 x) {
 // sampling: exactly uniform; for SEAL-style primes a retry has probability (2^bits - q) / 2^bits <
 // 2^-32).  `kx` = key + (prime 2^20 | n) * gamma is hoisted by callers that vary only the key.
 __host__ __device__ __forceinline__ u64 seeded_uniform_x(u64 kx, u64 q, unsigned bits) {
-    for (u64 m = 0;; ++m) {
+    const u64 v0 = sm64(kx) >> (64 - bits);
+    if (__builtin_expect(v0 < q, 1)) return v0;
+    for (u64 m = 1;; ++m) {   // taken with probability < 2^-32 per draw for SEAL-style primes
         const u64 v = sm64(kx + (m << 40) * 0x9E3779B97F4A7C15ULL) >> (64 - bits);
         if (v < q) return v;
     }

@@ -7,6 +7,7 @@
 #define __host__
 #define __global__
 #define __forceinline__ inline
+#define __noinline__ __attribute__((noinline))
 #define __shared__
 struct ulonglong2 { unsigned long long x, y; };
 static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
