@@ -464,8 +464,8 @@ struct Guard {
 extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int nprimes, int special,
                                          const uint64_t* galois_elts, int n_elts, int device, fhs_context** out) {
     if (!primes || !out) return fail(FHS_ERR_INVALID, "context_create: null argument");
-    if (N < 256 || N > 16384 || (N & (N - 1)))
-        return fail(FHS_ERR_INVALID, "context_create: poly_modulus_degree must be a power of two in [256, 16384]");
+    if (N < 256 || N > 32768 || (N & (N - 1)))
+        return fail(FHS_ERR_INVALID, "context_create: poly_modulus_degree must be a power of two in [256, 32768]");
     if (special < 1 || special >= nprimes) return fail(FHS_ERR_INVALID, "context_create: bad special modulus size");
     const int L0 = nprimes - special;
     if (L0 % special != 0)

@@ -69,6 +69,7 @@ namespace fhs {
         case 12: { constexpr int LOGN = 12; __VA_ARGS__; } break; \
         case 13: { constexpr int LOGN = 13; __VA_ARGS__; } break; \
         case 14: { constexpr int LOGN = 14; __VA_ARGS__; } break; \
+        case 15: { constexpr int LOGN = 15; __VA_ARGS__; } break; \
         default: return hipErrorInvalidValue;          \
     }
 
@@ -127,50 +128,126 @@ __device__ __forceinline__ int galois_src(int e, u64 elt, int logN) {
 template <int LOGN>
 constexpr size_t lds_bytes() { return (size_t)((1 << LOGN) + (1 << LOGN) / 16) * 8; }
 
-// ============================================================================ plain NTT
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_fwd(DevTables T, u64* data, int limbs, int l_split,
-                                                              size_t poly_stride) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, b = blockIdx.x;
-    const int pi = limb_prime(b, l_split, T.L0);
-    const RedU R = redu(PK(T, pi));
-    const u64 q = R.q;
-    u64* p = data + blockIdx.y * poly_stride + (size_t)b * N;
+// ---- one-limb transforms, full limb in LDS (N <= 16384: 136 KiB) or half a limb (N = 32768):
+// the half form does the global first forward stage / last inverse stage, which pairs e with
+// e + N/2, in registers and transforms each half in LDS (k_modup_h explains the scheme).
+template <int LOGN> constexpr bool ntt_half() { return LOGN > 14; }
+template <int LOGN> constexpr int ntt_threads() { return ntt_half<LOGN>() ? (1 << LOGN) / 32 : (1 << LOGN) / 16; }
+template <int LOGN> constexpr int ntt_lds_words() {
+    return ntt_half<LOGN>() ? (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16 : (1 << LOGN) + (1 << LOGN) / 16;
+}
+// forward: load(e) < 2q for every e < N; store(e, v) receives the canonical NTT value
+template <int LOGN, int RL, class Load, class Store>
+__device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restrict__ tw, const RedU& R, Load load,
+                                         Store store) {
+    constexpr int N = 1 << LOGN;
+    if constexpr (!ntt_half<LOGN>()) {
+        constexpr int TH = N / 16;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = p[tid + k * TH];
-    __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)pi * N * 2, q, R.lazy);
+        for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = load(tid + c * TH);
+        __syncthreads();
+        ntt_fwd_lds<LOGN, RL>(lds, tid, tw, R.q, R.lazy);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
-        p[e] = fwd_canon(lds[lds_pad(e)], R);
+        for (int c = 0; c < 16; ++c) store(tid + c * TH, fwd_canon(lds[lds_pad(tid + c * TH)], R));
+    } else {
+        constexpr int NH = N / 2, TH = N / 32;
+        const u64 q = R.q, q2 = 2 * q;
+        u64 w0, w0p;
+        ld_tw(tw, 1, w0, w0p);
+        u64 hi[16];
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int e = tid + c * TH;
+            const u64 xl = load(e), tt = shoup_lazy(load(e + NH), w0, w0p, q);
+            lds[lds_pad(e)] = xl + tt;
+            hi[c] = xl + (q2 - tt);
+        }
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {
+            if (h) {
+                __syncthreads();
+#pragma unroll
+                for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = hi[c];
+            }
+            __syncthreads();
+            ntt_fwd_lds<LOGN - 1, 3>(lds, tid, tw, q, R.lazy, 1 + h);
+#pragma unroll
+            for (int c = 0; c < 16; ++c) store(h * NH + tid + c * TH, fwd_canon(lds[lds_pad(tid + c * TH)], R));
+        }
+    }
+}
+// inverse with the last stage scaled by (s0, s1) (N^-1 and any per-limb constant folded in);
+// load(e) < 2q; store(e, v) receives the canonical coefficient
+template <int LOGN, int RL, class Load, class Store>
+__device__ __forceinline__ void inv_limb(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
+                                         u64 s1, u64 s1s, Load load, Store store) {
+    constexpr int N = 1 << LOGN;
+    if constexpr (!ntt_half<LOGN>()) {
+        constexpr int TH = N / 16;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = load(tid + c * TH);
+        __syncthreads();
+        ntt_inv_lds<LOGN, RL>(lds, tid, tw, q, s0, s0s, s1, s1s);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) store(tid + c * TH, csub(lds[lds_pad(tid + c * TH)], q));
+    } else {
+        constexpr int NH = N / 2, TH = N / 32;
+        u64 lo[16];
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {
+            if (h) __syncthreads();
+#pragma unroll
+            for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = load(h * NH + tid + c * TH);
+            __syncthreads();
+            ntt_inv_half_lds<LOGN - 1, 3>(lds, tid, tw, q, 1 + h);
+            if (h == 0) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) lo[c] = lds[lds_pad(tid + c * TH)];
+            }
+        }
+        const u64 q2 = 2 * q;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int e = tid + c * TH;
+            const u64 X = lo[c], Y = lds[lds_pad(e)];
+            store(e, csub(shoup_lazy(X + Y, s0, s0s, q), q));
+            store(NH + e, csub(shoup_lazy(X - Y + q2, s1, s1s, q), q));
+        }
     }
 }
 
+// ============================================================================ plain NTT
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_inv(DevTables T, u64* data, int limbs, int l_split,
-                                                              size_t poly_stride) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, b = blockIdx.x;
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd(DevTables T, u64* data, int limbs, int l_split,
+                                                                 size_t poly_stride) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int b = blockIdx.x;
+    const int pi = limb_prime(b, l_split, T.L0);
+    const RedU R = redu(PK(T, pi));
+    u64* p = data + blockIdx.y * poly_stride + (size_t)b * N;
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)pi * N * 2, R, [&](int e) { return p[e]; },
+                               [&](int e, u64 v) { p[e] = v; });
+}
+
+template <int LOGN>
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_inv(DevTables T, u64* data, int limbs, int l_split,
+                                                                 size_t poly_stride) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int b = blockIdx.x;
     const int pi = limb_prime(b, l_split, T.L0);
     const PrimeK& P = PK(T, pi);
     u64* p = data + blockIdx.y * poly_stride + (size_t)b * N;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = p[tid + c * TH];
-    __syncthreads();
-    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) p[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
+    inv_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv,
+                               P.w1ninv_s, [&](int e) { return p[e]; }, [&](int e, u64 v) { p[e] = v; });
 }
 
 hipError_t launch_ntt_fwd(const DevTables& T, u64* data, int limbs, int l_split, int npoly, size_t poly_stride,
                           hipStream_t st) {
     if (limbs <= 0 || npoly <= 0) return hipSuccess;
     FHS_DISPATCH_LOGN(T.logN, {
-        hipLaunchKernelGGL((k_ntt_fwd<LOGN>), dim3(limbs, npoly), dim3((1 << LOGN) / 16), 0, st, T,
+        hipLaunchKernelGGL((k_ntt_fwd<LOGN>), dim3(limbs, npoly), dim3(ntt_threads<LOGN>()), 0, st, T,
                            data, limbs, l_split, poly_stride);
     });
     return hipGetLastError();
@@ -179,7 +256,7 @@ hipError_t launch_ntt_inv(const DevTables& T, u64* data, int limbs, int l_split,
                           hipStream_t st) {
     if (limbs <= 0 || npoly <= 0) return hipSuccess;
     FHS_DISPATCH_LOGN(T.logN, {
-        hipLaunchKernelGGL((k_ntt_inv<LOGN>), dim3(limbs, npoly), dim3((1 << LOGN) / 16), 0, st, T,
+        hipLaunchKernelGGL((k_ntt_inv<LOGN>), dim3(limbs, npoly), dim3(ntt_threads<LOGN>()), 0, st, T,
                            data, limbs, l_split, poly_stride);
     });
     return hipGetLastError();
@@ -288,53 +365,43 @@ hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int l
 // ============================================================================ rescale (pb:185)
 // 1) last limb of each component -> coefficient form (scratch[comp])
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_intt(DevTables T, const u64* in, u64* scratch, int l) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, comp = blockIdx.x, pi = l - 1;
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_rescale_intt(DevTables T, const u64* in, u64* scratch, int l) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int comp = blockIdx.x, pi = l - 1;
     const PrimeK& P = PK(T, pi);
     const u64* src = in + ((size_t)comp * l + pi) * N;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[tid + c * TH];
-    __syncthreads();
-    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, P.ninv, P.ninv_s, P.w1ninv, P.w1ninv_s);
-    const u64 half = P.q >> 1;
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        scratch[(size_t)comp * N + tid + k * TH] = addmod(csub(lds[lds_pad(tid + k * TH)], P.q), half, P.q);
+    u64* dst = scratch + (size_t)comp * N;
+    const u64 half = P.q >> 1, q = P.q;
+    inv_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, q, P.ninv, P.ninv_s, P.w1ninv,
+                               P.w1ninv_s, [&](int e) { return src[e]; },
+                               [&](int e, u64 v) { dst[e] = addmod(v, half, q); });
 }
 // 2) per (i < l-1, comp): NTT_i([v mod q_i] - [half mod q_i]) and combine (a_i - t) * q_last^-1
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_rescale_ntt(DevTables T, const u64* in, const u64* scratch,
-                                                                  u64* out, int l) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, i = blockIdx.x, comp = blockIdx.y;
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_rescale_ntt(DevTables T, const u64* in, const u64* scratch,
+                                                                     u64* out, int l) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int i = blockIdx.x, comp = blockIdx.y;
     const PrimeK& P = PK(T, i);
-    const u64* rs = T.rescale + ((size_t)l * T.L0 + i) * 4;   // inv, inv_s, half mod q_i
-    const u64 inv = rs[0], inv_s = rs[1], hq = rs[2];
-    const u64* src = scratch + (size_t)comp * N;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = submod(reduce64(src[tid + k * TH], P), hq, P.q);
-    __syncthreads();
     const RedU RU = redu(P);
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q, RU.lazy);
+    const u64* rs = T.rescale + ((size_t)l * T.L0 + i) * 4;   // inv, inv_s, half mod q_i
+    const u64 inv = rs[0], inv_s = rs[1], hq = rs[2], q = RU.q;
+    const u64* src = scratch + (size_t)comp * N;
     const u64* a = in + ((size_t)comp * l + i) * N;
     u64* o = out + ((size_t)comp * (l - 1) + i) * N;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
-        const u64 t = fwd_canon(lds[lds_pad(e)], RU);
-        o[e] = shoup(submod(a[e], t, P.q), inv, inv_s, P.q);
-    }
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)i * N * 2, RU,
+                               [&](int e) { return submod(reduce64(src[e], P), hq, q); },
+                               [&](int e, u64 t) { o[e] = shoup(submod(a[e], t, q), inv, inv_s, q); });
 }
 hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
                           hipStream_t st, const KTimer* tm) {
     FHS_TMARK(tm, KID_RESCALE, 1, st);
     FHS_DISPATCH_LOGN(T.logN, {
-        hipLaunchKernelGGL((k_rescale_intt<LOGN>), dim3(ncomp), dim3((1 << LOGN) / 16), 0, st, T,
+        hipLaunchKernelGGL((k_rescale_intt<LOGN>), dim3(ncomp), dim3(ntt_threads<LOGN>()), 0, st, T,
                            in, scratch, l);
-        hipLaunchKernelGGL((k_rescale_ntt<LOGN>), dim3(l - 1, ncomp), dim3((1 << LOGN) / 16), 0, st,
+        hipLaunchKernelGGL((k_rescale_ntt<LOGN>), dim3(l - 1, ncomp), dim3(ntt_threads<LOGN>()), 0, st,
                            T, in, scratch, out, l);
     });
     FHS_TMARK(tm, KID_RESCALE, 0, st);
@@ -347,7 +414,8 @@ hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scra
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const u64* const* uniq, u64* acoef, int l, int U) {
     constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_half<LOGN>() ? 1 : (1 << LOGN) + (1 << LOGN) / 16];
+    if constexpr (!ntt_half<LOGN>()) {   // full-limb form: N <= 16384 only
     const int tid = threadIdx.x;
     int i, u;
     if (!plain_tm(l, U, i, u)) return;
@@ -361,6 +429,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const
     u64* dst = acoef + ((size_t)u * l + i) * N;
 #pragma unroll
     for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
+    }
 }
 
 // k_ks_intt with half the limb in LDS (two workgroups per CU, co-resident with the half-limb ModUp
@@ -496,7 +565,8 @@ template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u64* const* uniq, const u64* acoef,
                                                             const unsigned char* vcnt, u64* ext, int l, int U) {
     constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_half<LOGN>() ? 1 : (1 << LOGN) + (1 << LOGN) / 16];
+    if constexpr (!ntt_half<LOGN>()) {   // full-limb form: N <= 16384 only
     const int tid = threadIdx.x;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     int t, mi;
@@ -566,6 +636,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
         o[e] = fwd_canon(lds[lds_pad(e)], R);
+    }
     }
 }
 
@@ -673,7 +744,7 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
                          u64* ext, int l, int U, hipStream_t st) {
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     const int mgrid = FHS_MODUP_MAP == 1 ? xcd_grid(E, dn * U) : FHS_MODUP_MAP == 2 ? xcd_grid_m(E, dn * U) : E * dn * U;
-    if (FHS_MODUP_HALF && LOGN >= 9)
+    if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>())
         hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
@@ -776,24 +847,18 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
 
 // (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_special_intt(DevTables T, const u64* acc, u64* ycoef, int l,
-                                                                      int R) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, k = blockIdx.x, comp = blockIdx.y, r = blockIdx.z;
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ks_special_intt(DevTables T, const u64* acc, u64* ycoef, int l,
+                                                                         int R) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int k = blockIdx.x, comp = blockIdx.y, r = blockIdx.z;
     const int P_ = T.P, E = l + P_, pi = T.L0 + k;
     const PrimeK& P = PK(T, pi);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
-        lds[lds_pad(e)] = acc[(((size_t)r * 2 + comp) * E + l + k) * N + e];
-    }
-    __syncthreads();
-    const u64* cst = T.md_intt + (size_t)k * 4;
-    ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
+    const u64* src = acc + (((size_t)r * 2 + comp) * E + l + k) * N;
     u64* dst = ycoef + (((size_t)r * 2 + comp) * P_ + k) * N;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) dst[tid + kk * TH] = csub(lds[lds_pad(tid + kk * TH)], P.q);
+    const u64* cst = T.md_intt + (size_t)k * 4;
+    inv_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3],
+                               [&](int e) { return src[e]; }, [&](int e, u64 v) { dst[e] = v; });
 }
 
 // (d) ModDown: out_c[i] = (acc_c[i] - NTT(conv_P->q_i(y_c))) * P^-1 (+ add_c)
@@ -801,7 +866,8 @@ template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const KsItem* items, const u64* acc,
                                                               const u64* ycoef, int l, int R) {
     constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_half<LOGN>() ? 1 : (1 << LOGN) + (1 << LOGN) / 16];
+    if constexpr (!ntt_half<LOGN>()) {   // full-limb form: N <= 16384 only
     const int tid = threadIdx.x;
     const int P_ = T.P, E = l + P_;
     int i, m;
@@ -837,6 +903,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
         u64 res = shoup(submod(a, v, q), pinv, pinv_s, q);
         if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
         o[e] = res;
+    }
     }
 }
 
@@ -943,7 +1010,7 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     unsigned char* vcnt = reinterpret_cast<unsigned char*>(ycoef + (size_t)R * 2 * T.P * N);
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    if (FHS_INTT_HALF && LOGN >= 9)
+    if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
         hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, l, U);
     else
         hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, acoef, l, U);
@@ -957,7 +1024,7 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
                        0);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), blk, 0, st, T, acc, ycoef, l, R);
+    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, st, T, acc, ycoef, l, R);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
     *acc_out = acc;
     *ycoef_out = ycoef;
@@ -988,7 +1055,7 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
         u64 *acc, *ycoef;
         ks_front<LOGN>(T, it, uq, R, U, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_MODDOWN, 1, st);
-        if (FHS_MODDOWN_HALF && LOGN >= 9)
+        if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>())
             hipLaunchKernelGGL((k_moddown_h<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc, ycoef, l, R);
         else
         hipLaunchKernelGGL((k_moddown<LOGN>), dim3(FHS_MODDOWN_MAP == 1 ? xcd_grid(l, 2 * R) : l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
@@ -1121,25 +1188,18 @@ __global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, con
     }
 }
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_giant_final(DevTables T, const u64* base, const u64* convsum,
-                                                                  u64* out, int l) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, i = blockIdx.x, comp = blockIdx.y;
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_giant_final(DevTables T, const u64* base, const u64* convsum,
+                                                                     u64* out, int l) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int i = blockIdx.x, comp = blockIdx.y;
     const PrimeK& P = PK(T, i);
-    const size_t off = ((size_t)comp * l + i) * N;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = convsum[off + tid + k * TH];
-    __syncthreads();
     const RedU RU = redu(P);
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)i * N * 2, P.q, RU.lazy);
-    const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
-        const u64 v = fwd_canon(lds[lds_pad(e)], RU);
-        out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, P.q), P.q);
-    }
+    const size_t off = ((size_t)comp * l + i) * N;
+    const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1], q = RU.q;
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)i * N * 2, RU,
+                               [&](int e) { return convsum[off + e]; },
+                               [&](int e, u64 v) { out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, q), q); });
 }
 
 // ---- key-switch stages on explicit buffers (the pipelined BSGS launcher runs them per chunk)
@@ -1169,7 +1229,7 @@ static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, in
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    if (FHS_INTT_HALF && LOGN >= 9)
+    if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
         hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, b.acoef, l, U);
     else
         hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, b.acoef, l, U);
@@ -1188,7 +1248,7 @@ static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* cons
     hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3((1 << LOGN) / 16), 0, st, T, b.acc, b.ycoef, l, R);
+    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, st, T, b.acc, b.ycoef, l, R);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
 }
 
@@ -1289,7 +1349,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         hipEventRecord(ev_end, sa);
         hipStreamWaitEvent(sm, ev_end, 0);
         FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-        hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3((1 << LOGN) / 16), 0, sm, T, base, convsum, out, l);
+        hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum, out, l);
         FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
     });
     return hipGetLastError();
@@ -1443,27 +1503,16 @@ __global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64*
 // LDS (f64), then each coefficient is scaled, rounded (half away from zero, as the host decoder's
 // inverse) and reduced exactly mod every limb's prime.  The NTT follows (k_ntt_fwd_ptrs).
 template <int LOGN>
-__global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024)
-    k_encode(DevTables T, const double* vals, size_t n, size_t stride, int is_real, double scale, u64* const* outs,
-             int l) {
-    constexpr int N = 1 << LOGN, H = N / 2, LOGH = LOGN - 1;
-    constexpr int TH = (N / 16) < 1024 ? (N / 16) : 1024;
-    __shared__ double2 a[H];
-    const int tid = threadIdx.x;
-    const double* src = vals + (size_t)blockIdx.x * stride;
-    for (int j = tid; j < H; j += TH) {
-        double2 z = {0.0, 0.0};
-        if ((size_t)j < n) z = is_real ? double2{src[j], 0.0} : double2{src[2 * j], src[2 * j + 1]};
-        a[T.enc_pos[j]] = z;
-    }
-    __syncthreads();
-    const double2* W = reinterpret_cast<const double2*>(T.enc_w);
-    for (int s = 0; s < LOGH; ++s) {
+__device__ __forceinline__ void enc_fft_stages(double2* a, int tid, int TH, int n_pts, int log_pts, const double2* W,
+                                               int logh) {
+    // radix-2 DIT over n_pts = 2^log_pts points in LDS, bit-reversed in, natural out; twiddles of
+    // the full 2^logh-point transform (a sub-FFT uses the same ones)
+    for (int s = 0; s < log_pts; ++s) {
         const int half = 1 << s;
-        for (int b = tid; b < H / 2; b += TH) {
+        for (int b = tid; b < n_pts / 2; b += TH) {
             const int k = b & (half - 1);
             const int i = ((b >> s) << (s + 1)) + k, j = i + half;
-            const double2 w = W[(size_t)k << (LOGH - 1 - s)];
+            const double2 w = W[(size_t)k << (logh - 1 - s)];
             const double2 x = a[i], y = a[j];
             const double2 t = {y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x};
             a[i] = double2{x.x + t.x, x.y + t.y};
@@ -1471,36 +1520,80 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
         }
         __syncthreads();
     }
-    const double2* Z = reinterpret_cast<const double2*>(T.enc_twist);
+}
+template <int LOGN>
+__device__ __forceinline__ void enc_finish(const DevTables& T, double2 v, int k, double scale, u64* out, int l) {
+    constexpr int N = 1 << LOGN, H = N / 2;
+    const double2 z = reinterpret_cast<const double2*>(T.enc_twist)[k];
+    const double lo = round((v.x * z.x - v.y * z.y) * scale);
+    const double hi = round((v.x * z.y + v.y * z.x) * scale);
+    for (int i = 0; i < l; ++i) {
+        out[(size_t)i * N + k] = dbl_mod(T, lo, i);
+        out[(size_t)i * N + H + k] = dbl_mod(T, hi, i);
+    }
+}
+template <int LOGN>
+__global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024)
+    k_encode(DevTables T, const double* vals, size_t n, size_t stride, int is_real, double scale, u64* const* outs,
+             int l) {
+    constexpr int N = 1 << LOGN, H = N / 2, LOGH = LOGN - 1;
+    constexpr int TH = (N / 16) < 1024 ? (N / 16) : 1024;
+    constexpr bool SPLIT = LOGN > 14;   // N = 32768: the H-point FFT as two H/2-point halves + a final stage
+    __shared__ double2 a[SPLIT ? H / 2 : H];
+    const int tid = threadIdx.x;
+    const double* src = vals + (size_t)blockIdx.x * stride;
+    const double2* W = reinterpret_cast<const double2*>(T.enc_w);
     u64* out = outs[blockIdx.x];
-    for (int k = tid; k < H; k += TH) {
-        const double2 v = a[k], z = Z[k];
-        const double lo = round((v.x * z.x - v.y * z.y) * scale);
-        const double hi = round((v.x * z.y + v.y * z.x) * scale);
-        for (int i = 0; i < l; ++i) {
-            out[(size_t)i * N + k] = dbl_mod(T, lo, i);
-            out[(size_t)i * N + H + k] = dbl_mod(T, hi, i);
+    if constexpr (!SPLIT) {
+        for (int j = tid; j < H; j += TH) {
+            double2 z = {0.0, 0.0};
+            if ((size_t)j < n) z = is_real ? double2{src[j], 0.0} : double2{src[2 * j], src[2 * j + 1]};
+            a[T.enc_pos[j]] = z;
+        }
+        __syncthreads();
+        enc_fft_stages<LOGN>(a, tid, TH, H, LOGH, W, LOGH);
+        for (int k = tid; k < H; k += TH) enc_finish<LOGN>(T, a[k], k, scale, out, l);
+    } else {
+        // bit-reversed input: slots with rev(s_j) < H/2 form the first half's sub-FFT
+        constexpr int HH = H / 2, PER = HH / TH;
+        double2 lo[PER];
+        for (int h = 0; h < 2; ++h) {
+            if (h) __syncthreads();
+            for (int j = tid; j < H; j += TH) {
+                const unsigned pos = T.enc_pos[j];
+                if ((int)(pos / HH) != h) continue;
+                double2 z = {0.0, 0.0};
+                if ((size_t)j < n) z = is_real ? double2{src[j], 0.0} : double2{src[2 * j], src[2 * j + 1]};
+                a[pos - h * HH] = z;
+            }
+            __syncthreads();
+            enc_fft_stages<LOGN>(a, tid, TH, HH, LOGH - 1, W, LOGH);
+            if (h == 0) {
+#pragma unroll
+                for (int c = 0; c < PER; ++c) lo[c] = a[tid + c * TH];
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < PER; ++c) {   // last stage: pairs (k, k + H/2), twiddle omega^-k
+            const int k = tid + c * TH;
+            const double2 x = lo[c], y = a[k], w = W[k];
+            const double2 t = {y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x};
+            enc_finish<LOGN>(T, double2{x.x + t.x, x.y + t.y}, k, scale, out, l);
+            enc_finish<LOGN>(T, double2{x.x - t.x, x.y - t.y}, k + HH, scale, out, l);
         }
     }
 }
 
 // forward NTT of `limbs` limbs of each polynomial ptrs[blockIdx.y] (plaintext batches)
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ntt_fwd_ptrs(DevTables T, u64* const* ptrs, int limbs) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x, b = blockIdx.x;
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_ptrs(DevTables T, u64* const* ptrs, int limbs) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int b = blockIdx.x;
     const RedU R = redu(PK(T, b));
     u64* p = ptrs[blockIdx.y] + (size_t)b * N;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) lds[lds_pad(tid + k * TH)] = p[tid + k * TH];
-    __syncthreads();
-    ntt_fwd_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_fwd + (size_t)b * N * 2, R.q, R.lazy);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
-        p[e] = fwd_canon(lds[lds_pad(e)], R);
-    }
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R, [&](int e) { return p[e]; },
+                               [&](int e, u64 v) { p[e] = v; });
 }
 
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
@@ -1510,7 +1603,7 @@ hipError_t launch_encode(const DevTables& T, const double* vals, int count, size
         constexpr int TH = ((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024;
         hipLaunchKernelGGL((k_encode<LOGN>), dim3(count), dim3(TH), 0, st, T, vals, n, stride, is_real ? 1 : 0, scale,
                            outs_dev, l);
-        hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3((1 << LOGN) / 16), 0, st, T, outs_dev, l);
+        hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T, outs_dev, l);
     });
     return hipGetLastError();
 }

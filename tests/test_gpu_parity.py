@@ -45,7 +45,7 @@ def rand_pt(o, rng, l):
     return np.stack([rng.integers(0, o.primes[i], o.N, dtype=np.uint64) for i in range(l)])
 
 
-PARAMS = [(1024, 6, 3), (2048, 4, 1), (4096, 6, 2)]
+PARAMS = [(1024, 6, 3), (2048, 4, 1), (4096, 6, 2), (32768, 3, 1)]   # N = 32768: half-limb NTT forms
 
 
 @pytest.mark.parametrize("N,L0,P", PARAMS)
@@ -260,3 +260,45 @@ def test_errors(ph):
     parms.set_coeff_modulus(ph.create_coeff_modulus(1024, [59] * 8))   # L0 = 5, not a multiple of 3
     with pytest.raises(ValueError):
         ph.context(parms)
+
+
+def test_n32768_encode_bsgs_and_fused_equals_loop(ph):
+    """cfg5's ring size (N = 32768, BASELINE configs[4]): every NTT runs in its half-limb form and
+    the encoder FFT in its split form; decode accuracy, fused BSGS == op-by-op loop, and the
+    decrypted matvec."""
+    import __graft_entry__ as ge
+    N, L0, P, D = 32768, 3, 1, 64
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=11)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(12)
+    z = rng.normal(0, 1, N // 2) + 1j * rng.normal(0, 1, N // 2)
+    assert np.max(np.abs(np.array(enc.decode_complex_vector(ctx, enc.encode_complex_vector(ctx, z, 2.0 ** 40))) - z)) < 1e-6
+    gk = sk.create_galois_keys(ctx)
+    x = rng.normal(0, 0.1, D)
+    W = rng.normal(0, 0.02, (D, D))
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), 2.0 ** 59))
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    pts = enc.encode_double_vector_batch(ctx, ge._rolled_diagonals(W, D, G, N // 2), 2.0 ** 59,
+                                         chain_index=ct.chain_index())
+    res = None
+    for g in range(B):
+        inner = None
+        for b in range(G):
+            k = g * G + b
+            if k >= D:
+                continue
+            term = ph.multiply_plain(ctx, baby[b], pts[k])
+            inner = term if inner is None else ph.add(ctx, inner, term)
+        if g > 0:
+            inner = ph.rotate(ctx, inner, g * G, gk)
+        res = inner if res is None else ph.add(ctx, res, inner)
+    res = ph.rescale_to_next(ctx, res)
+    fused = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    assert np.array_equal(fused.to_numpy(), res.to_numpy())
+    dec = np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, fused)))[:D]
+    ref = W @ x
+    assert np.corrcoef(dec, ref)[0, 1] > 0.999999
+    assert np.max(np.abs(dec - ref)) < 1e-8
