@@ -35,6 +35,8 @@ CONFIGS = {
     # BASELINE configs[0] shape (CPU-runnable case in the reference)
     "cfg1": dict(N=8192, L0=24, P=3, D=1024, workload="BSGS matvec d=1024 N=8192 L0=24 P=3 (62 rotations)"),
     "small": dict(N=4096, L0=6, P=3, D=256, workload="BSGS matvec d=256 N=4096 L0=6 P=3 (smoke size)"),
+    # BASELINE configs[4] ring (tf --N 32768 --L0 36 --P 3): one BSGS matvec of that 24-block run
+    "cfg5mv": dict(N=32768, L0=36, P=3, D=2048, workload="BSGS matvec d=2048 N=32768 L0=36 P=3 (cfg5 ring)"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 BFLY_PEAK_GOPS = 1466.6        # measured lazy NTT butterflies/s, registers only (tools/microbench/bfly.hip)
