@@ -302,3 +302,28 @@ def test_n32768_encode_bsgs_and_fused_equals_loop(ph):
     ref = W @ x
     assert np.corrcoef(dec, ref)[0, 1] > 0.999999
     assert np.max(np.abs(dec - ref)) < 1e-8
+
+
+def test_ffn_block_ct_ct_chain(ph):
+    """tf:26-118's FFN block (BSGS key chunks, CT x CT square + relinearize +
+    rescale, value chunks, mod_switch alignment, set_scale, residual add) decrypts to the plaintext
+    FFN (tf:272-298 pass criterion corr > 0.999) over two blocks."""
+    sys_path = str(Path(__file__).resolve().parents[1] / "tools")
+    import sys
+    if sys_path not in sys.path:
+        sys.path.insert(0, sys_path)
+    import ffn_block as fb
+    N, L0, P, D, F = 4096, 12, 3, 64, 128
+    rng = np.random.default_rng(7)
+    ck = fb.Ckks(ph, N, L0, P, D, seed=3)
+    x = rng.normal(0, 0.1, D)
+    ct = ck.encrypt_replicated(x)
+    ref = x.copy()
+    for _ in range(2):
+        Wk = rng.normal(0, 0.02, (D, F))
+        Wv = rng.normal(0, 0.02, (F, D))
+        ct = fb.ffn_block(ck, ct, Wk, Wv, D, F)
+        ref = fb.plain_ffn(ref, Wk, Wv)
+        dec = ck.decrypt(ct, D)
+        assert np.corrcoef(dec, ref)[0, 1] > 0.999
+        assert np.max(np.abs(dec - ref)) < 1e-6
