@@ -232,6 +232,9 @@ struct fhs_context {
     std::vector<std::complex<double>> fft_w;   // exp(2 pi i k / N), k < N
     std::vector<uint64_t> slot_index;          // (5^j mod 2N - 1)/2, j < N/2
     std::atomic<uint64_t> bytes_live{0};
+    // lifetime: the caller's reference + one per live object (ciphertext, plaintext, key), so objects
+    // may be destroyed after fhs_context_destroy (Python finalisation order is arbitrary)
+    std::atomic<int> refs{1};
     // caching allocator: freed device blocks are kept per exact size and reused in stream order
     // (every use of a block is ordered on `st`, aux-stream work is joined back into `st`).  A large
     // hipMallocAsync costs ~0.35 ms/GB of host time and each hipFreeAsync ~8 us (tools/microbench/
@@ -291,6 +294,9 @@ struct fhs_galois_keys {
     fhs_context* ctx;
     std::map<uint64_t, uint64_t*> keys;
 };
+
+static void ctx_retain(fhs_context* c) { c->refs.fetch_add(1); }
+static void ctx_release(fhs_context* c);
 
 // switching key in HBM: b_j [dnum][K][N] then the dnum seeds of the uniform a_j, which the key
 // inner product regenerates on the fly (SAMPLE_SEEDED): half the bytes of storing (b_j, a_j)
@@ -360,6 +366,7 @@ static fhs_status new_ct(fhs_context* c, int ncomp, int ci, double scale, fhs_ci
         delete ct;
         return hip_fail(e, "ciphertext allocation");
     }
+    ctx_retain(c);
     *out = ct;
     return FHS_OK;
 }
@@ -372,6 +379,7 @@ static fhs_status new_pt(fhs_context* c, int ci, double scale, fhs_plaintext** o
         delete pt;
         return hip_fail(e, "plaintext allocation");
     }
+    ctx_retain(c);
     *out = pt;
     return FHS_OK;
 }
@@ -705,8 +713,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     return FHS_OK;
 }
 
-extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
-    if (!c) return FHS_OK;
+static void ctx_free(fhs_context* c) {
     {
         Guard g(c);
         flush(c);
@@ -726,6 +733,13 @@ extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
         hipStreamDestroy(c->st);
     }
     delete c;
+}
+static void ctx_release(fhs_context* c) {
+    if (c->refs.fetch_sub(1) == 1) ctx_free(c);
+}
+extern "C" fhs_status fhs_context_destroy(fhs_context* c) {
+    if (!c) return FHS_OK;
+    ctx_release(c);
     return FHS_OK;
 }
 extern "C" fhs_status fhs_context_info(const fhs_context* c, uint64_t* N, int* L0, int* P, int* n_elts) {
@@ -774,13 +788,16 @@ extern "C" fhs_status fhs_secret_key_create(fhs_context* c, uint64_t seed, fhs_s
     if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key"); }
     e = sample_small_ntt(c, fhs::SAMPLE_TERNARY, stream_key(seed, stream_id(ST_SECRET, 0, 0)), sk->s, c->K);
     if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key sampling"); }
+    ctx_retain(c);
     *out = sk;
     return FHS_OK;
 }
 extern "C" fhs_status fhs_secret_key_destroy(fhs_secret_key* sk) {
     if (!sk) return FHS_OK;
-    { Guard g(sk->ctx); flush(sk->ctx); dfree(sk->ctx, sk->s, 8ull * sk->ctx->K * sk->ctx->N); }
+    fhs_context* c = sk->ctx;
+    { Guard g(c); flush(c); dfree(c, sk->s, 8ull * c->K * c->N); }
     delete sk;
+    ctx_release(c);
     return FHS_OK;
 }
 
@@ -842,13 +859,16 @@ extern "C" fhs_status fhs_gen_relin_key(fhs_context* c, fhs_secret_key* sk, fhs_
     fhs_status s = gen_switch_key(c, sk->seed, stream_id(ST_RELIN, 0, 0), sk->s, s2, &rk->key);
     dfree(c, s2, 8ull * c->K * c->N);
     if (s != FHS_OK) { delete rk; return s; }
+    ctx_retain(c);
     *out = rk;
     return FHS_OK;
 }
 extern "C" fhs_status fhs_relin_key_destroy(fhs_relin_key* rk) {
     if (!rk) return FHS_OK;
-    { Guard g(rk->ctx); flush(rk->ctx); dfree(rk->ctx, rk->key, 8 * key_words(rk->ctx)); }
+    fhs_context* c = rk->ctx;
+    { Guard g(c); flush(c); dfree(c, rk->key, 8 * key_words(c)); }
     delete rk;
+    ctx_release(c);
     return FHS_OK;
 }
 
@@ -882,17 +902,20 @@ extern "C" fhs_status fhs_create_galois_keys(fhs_context* c, fhs_secret_key* sk,
         delete gk;
         return hip_fail(e, "galois key generation");
     }
+    ctx_retain(c);
     *out = gk;
     return FHS_OK;
 }
 extern "C" fhs_status fhs_galois_keys_destroy(fhs_galois_keys* gk) {
     if (!gk) return FHS_OK;
+    fhs_context* c = gk->ctx;
     {
-        Guard g(gk->ctx);
-        flush(gk->ctx);
-        for (auto& kv : gk->keys) dfree(gk->ctx, kv.second, 8 * key_words(gk->ctx));
+        Guard g(c);
+        flush(c);
+        for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
     }
     delete gk;
+    ctx_release(c);
     return FHS_OK;
 }
 extern "C" fhs_status fhs_galois_keys_has(const fhs_galois_keys* gk, uint64_t elt, int* has) {
@@ -948,13 +971,16 @@ extern "C" fhs_status fhs_gen_public_key(fhs_context* c, fhs_secret_key* sk, fhs
                                         c->L0, c->st);
     dfree(c, eb, 8 * S);
     if (e != hipSuccess) { dfree(c, pk->pk, 16 * S); delete pk; return hip_fail(e, "public key generation"); }
+    ctx_retain(c);
     *out = pk;
     return FHS_OK;
 }
 extern "C" fhs_status fhs_public_key_destroy(fhs_public_key* pk) {
     if (!pk) return FHS_OK;
-    { Guard g(pk->ctx); flush(pk->ctx); dfree(pk->ctx, pk->pk, 16ull * pk->ctx->L0 * pk->ctx->N); }
+    fhs_context* c = pk->ctx;
+    { Guard g(c); flush(c); dfree(c, pk->pk, 16ull * c->L0 * c->N); }
     delete pk;
+    ctx_release(c);
     return FHS_OK;
 }
 extern "C" fhs_status fhs_public_key_export(fhs_context* c, const fhs_public_key* pk, uint64_t* host) {
@@ -975,12 +1001,15 @@ extern "C" fhs_status fhs_ciphertext_destroy(fhs_ciphertext* ct) {
         dfree(c, ct->d, ct_bytes(ct));
     }
     delete ct;
+    ctx_release(c);
     return FHS_OK;
 }
 extern "C" fhs_status fhs_plaintext_destroy(fhs_plaintext* pt) {
     if (!pt) return FHS_OK;
-    { Guard g(pt->ctx); dfree(pt->ctx, pt->d, pt_bytes(pt)); }
+    fhs_context* c = pt->ctx;
+    { Guard g(c); dfree(c, pt->d, pt_bytes(pt)); }
     delete pt;
+    ctx_release(c);
     return FHS_OK;
 }
 extern "C" fhs_status fhs_ciphertext_info(const fhs_ciphertext* ct, int* ncomp, int* ci, int* l, double* scale) {
@@ -1115,6 +1144,96 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
         if (ht.on) { hipStreamSynchronize(c->st); ht.mark("encode: gpu"); }
         if (e != hipSuccess) return hip_fail(e, "encode");
     }
+    return FHS_OK;
+}
+
+// Extended-precision encoder for constant plaintexts (bootstrapping transforms): the f64 FFT of
+// the GPU encoder has relative error ~2^-52 log n, i.e. hundreds of integer units at scale 2^59,
+// which CoeffToSlot multiplies by |I| ~ K (DESIGN.md §3 bootstrapping).  Here the N/2-point DFT
+// runs on the host in x87 long double (64-bit mantissa), each coefficient is rounded exactly to a
+// 128-bit integer (hi, lo), and the device reduces it mod every limb and runs the NTT.
+static void encode_precise_rows(const fhs_context* c, const double* vals, size_t n_in, size_t r0, size_t r1,
+                                long double scale, int64_t* hi, uint64_t* lo, std::atomic<int>* overflow) {
+    typedef std::complex<long double> cl;
+    const size_t N = c->N, n = N / 2;
+    int logn = 0;
+    while (((size_t)1 << logn) < n) ++logn;
+    const long double pi = acosl(-1.0L);
+    std::vector<cl> w(n / 2), tw(n), a(n);
+    for (size_t t = 0; t < n / 2; ++t) w[t] = cl(cosl(2 * pi * t / n), -sinl(2 * pi * t / n));   // omega^-t
+    for (size_t k = 0; k < n; ++k)                                                              // (2/N) zeta^-k
+        tw[k] = cl(cosl(pi * k / N), -sinl(pi * k / N)) * (2.0L / (long double)N);
+    const long double two64 = 18446744073709551616.0L;
+    for (size_t r = r0; r < r1; ++r) {
+        std::fill(a.begin(), a.end(), cl(0, 0));
+        for (size_t j = 0; j < n_in; ++j) {                       // Z[s_j] = z_j, 5^j = 4 s_j + 1
+            const size_t s = (size_t)(c->slot_index[j] >> 1);
+            a[h_bitrev((uint32_t)s, logn)] = cl(vals[(r * n_in + j) * 2], vals[(r * n_in + j) * 2 + 1]);
+        }
+        for (size_t len = 2; len <= n; len <<= 1) {               // DIT, natural-order output
+            const size_t step = n / len;
+            for (size_t i = 0; i < n; i += len)
+                for (size_t k = 0; k < len / 2; ++k) {
+                    const cl u = a[i + k], v = a[i + k + len / 2] * w[k * step];
+                    a[i + k] = u + v;
+                    a[i + k + len / 2] = u - v;
+                }
+        }
+        for (size_t k = 0; k < n; ++k) {
+            const cl ck = a[k] * tw[k];
+            const long double part[2] = {ck.real() * scale, ck.imag() * scale};
+            for (int h = 0; h < 2; ++h) {
+                const long double x = roundl(part[h]);
+                if (!(fabsl(x) < 0x1p126L)) { overflow->store(1); continue; }
+                const long double xh = floorl(x / two64);
+                const size_t idx = r * N + k + (size_t)h * n;
+                hi[idx] = (int64_t)xh;
+                lo[idx] = (uint64_t)(x - xh * two64);
+            }
+        }
+    }
+}
+extern "C" fhs_status fhs_encode_precise(fhs_context* c, const double* re_im, size_t count, size_t n, double scale,
+                                         int ci, fhs_plaintext** outs) {
+    ENTER(c);
+    if ((!re_im && n) || !outs) return fail(FHS_ERR_INVALID, "encode_precise: null argument");
+    if (n > c->N / 2) return fail(FHS_ERR_INVALID, "encode_precise: more values than slots");
+    if (!(scale > 0) || !std::isfinite(scale) || scale > 0x1p126) return fail(FHS_ERR_INVALID, "encode_precise: bad scale");
+    const int l = c->L0 + 1 - ci;
+    if (ci < 1 || l < 1) return fail(FHS_ERR_LEVEL, "encode: chain index out of range");
+    if (count == 0) return FHS_OK;
+    const size_t N = c->N;
+    std::vector<int64_t> hi(count * N);
+    std::vector<uint64_t> lo(count * N);
+    const size_t nth = std::max<size_t>(1, std::min<size_t>({count, 16, (size_t)std::thread::hardware_concurrency()}));
+    std::vector<std::thread> th;
+    std::atomic<int> overflow{0};
+    for (size_t t = 0; t < nth; ++t)
+        th.emplace_back(encode_precise_rows, c, re_im, n, count * t / nth, count * (t + 1) / nth, (long double)scale,
+                        hi.data(), lo.data(), &overflow);
+    for (auto& x : th) x.join();
+    if (overflow.load()) return fail(FHS_ERR_INVALID, "encode_precise: |value x scale| >= 2^126 (or not finite)");
+    uint64_t* dbuf = nullptr;
+    HIPCHK(dalloc(c, &dbuf, 16 * count * N), "encode_precise staging");
+    hipError_t e = hipMemcpyAsync(dbuf, hi.data(), 8 * count * N, hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(dbuf + count * N, lo.data(), 8 * count * N, hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    std::vector<uint64_t*> ptrs(count);
+    for (size_t v = 0; v < count && e == hipSuccess; ++v) {
+        fhs_plaintext* pt = nullptr;
+        fhs_status s = new_pt(c, ci, scale, &pt);
+        if (s != FHS_OK) { dfree(c, dbuf, 16 * count * N); return s; }
+        outs[v] = pt;
+        ptrs[v] = pt->d;
+    }
+    uint64_t* dptrs = nullptr;
+    if (e == hipSuccess) e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * count, &dptrs);
+    if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * count);
+    if (e == hipSuccess)
+        e = fhs::launch_encode_int128(c->T, reinterpret_cast<const int64_t*>(dbuf), dbuf + count * N, (int)count,
+                                      reinterpret_cast<fhs::u64* const*>(dptrs), l, c->st);
+    dfree(c, dbuf, 16 * count * N);
+    if (e != hipSuccess) return hip_fail(e, "encode_precise");
     return FHS_OK;
 }
 
@@ -1534,8 +1653,11 @@ extern "C" fhs_status fhs_rotate_many(fhs_context* c, const fhs_ciphertext* cons
 }
 
 // ============================================================================ fused BSGS
+// giant_elts: null = 5^(g G) (the matvec, bg:478-483); else B Galois elements, giant_elts[0] = 1.
+// rescale = false leaves the sum at the product scale (last SlotToCoeff group of the bootstrap).
 static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, int G, const uint64_t* const* pt_ptrs,
-                            int D, int B, int ci, double pt_scale, const fhs_galois_keys* gk, fhs_ciphertext** out) {
+                            int D, int B, int ci, double pt_scale, const fhs_galois_keys* gk, fhs_ciphertext** out,
+                            const uint64_t* giant_elts = nullptr, bool rescale = true) {
     if (G < 1 || D < 1 || !baby) return fail(FHS_ERR_INVALID, "bsgs: bad G/D");
     const int Beff = std::min(B, (D + G - 1) / G);
     if (Beff < 1) return fail(FHS_ERR_INVALID, "bsgs: no giant groups");
@@ -1545,11 +1667,12 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
         if (!baby[b] || baby[b]->l != l || baby[b]->ncomp != 2 || baby[b]->ci != ci)
             return fail(FHS_ERR_LEVEL, "bsgs: baby steps and diagonals must share one chain index");
     }
-    if (l < 2) return fail(FHS_ERR_LEVEL, "bsgs: no level left for the final rescale");
+    if (rescale && l < 2) return fail(FHS_ERR_LEVEL, "bsgs: no level left for the final rescale");
+    if (giant_elts && giant_elts[0] != 1) return fail(FHS_ERR_INVALID, "linear_transform: giant group 0 must be the identity");
     HostTrace ht;
     std::vector<const uint64_t*> keys(Beff, nullptr);
     for (int g = 1; g < Beff; ++g) {
-        const uint64_t elt = fhs_galois_elt_from_step(g * G, c->N);
+        const uint64_t elt = giant_elts ? giant_elts[g] : fhs_galois_elt_from_step(g * G, c->N);
         auto it = gk->keys.find(elt);
         if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "bsgs: galois key for a giant step is missing");
         keys[g] = it->second;
@@ -1575,11 +1698,18 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     ht.mark("workspaces");
     const fhs::BsgsStreams ss{c->st, c->st_aux, c->bsgs_ev.data(), (int)c->bsgs_ev.size(), c->bsgs_chunks,
                               c->bsgs_split_h};
-    HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), inner, sum, ws, wsb, c->items_dev,
+    HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), giant_elts, inner, sum, ws, wsb, c->items_dev,
                             c->stager, ss, tm),
            "bsgs");
     ht.mark("launch bsgs");
     fhs_ciphertext* r;
+    if (!rescale) {
+        fhs_status s = new_ct(c, 2, ci, baby[0]->scale * pt_scale, &r);
+        if (s != FHS_OK) return s;
+        HIPCHK(hipMemcpyAsync(r->d, sum, 8 * 2 * S, hipMemcpyDeviceToDevice, c->st), "linear_transform");
+        *out = r;
+        return FHS_OK;
+    }
     fhs_status s = new_ct(c, 2, ci + 1, baby[0]->scale * pt_scale / (double)c->q[l - 1], &r);
     if (s != FHS_OK) return s;
     uint64_t* scr = nullptr;
@@ -1602,6 +1732,91 @@ extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_cip
         p[k] = pts[k]->d;
     }
     return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out);
+}
+
+extern "C" fhs_status fhs_linear_transform(fhs_context* c, const fhs_ciphertext* const* baby, int G,
+                                           const fhs_plaintext* const* pts, int D, int B, const uint64_t* giant_elts,
+                                           const fhs_galois_keys* gk, int rescale, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!pts || !gk || !out || !baby || !giant_elts) return fail(FHS_ERR_INVALID, "null argument");
+    if (B < 1 || D != B * G) return fail(FHS_ERR_INVALID, "linear_transform: expects D = B * G plaintexts");
+    std::vector<const uint64_t*> p(D);
+    for (int k = 0; k < D; ++k) {
+        if (!pts[k] || pts[k]->ci != baby[0]->ci) return fail(FHS_ERR_LEVEL, "linear_transform: plaintext at a different chain index");
+        if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "linear_transform: plaintext scales differ");
+        p[k] = pts[k]->d;
+    }
+    for (int g = 0; g < B; ++g)
+        if ((giant_elts[g] & 1) == 0 || giant_elts[g] >= 2 * c->N) return fail(FHS_ERR_INVALID, "linear_transform: bad Galois element");
+    return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out, giant_elts, rescale != 0);
+}
+
+// ============================================================================ bootstrapping primitives
+// exact residue of the integer-valued double p modulo q
+static uint64_t dbl_int_mod(double p, uint64_t q) {
+    const bool neg = p < 0;
+    const double a = std::fabs(p);
+    uint64_t r;
+    if (a < 18446744073709551616.0) {
+        r = (uint64_t)a % q;
+    } else {
+        int e;
+        const double f = std::frexp(a, &e);              // a = f 2^e, f in [0.5, 1)
+        const uint64_t m = (uint64_t)std::ldexp(f, 53);  // exact 53-bit mantissa
+        r = h_mulmod(m % q, h_pow(2, (uint64_t)(e - 53), q), q);
+    }
+    return neg && r ? q - r : r;
+}
+static fhs_status scalar_consts(fhs_context* c, double v, int l, fhs::ScalarConsts& K) {
+    if (!std::isfinite(v)) return fail(FHS_ERR_INVALID, "constant is not finite");
+    if (l > fhs::kMaxScalarLimbs) return fail(FHS_ERR_INVALID, "too many limbs for a constant op");
+    const double p = std::round(v);                      // half away from zero
+    for (int i = 0; i < l; ++i) {
+        K.v[i] = dbl_int_mod(p, c->q[i]);
+        K.vs[i] = h_shoup(K.v[i], c->q[i]);
+    }
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_multiply_const(fhs_context* c, const fhs_ciphertext* a, double value, double const_scale,
+                                         fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (!(const_scale > 0) || !std::isfinite(const_scale)) return fail(FHS_ERR_INVALID, "multiply_const: bad scale");
+    fhs::ScalarConsts K;
+    fhs_status s = scalar_consts(c, value * const_scale, a->l, K);
+    if (s != FHS_OK) return s;
+    fhs_ciphertext* r;
+    s = new_ct(c, a->ncomp, a->ci, a->scale * const_scale, &r);
+    if (s != FHS_OK) return s;
+    HIPCHK(fhs::launch_scalar(c->T, fhs::SCALAR_MUL, a->d, r->d, a->ncomp, a->l, K, c->st), "multiply_const");
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_add_const(fhs_context* c, const fhs_ciphertext* a, double value, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    fhs::ScalarConsts K;
+    fhs_status s = scalar_consts(c, value * a->scale, a->l, K);
+    if (s != FHS_OK) return s;
+    fhs_ciphertext* r;
+    s = new_ct(c, a->ncomp, a->ci, a->scale, &r);
+    if (s != FHS_OK) return s;
+    HIPCHK(fhs::launch_scalar(c->T, fhs::SCALAR_ADD, a->d, r->d, a->ncomp, a->l, K, c->st), "add_const");
+    *out = r;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_mod_raise(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (a->ncomp != 2) return fail(FHS_ERR_INVALID, "mod_raise expects a 2-component ciphertext");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, 2, 1, a->scale, &r);
+    if (s != FHS_OK) return s;
+    uint64_t* scr = nullptr;
+    HIPCHK(scratch(c, fhs_context::SCR_RESCALE, 16ull * c->N, &scr), "mod_raise");
+    HIPCHK(fhs::launch_mod_raise(c->T, a->d, a->l, r->d, scr, 2, c->st), "mod_raise");
+    *out = r;
+    return FHS_OK;
 }
 
 extern "C" fhs_status fhs_host_alloc(uint64_t bytes, void** ptr) {

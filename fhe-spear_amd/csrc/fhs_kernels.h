@@ -85,9 +85,11 @@ struct BsgsStreams {
     int split_hadamard;   // 1: Hadamard per chunk on the aux stream; 0: one Hadamard launch on main
 };
 size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
+// giant_elts (host, B entries, may be null): Galois element of giant group g (g >= 1); null means
+// 5^(g G) mod 2N (the BSGS matvec of bg:464-485).  Group 0 is never rotated.
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
-                       int l, const u64* const* keys_host, u64* inner, u64* out, u64* workspace, size_t ws_bytes,
-                       void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
+                       int l, const u64* const* keys_host, const u64* giant_elts, u64* inner, u64* out, u64* workspace,
+                       size_t ws_bytes, void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
 // CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
 // apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
@@ -102,6 +104,23 @@ hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st);
 hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st);
+
+// per-limb constants for k_scalar (value mod q_i and its Shoup companion)
+constexpr int kMaxScalarLimbs = 64;
+struct ScalarConsts {
+    u64 v[kMaxScalarLimbs];
+    u64 vs[kMaxScalarLimbs];
+};
+enum ScalarOp { SCALAR_MUL = 0, SCALAR_ADD = 1 };
+hipError_t launch_scalar(const DevTables& T, int op, const u64* a, u64* out, int ncomp, int l, const ScalarConsts& K,
+                         hipStream_t st);
+// ModRaise (bootstrapping): limb 0 of each component -> centred lift to all L0 data limbs (NTT form)
+hipError_t launch_mod_raise(const DevTables& T, const u64* in, int l, u64* out, u64* scratch, int ncomp,
+                            hipStream_t st);
+
+// exact 128-bit integer coefficients (x = hi 2^64 + lo) reduced into every limb, then NTT
+hipError_t launch_encode_int128(const DevTables& T, const int64_t* hi, const u64* lo, int count, u64* const* outs_dev,
+                                int l, hipStream_t st);
 
 enum EltOp { OP_ADD = 0, OP_SUB = 1, OP_NEG = 2, OP_MULP = 3, OP_ADDP = 4, OP_SUBP = 5, OP_SUBNEG = 6 };
 enum SampleMode { SAMPLE_UNIFORM = 0, SAMPLE_TERNARY = 1, SAMPLE_CBD = 2, SAMPLE_SEEDED = 3 };

@@ -1259,7 +1259,8 @@ static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* cons
 // only reorder independent work: the limbs are identical to the serial schedule.
 size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) { return bsgs_giant_workspace_bytes(T, R, l); }
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
-                       int l, const u64* const* keys_host, u64* inner, u64* out, u64* ws, size_t ws_bytes,
+                       int l, const u64* const* keys_host, const u64* giant_elts, u64* inner, u64* out, u64* ws,
+                       size_t ws_bytes,
                        void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm) {
     constexpr int VEC = FHS_INNER_VEC, W = 64 * VEC;
     const int R = B - 1;
@@ -1280,7 +1281,9 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             const int g = r + 1;
             const u64* ct = inner + (size_t)g * 2 * S;
             u64 elt = 1;
-            for (int s2 = 0; s2 < g * G; ++s2) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
+            if (giant_elts) elt = giant_elts[g];
+            else
+                for (int s2 = 0; s2 < g * G; ++s2) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
             items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)(r - rb(c))};
             uniq[r] = ct + S;
         }
@@ -1611,6 +1614,103 @@ hipError_t launch_encode(const DevTables& T, const double* vals, int count, size
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st) {
     hipLaunchKernelGGL(k_encode_reduce, dim3(eltwise_grid((size_t)count * l * T.N)), dim3(256), 0, st, T, coef, count,
                        out, l);
+    return hipGetLastError();
+}
+
+// ============================================================================ bootstrapping primitives
+// Constant products / sums (ckks_bootstrapper: pre-scale, EvalMod's Chebyshev coefficients and
+// constants, scale alignment).  A constant polynomial c has NTT image c in every slot, so both ops
+// are slot-wise: MULC multiplies every component by c_i (Shoup), ADDC adds c_i to component 0.
+__global__ void k_scalar(DevTables T, int op, const u64* __restrict__ a, u64* __restrict__ out, int ncomp, int l,
+                         ScalarConsts K) {
+    const int N = T.N;
+    const size_t total = (size_t)ncomp * l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t li = idx / N;
+        const int i = (int)(li % l), comp = (int)(li / l);
+        const u64 q = PK(T, i).q, x = a[idx];
+        u64 r;
+        if (op == SCALAR_MUL) r = shoup(x, K.v[i], K.vs[i], q);
+        else r = comp == 0 ? addmod(x, K.v[i], q) : x;
+        out[idx] = r;
+    }
+}
+hipError_t launch_scalar(const DevTables& T, int op, const u64* a, u64* out, int ncomp, int l, const ScalarConsts& K,
+                         hipStream_t st) {
+    if (l > kMaxScalarLimbs) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_scalar, dim3(eltwise_grid((size_t)ncomp * l * T.N)), dim3(256), 0, st, T, op, a, out, ncomp, l,
+                       K);
+    return hipGetLastError();
+}
+
+// ModRaise: the q0 limb of each component (coefficient form after k_ntt_inv) lifted to its
+// centred representative in (-q0/2, q0/2] and reduced into all L0 data limbs, then NTT.
+__global__ void k_mod_raise_lift(DevTables T, const u64* __restrict__ coef, u64* __restrict__ out, int ncomp) {
+    const int N = T.N, L = T.L0;
+    const u64 q0 = PK(T, 0).q, half = q0 >> 1;
+    const size_t total = (size_t)ncomp * L * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int n = (int)(idx % N);
+        const size_t li = idx / N;
+        const int i = (int)(li % L), comp = (int)(li / L);
+        const u64 x = coef[(size_t)comp * N + n], qi = PK(T, i).q;
+        u64 r;
+        if (x <= half) r = x % qi;                        // non-negative representative
+        else {                                            // x - q0 < 0
+            const u64 m = (q0 - x) % qi;
+            r = m ? qi - m : 0;
+        }
+        out[idx] = r;
+    }
+}
+// in: ncomp components of l limbs (NTT form), limb 0 used; out: ncomp x L0 limbs; scratch: ncomp x N
+hipError_t launch_mod_raise(const DevTables& T, const u64* in, int l, u64* out, u64* scratch, int ncomp,
+                            hipStream_t st) {
+    const size_t N = T.N;
+    hipError_t e = hipMemcpy2DAsync(scratch, 8 * N, in, 8 * N * l, 8 * N, ncomp, hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) return e;
+    e = launch_ntt_inv(T, scratch, 1, 1, ncomp, N, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_mod_raise_lift, dim3(eltwise_grid((size_t)ncomp * T.L0 * N)), dim3(256), 0, st, T, scratch, out,
+                       ncomp);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_ntt_fwd(T, out, T.L0, T.L0, ncomp, (size_t)T.L0 * N, st);
+}
+
+// Exact 128-bit integer coefficients (hi signed, lo unsigned: x = hi 2^64 + lo) -> every limb, NTT
+// (fhs_encode_precise: bootstrapping transform plaintexts).
+__global__ void k_reduce_i128(DevTables T, const int64_t* hi, const u64* lo, int count, u64* const* outs, int l) {
+    const int N = T.N;
+    const size_t total = (size_t)count * l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int n = (int)(idx % N);
+        const size_t rest = idx / N;
+        const int i = (int)(rest % l);
+        const size_t v = rest / l;
+        const PrimeK& P = PK(T, i);
+        const u64 q = P.q;
+        const int64_t h = hi[v * N + n];
+        u64 hm = (u64)(h < 0 ? -(h + 1) : h) % q;                 // |h| - [h < 0], no overflow
+        if (h < 0) hm = submod(0, (hm + 1) % q, q);
+        const u64 t64 = (0 - q) % q;                              // 2^64 mod q
+        const u64 r = addmod(mulmod(hm, t64, P), lo[v * N + n] % q, q);
+        outs[v][(size_t)i * N + n] = r;
+    }
+}
+hipError_t launch_encode_int128(const DevTables& T, const int64_t* hi, const u64* lo, int count, u64* const* outs_dev,
+                                int l, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reduce_i128, dim3(eltwise_grid((size_t)count * l * T.N)), dim3(256), 0, st, T, hi, lo, count,
+                       outs_dev, l);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    FHS_DISPATCH_LOGN(T.logN, {
+        hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T, outs_dev, l);
+    });
     return hipGetLastError();
 }
 

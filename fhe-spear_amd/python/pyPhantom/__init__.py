@@ -11,13 +11,15 @@ ImportError, and creating a context without an AMD GPU raises RuntimeError.
 Fork-only symbols the reference probes with try/except AttributeError are
 implemented: bsgs_multiply_accumulate (bg:459), encode_*_vector_batch (bg:382, 423),
 offload_plaintexts / upload_plaintexts / bsgs_from_cpu (bg:336-358, 449), ciphertext.chain_index /
-scale / coeff_modulus_size.  ckks_bootstrapper is not provided yet (run tf with --no-bootstrap).
+scale / coeff_modulus_size, and ckks_bootstrapper (bootstrap.py; the fork's is un-vendored, so its
+limbs are unpinned -- DESIGN.md §4).
 """
 from __future__ import annotations
 
 import ctypes as C
 import enum
 import os
+import sys
 import threading
 from pathlib import Path
 
@@ -115,6 +117,12 @@ _SIGS = {
     "fhs_upload_plaintexts": (C.c_int, [_vp, _u64p, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
     "fhs_bsgs_from_cpu": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u64p, C.c_int, C.c_int, C.c_int, C.c_double, _vp,
                                     C.POINTER(_vp)]),
+    "fhs_linear_transform": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.c_int, _u64p, _vp,
+                                       C.c_int, C.POINTER(_vp)]),
+    "fhs_multiply_const": (C.c_int, [_vp, _vp, C.c_double, C.c_double, C.POINTER(_vp)]),
+    "fhs_add_const": (C.c_int, [_vp, _vp, C.c_double, C.POINTER(_vp)]),
+    "fhs_mod_raise": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
+    "fhs_encode_precise": (C.c_int, [_vp, _dblp, C.c_size_t, C.c_size_t, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_host_alloc": (C.c_int, [_u64, C.POINTER(_vp)]),
     "fhs_host_free": (C.c_int, [_vp]),
     "fhs_random_plaintexts": (C.c_int, [_vp, _u64, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
@@ -517,13 +525,15 @@ class ckks_encoder:
         return _pt(ctx, _lib.fhs_encode, v.ctypes.data_as(_dblp), v.shape[0], float(scale), int(chain_index),
                    what="encode_complex_vector")
 
-    def _batch(self, ctx, mat, scale, chain_index, cplx):
+    def _batch(self, ctx, mat, scale, chain_index, cplx, precise=False):
+        if precise:
+            cplx = True
         m = np.ascontiguousarray(np.asarray(mat, dtype=np.complex128 if cplx else np.float64))
         if m.ndim != 2:
             raise ValueError("batch encode expects a 2-D array (count, values)")
         count, n = m.shape
         hs = (_vp * count)()
-        fn = _lib.fhs_encode_batch if cplx else _lib.fhs_encode_real_batch
+        fn = _lib.fhs_encode_precise if precise else (_lib.fhs_encode_batch if cplx else _lib.fhs_encode_real_batch)
         _check(fn(ctx._h, m.ctypes.data_as(_dblp), count, n, float(scale), int(chain_index), hs), "encode batch")
         return [plaintext(ctx, _vp(hs[i])) for i in range(count)]
 
@@ -531,9 +541,10 @@ class ckks_encoder:
         """bg:382: one plaintext per row of `mat` (D diagonals x slots)."""
         return self._batch(ctx, mat, scale, chain_index, False)
 
-    def encode_complex_vector_batch(self, ctx, mat, scale, chain_index=1):
-        """bg:423"""
-        return self._batch(ctx, mat, scale, chain_index, True)
+    def encode_complex_vector_batch(self, ctx, mat, scale, chain_index=1, precise=False):
+        """bg:423.  precise=True (extension): long-double canonical embedding with exact rounding
+        (fhs_encode_precise), for constant plaintexts such as the bootstrap transforms."""
+        return self._batch(ctx, mat, scale, chain_index, True, precise)
 
     def _decode(self, ctx, pt):
         out = np.empty((ctx.N // 2, 2), dtype=np.float64)
@@ -637,6 +648,34 @@ def bsgs_multiply_accumulate(ctx, ct_baby, pts, G, B, D, gk):
     bb = (_vp * G)(*[c._h for c in ct_baby[:G]])
     pp = (_vp * D)(*[p._h for p in pts[:D]])
     return _ct(ctx, _lib.fhs_bsgs_multiply_accumulate, bb, G, pp, D, B, gk._h, what="bsgs_multiply_accumulate")
+
+
+# ------------------------------------------------------------------ bootstrapping primitives
+def linear_transform(ctx, ct_baby, pts, G, giant_elts, gk, rescale=True):
+    """Generalised fused BSGS (CoeffToSlot / SlotToCoeff groups of ckks_bootstrapper):
+    [rescale]( sum_g galois_{giant_elts[g]}( sum_b baby[b] * pts[g G + b] ) ), giant_elts[0] = 1."""
+    G, B = int(G), len(giant_elts)
+    D = len(pts)
+    bb = (_vp * G)(*[c._h for c in ct_baby[:G]])
+    pp = (_vp * D)(*[p._h for p in pts])
+    e, ep = _u64_arr(giant_elts)
+    return _ct(ctx, _lib.fhs_linear_transform, bb, G, pp, D, B, ep, gk._h, 1 if rescale else 0,
+               what="linear_transform")
+
+
+def multiply_const(ctx, a, value, const_scale=1.0):
+    """a * round(value * const_scale) (exact integer constant); scale *= const_scale."""
+    return _ct(ctx, _lib.fhs_multiply_const, a._h, float(value), float(const_scale), what="multiply_const")
+
+
+def add_const(ctx, a, value):
+    """a + value (encoded as round(value * a.scale) in every slot)."""
+    return _ct(ctx, _lib.fhs_add_const, a._h, float(value), what="add_const")
+
+
+def mod_raise(ctx, a):
+    """Bootstrapping ModRaise: limb q0 lifted (centred) to all L0 data limbs, chain index 1."""
+    return _ct(ctx, _lib.fhs_mod_raise, a._h, what="mod_raise")
 
 
 class _HostPlaintexts(np.ndarray):
@@ -757,6 +796,16 @@ def ciphertext_from_device(ctx, src_ptr, ncomp, chain_index, scale):
     _check(_lib.fhs_ciphertext_from_device(ctx._h, _vp(int(src_ptr)), int(ncomp), int(chain_index), float(scale),
                                            C.byref(h)), "from_device")
     return ciphertext(ctx, h)
+
+
+from . import bootstrap as _bootstrap  # noqa: E402
+
+
+class ckks_bootstrapper(_bootstrap.Bootstrapper):
+    """bg:72-74, 112-116, 149-154: CKKS bootstrapping (pyPhantom/bootstrap.py) on the GPU ops."""
+
+
+ckks_bootstrapper._ph = sys.modules[__name__]
 
 
 def device_count():

@@ -166,6 +166,30 @@ fhs_status fhs_bsgs_from_cpu(fhs_context* ctx, const fhs_ciphertext* const* baby
 fhs_status fhs_host_alloc(uint64_t bytes, void** ptr);   /* pinned host memory */
 fhs_status fhs_host_free(void* ptr);
 
+/* ---- CKKS bootstrapping primitives (ckks_bootstrapper, bg:72-74, 110-116, 149-154; tf:243-262;
+ * the fork's C++ bootstrapper behind pb is un-vendored) ----
+ * Generalised fused BSGS linear transform (CoeffToSlot / SlotToCoeff groups):
+ *   out = [rescale]( sum_{g<B} galois_{giant_elts[g]}( sum_{b<G} baby[b] (.) pts[g G + b] ) )
+ * D = B * G plaintexts; giant_elts[0] must be 1 (identity group).  rescale = 0 keeps the product
+ * scale (baby scale x plaintext scale) and the level. */
+fhs_status fhs_linear_transform(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
+                                const fhs_plaintext* const* pts, int D, int B, const uint64_t* giant_elts,
+                                const fhs_galois_keys* gk, int rescale, fhs_ciphertext** out);
+/* encode_complex_vector_batch with an extended-precision (long double) canonical-embedding FFT on the
+ * host and exact 128-bit rounding: for constant plaintexts whose f64 encoding error (~2^-52 log n
+ * relative) matters -- the bootstrap's CoeffToSlot / SlotToCoeff diagonals.  |values x scale| < 2^126. */
+fhs_status fhs_encode_precise(fhs_context* ctx, const double* re_im, size_t count, size_t n, double scale,
+                              int chain_index, fhs_plaintext** out_array);
+/* out = a * c with the integer c = round(value * const_scale) (half away from zero, exact for any
+ * finite double); out scale = a.scale * const_scale */
+fhs_status fhs_multiply_const(fhs_context* ctx, const fhs_ciphertext* a, double value, double const_scale,
+                              fhs_ciphertext** out);
+/* out = a + round(value * a.scale) (added to component 0; scale unchanged) */
+fhs_status fhs_add_const(fhs_context* ctx, const fhs_ciphertext* a, double value, fhs_ciphertext** out);
+/* ModRaise: limb q0 of a (any level) lifted centred to all L0 data limbs; out at chain index 1,
+ * same scale (decrypts to m + q0 I) */
+fhs_status fhs_mod_raise(fhs_context* ctx, const fhs_ciphertext* a, fhs_ciphertext** out);
+
 /* ---- measurement hooks (bench.py) ---- */
 /* fill n plaintexts with i.i.d. uniform limbs mod q_i (SURVEY.md §8d throughput workload) */
 fhs_status fhs_random_plaintexts(fhs_context* ctx, uint64_t seed, int count, int chain_index, double scale,

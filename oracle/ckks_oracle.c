@@ -288,6 +288,41 @@ void ock_rescale_to_next(const ock_ctx* c, const uint64_t* in, uint64_t* out, in
     free(tmp); free(t2);
 }
 
+/* ------------------------------------------------------------------ bootstrapping primitives */
+/* ModRaise (ckks_bootstrapper.bootstrap, bg:149-154): limb q0 of each component, centred in
+ * (-q0/2, q0/2], re-embedded into all L0 data limbs (standard CKKS bootstrapping, Cheon et al. 2018). */
+void ock_mod_raise(const ock_ctx* c, const uint64_t* in, int l, int ncomp, uint64_t* out) {
+    uint64_t N = c->N; int L = c->L0; uint64_t q0 = c->q[0], half = q0 >> 1;
+    uint64_t* x = (uint64_t*)malloc(8 * N);
+    for (int k = 0; k < ncomp; k++) {
+        memcpy(x, in + (size_t)k * l * N, 8 * N);
+        ock_ntt_inv(c, x, 0);
+        for (int i = 0; i < L; i++) {
+            uint64_t q = c->q[i];
+            uint64_t* o = out + ((size_t)k * L + i) * N;
+            for (uint64_t j = 0; j < N; j++) {
+                if (x[j] <= half) o[j] = x[j] % q;
+                else { uint64_t m = (q0 - x[j]) % q; o[j] = m ? q - m : 0; }
+            }
+            ock_ntt_fwd(c, o, i);
+        }
+    }
+    free(x);
+}
+/* constant product (op 0: every component times k_i) or sum (op 1: k_i added to component 0);
+ * k_i = the integer constant mod q_i (a constant polynomial is constant in the NTT domain) */
+void ock_scalar(const ock_ctx* c, int op, const uint64_t* in, const uint64_t* k, uint64_t* out, int ncomp, int l) {
+    uint64_t N = c->N;
+    for (int comp = 0; comp < ncomp; comp++)
+        for (int i = 0; i < l; i++) {
+            uint64_t q = c->q[i];
+            const uint64_t* a = in + ((size_t)comp * l + i) * N;
+            uint64_t* o = out + ((size_t)comp * l + i) * N;
+            for (uint64_t j = 0; j < N; j++)
+                o[j] = op == 0 ? mulmod(a[j], k[i], q) : (comp == 0 ? addmod(a[j], k[i], q) : a[j]);
+        }
+}
+
 /* ------------------------------------------------------------------ hybrid key-switch */
 /* Exact centred base extension count: v = round(sum_u y_u / q_u) = the number of Q_S to subtract
  * from X = sum_u y_u (Q_S/q_u) so that X - v Q_S lies in (-Q_S/2, Q_S/2).  Fast path: 64-bit

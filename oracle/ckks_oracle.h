@@ -57,6 +57,10 @@ void ock_apply_galois_ntt(const ock_ctx* c, const uint64_t* in, uint64_t* out, u
 void ock_add(const ock_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* out, int ncomp, int l);
 void ock_sub(const ock_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* out, int ncomp, int l);
 void ock_negate(const ock_ctx* c, const uint64_t* a, uint64_t* out, int ncomp, int l);
+/* bootstrapping primitives (ckks_bootstrapper, bg:149-154): ModRaise of limb q0 to all L0 limbs;
+ * constant product (op 0) / sum into component 0 (op 1) with per-limb residues k[i] */
+void ock_mod_raise(const ock_ctx* c, const uint64_t* in, int l, int ncomp, uint64_t* out);
+void ock_scalar(const ock_ctx* c, int op, const uint64_t* in, const uint64_t* k, uint64_t* out, int ncomp, int l);
 void ock_multiply_plain(const ock_ctx* c, const uint64_t* ct, const uint64_t* pt, uint64_t* out, int ncomp, int l);
 void ock_add_plain(const ock_ctx* c, const uint64_t* ct, const uint64_t* pt, uint64_t* out, int ncomp, int l);
 void ock_multiply(const ock_ctx* c, const uint64_t* a, const uint64_t* b, uint64_t* out3, int l);

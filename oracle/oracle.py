@@ -63,6 +63,8 @@ def lib():
         L.ock_rotate.argtypes = [vp, _u64p, _u64p, C.c_uint64, C.c_int, _u64p]
         L.ock_relinearize.argtypes = [vp, _u64p, _u64p, C.c_int, _u64p]
         L.ock_rotate_hoisted.argtypes = [vp, _u64p, C.POINTER(_u64p), _u64p, C.c_int, C.c_int, C.POINTER(_u64p)]
+        L.ock_mod_raise.argtypes = [vp, _u64p, C.c_int, C.c_int, _u64p]
+        L.ock_scalar.argtypes = [vp, C.c_int, _u64p, _u64p, _u64p, C.c_int, C.c_int]
         L.ock_centered_count_test.argtypes = [_u64p, _u64p, C.c_int]
         L.ock_centered_count_test.restype = C.c_int
         L.ock_seeded_uniform.argtypes = [C.c_uint64, C.c_int, C.c_uint64, C.c_uint64]
@@ -193,6 +195,23 @@ class Oracle:
         ct = np.ascontiguousarray(ct, dtype=np.uint64)
         out = np.empty((ncomp, l - 1, N), dtype=np.uint64)
         lib().ock_rescale_to_next(self._h, _p(ct), _p(out), ncomp, l)
+        return out
+
+    def mod_raise(self, ct):
+        """ckks_bootstrapper ModRaise: limb q0 lifted centred to all L0 limbs (ock_mod_raise)."""
+        ncomp, l, N = ct.shape
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        out = np.empty((ncomp, self.L0, N), dtype=np.uint64)
+        lib().ock_mod_raise(self._h, _p(ct), l, ncomp, _p(out))
+        return out
+
+    def scalar(self, ct, k: int, add: bool):
+        """ct * k (add=False) or ct + k into component 0 (add=True) for the integer k."""
+        ncomp, l, N = ct.shape
+        ct = np.ascontiguousarray(ct, dtype=np.uint64)
+        res = np.array([int(k) % int(self.primes[i]) for i in range(l)], dtype=np.uint64)
+        out = np.empty_like(ct)
+        lib().ock_scalar(self._h, 1 if add else 0, _p(ct), _p(res), _p(out), ncomp, l)
         return out
 
     def keyswitch(self, a, key):

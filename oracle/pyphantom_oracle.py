@@ -79,6 +79,7 @@ class context:
         if L0 % p.special != 0:
             raise ValueError("L0 % special_modulus_size != 0 is not supported (README.md:59)")
         self.o = Oracle(p.N, p.coeff, p.special)
+        self.primes = list(p.coeff)
         self.params = p
         self.N = p.N
         self.L0 = L0
@@ -154,8 +155,8 @@ class secret_key:
     def gen_relinkey(self, ctx):
         return relin_key(ctx.o.gen_relin_key(self.seed, self.s))
 
-    def create_galois_keys(self, ctx):
-        elts = ctx.params.galois_elts
+    def create_galois_keys(self, ctx, elts=None):
+        elts = elts or ctx.params.galois_elts
         if elts is None:
             N = ctx.N
             steps = []
@@ -190,6 +191,9 @@ class ckks_encoder:
         _count("encode")
         return plaintext(ctx.o.encode(np.asarray(values, dtype=np.complex128), scale, ctx.limbs(chain_index)),
                          chain_index, scale)
+
+    def encode_complex_vector_batch(self, ctx, mat, scale, chain_index=1, precise=False):
+        return [self.encode_complex_vector(ctx, row, scale, chain_index) for row in np.asarray(mat)]
 
     def decode_double_vector(self, ctx, pt):
         return list(ctx.o.decode(pt.data, pt.scale()).real)
@@ -268,3 +272,49 @@ def rotate(ctx, ct, step, gk):
     if elt not in gk.keys:
         raise ValueError(f"galois key for step {step} (elt {elt}) not present")
     return ciphertext(ctx.o.rotate_elt(ct.data, gk.keys[elt], elt), ct.chain_index(), ct.scale())
+
+
+def apply_galois(ctx, ct, elt, gk):
+    _count("rotate")
+    return ciphertext(ctx.o.rotate_elt(ct.data, gk.keys[int(elt)], int(elt)), ct.chain_index(), ct.scale())
+
+
+def hoisting(ctx, ct, gk, steps):
+    return [rotate(ctx, ct, s, gk) for s in steps]
+
+
+# ---- bootstrapping primitives (ckks_bootstrapper; restated in ckks_oracle.c / below) ----
+def _round_half_away(p):
+    """std::round of the double p, exactly (the library's constant rule, fhs_host.hip scalar_consts)."""
+    from fractions import Fraction
+    import math
+    f = Fraction(float(p))
+    return math.floor(f + Fraction(1, 2)) if f >= 0 else -math.floor(-f + Fraction(1, 2))
+
+
+def multiply_const(ctx, ct, value, const_scale=1.0):
+    k = _round_half_away(float(value) * float(const_scale))
+    return ciphertext(ctx.o.scalar(ct.data, k, add=False), ct.chain_index(), ct.scale() * float(const_scale))
+
+
+def add_const(ctx, ct, value):
+    k = _round_half_away(float(value) * ct.scale())
+    return ciphertext(ctx.o.scalar(ct.data, k, add=True), ct.chain_index(), ct.scale())
+
+
+def mod_raise(ctx, ct):
+    return ciphertext(ctx.o.mod_raise(ct.data), 1, ct.scale())
+
+
+def linear_transform(ctx, babies, pts, G, giant_elts, gk, rescale=True):
+    """Loop form of the fused linear transform: sum_g galois_g(sum_b baby[b] * pt[gG+b]), then rescale."""
+    acc = None
+    for g, elt in enumerate(giant_elts):
+        inner = None
+        for b in range(G):
+            t = multiply_plain(ctx, babies[b], pts[g * G + b])
+            inner = t if inner is None else ciphertext(ctx.o.add(inner.data, t.data), t.chain_index(), t.scale())
+        if int(elt) != 1:
+            inner = apply_galois(ctx, inner, elt, gk)
+        acc = inner if acc is None else ciphertext(ctx.o.add(acc.data, inner.data), acc.chain_index(), acc.scale())
+    return rescale_to_next(ctx, acc) if rescale else acc
