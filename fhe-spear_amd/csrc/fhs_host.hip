@@ -11,9 +11,12 @@
 //    not a rotation at the same level.  The reference's baby-step loop (bg:215-220) issues G-1
 //    independent rotations back to back; batching turns 39 workgroups per rotation into
 //    39 (G-1) workgroups per launch.  Each rotation is computed exactly as it would be alone.
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <csignal>
 #include <atomic>
 #include <cmath>
 #include <complex>
@@ -42,6 +45,20 @@ static thread_local std::string g_err;
 static fhs_status fail(fhs_status code, const std::string& msg) {
     g_err = msg;
     return code;
+}
+// FHESPEAR_SEGV_TRACE=1: print a native backtrace on SIGSEGV (diagnostics for faults outside
+// Python frames, e.g. during process teardown, where faulthandler is no longer installed)
+static void segv_trace(int sig) {
+    void* fr[64];
+    const int n = backtrace(fr, 64);
+    static const char hdr[] = "[fhespear] native backtrace:\n";
+    (void)!write(2, hdr, sizeof(hdr) - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+__attribute__((constructor)) static void segv_trace_install() {
+    if (getenv("FHESPEAR_SEGV_TRACE")) signal(SIGSEGV, segv_trace);
 }
 static fhs_status hip_fail(hipError_t e, const char* where) {
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
@@ -242,6 +259,12 @@ struct fhs_context {
     // after warm-up is a free-list pop.  Trimmed on out-of-memory and at context destruction.
     std::unordered_map<size_t, std::vector<void*>> free_blocks;
     size_t cached_bytes = 0;
+    // bounded: a chain walks down the levels, so every level brings new sizes and the sizes of the
+    // levels behind it go cold.  Over the cap, whole sizes are evicted least-recently-used first
+    // (a 13-block d=2048 chain otherwise parked 135 GB here).  FHESPEAR_CACHE_BYTES overrides.
+    size_t cache_cap = 0;
+    uint64_t cache_tick = 0;
+    std::unordered_map<size_t, uint64_t> size_tick;   // last dalloc/dfree of each size
     // kernel timer (bench): events around the timed kernel launches
     // per-kernel event timer (fhs_kernel_timer): bitmask of fhs::KernelId, completed pairs per id
     uint32_t timer_mask = 0;
@@ -306,6 +329,9 @@ static size_t key_words_full(const fhs_context* c) { return (size_t)c->dnum * 2 
 
 static void trim_cache(fhs_context* c) {
     if (c->free_blocks.empty()) return;
+    if (getenv("FHESPEAR_TRACE_LIFETIME"))
+        fprintf(stderr, "[fhespear] trim: %zu cached bytes in %zu sizes, %llu live\n", c->cached_bytes,
+                c->free_blocks.size(), (unsigned long long)c->bytes_live.load());
     if (c->st_aux) hipStreamSynchronize(c->st_aux);
     for (auto& kv : c->free_blocks)
         for (void* p : kv.second) (void)hipFreeAsync(p, c->st);
@@ -313,8 +339,28 @@ static void trim_cache(fhs_context* c) {
     c->free_blocks.clear();
     c->cached_bytes = 0;
 }
+static void evict_cold(fhs_context* c, size_t keep) {
+    while (c->cached_bytes > c->cache_cap) {
+        size_t victim = 0;
+        uint64_t oldest = ~0ull;
+        for (auto& kv : c->free_blocks)
+            if (kv.first != keep && !kv.second.empty() && c->size_tick[kv.first] < oldest) {
+                oldest = c->size_tick[kv.first];
+                victim = kv.first;
+            }
+        if (!victim) victim = keep;   // only the size in hand is cached: shed its blocks
+        auto& v = c->free_blocks[victim];
+        while (!v.empty() && c->cached_bytes > c->cache_cap) {
+            (void)hipFreeAsync(v.back(), c->st);
+            v.pop_back();
+            c->cached_bytes -= victim;
+        }
+        if (v.empty()) c->free_blocks.erase(victim);
+    }
+}
 static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
     bytes = bytes ? bytes : 8;
+    c->size_tick[bytes] = ++c->cache_tick;
     auto it = c->free_blocks.find(bytes);
     if (it != c->free_blocks.end() && !it->second.empty()) {
         *p = static_cast<uint64_t*>(it->second.back());
@@ -342,6 +388,8 @@ static void dfree(fhs_context* c, void* p, size_t bytes) {
     c->free_blocks[bytes].push_back(p);
     c->cached_bytes += bytes;
     c->bytes_live -= bytes;
+    c->size_tick[bytes] = ++c->cache_tick;
+    if (c->cached_bytes > c->cache_cap) evict_cold(c, bytes);
 }
 
 static hipError_t scratch(fhs_context* c, int slot, size_t bytes, uint64_t** p) {
@@ -472,6 +520,7 @@ struct Guard {
 extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int nprimes, int special,
                                          const uint64_t* galois_elts, int n_elts, int device, fhs_context** out) {
     if (!primes || !out) return fail(FHS_ERR_INVALID, "context_create: null argument");
+    segv_trace_install();
     if (N < 256 || N > 32768 || (N & (N - 1)))
         return fail(FHS_ERR_INVALID, "context_create: poly_modulus_degree must be a power of two in [256, 32768]");
     if (special < 1 || special >= nprimes) return fail(FHS_ERR_INVALID, "context_create: bad special modulus size");
@@ -509,6 +558,10 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
             uint64_t thr = ~0ull;
             (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
         }
+        size_t free_b = 0, total_b = 0;
+        (void)hipMemGetInfo(&free_b, &total_b);
+        c->cache_cap = total_b / 4;
+        if (const char* e = getenv("FHESPEAR_CACHE_BYTES")) c->cache_cap = strtoull(e, nullptr, 10);
     }
     if (galois_elts && n_elts > 0) {
         c->elts.assign(galois_elts, galois_elts + n_elts);
@@ -714,6 +767,10 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
 }
 
 static void ctx_free(fhs_context* c) {
+    const bool trace = getenv("FHESPEAR_TRACE_LIFETIME") != nullptr;
+    if (trace)
+        fprintf(stderr, "[fhespear] context %p: freeing (%zu cached bytes, %llu live)\n", (void*)c, c->cached_bytes,
+                (unsigned long long)c->bytes_live.load());
     {
         Guard g(c);
         flush(c);
@@ -727,12 +784,18 @@ static void ctx_free(fhs_context* c) {
         for (auto& kv : c->free_blocks)
             for (void* p : kv.second) hipFreeAsync(p, c->st);
         hipStreamSynchronize(c->st);
+        // hand the stream-ordered pool's freed blocks back while the stream that freed them still
+        // exists: blocks left in the default pool tied to a destroyed stream crashed the HIP
+        // runtime's own exit handler after multi-GB chains (tools/debug/exit_crash.py)
+        hipMemPool_t pool = nullptr;
+        if (hipDeviceGetDefaultMemPool(&pool, c->device) == hipSuccess && pool) hipMemPoolTrimTo(pool, 0);
         if (c->ring) hipHostFree(c->ring);
         for (auto& v : c->timer_pairs)
             for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
         hipStreamDestroy(c->st);
     }
     delete c;
+    if (trace) fprintf(stderr, "[fhespear] context %p: freed\n", (void*)c);
 }
 static void ctx_release(fhs_context* c) {
     if (c->refs.fetch_sub(1) == 1) ctx_free(c);
@@ -1817,6 +1880,201 @@ extern "C" fhs_status fhs_mod_raise(fhs_context* c, const fhs_ciphertext* a, fhs
     HIPCHK(fhs::launch_mod_raise(c->T, a->d, a->l, r->d, scr, 2, c->st), "mod_raise");
     *out = r;
     return FHS_OK;
+}
+
+// ---- EvalMod orchestration in C++ (ckks_bootstrapper._evalmod, pyPhantom/bootstrap.py).  The same
+// op sequence as the Python restatement (which the oracle runs): ~300 small ops per EvalMod, whose
+// per-call Python overhead dominated the bootstrap.  Every double expression mirrors the Python one
+// (same IEEE operations in the same order), so the limbs are identical.
+namespace {
+struct Ct {   // owning ciphertext handle
+    fhs_ciphertext* p = nullptr;
+    Ct() = default;
+    explicit Ct(fhs_ciphertext* x) : p(x) {}
+    Ct(const Ct&) = delete;
+    Ct& operator=(const Ct&) = delete;
+    Ct(Ct&& o) noexcept : p(o.p) { o.p = nullptr; }
+    Ct& operator=(Ct&& o) noexcept {
+        if (this != &o) {
+            reset();
+            p = o.p;
+            o.p = nullptr;
+        }
+        return *this;
+    }
+    ~Ct() { reset(); }
+    void reset() {
+        if (p) fhs_ciphertext_destroy(p);
+        p = nullptr;
+    }
+    fhs_ciphertext* release() {
+        fhs_ciphertext* x = p;
+        p = nullptr;
+        return x;
+    }
+};
+struct EmErr {
+    fhs_status s;
+};
+inline void em_try(fhs_status s) {
+    if (s != FHS_OK) throw EmErr{s};
+}
+
+struct EvalMod {
+    fhs_context* c;
+    const fhs_relin_key* rk;
+    std::map<int, Ct> own;   // T_k computed here (T_1 is borrowed)
+    std::map<int, const fhs_ciphertext*> T;
+
+    double q_drop(int ci) const { return (double)c->q[c->L0 - ci]; }   // Bootstrapper._q_drop
+    Ct mod_switch(const fhs_ciphertext* a, int ci) {
+        fhs_ciphertext* r;
+        em_try(fhs_mod_switch_to(c, a, ci, &r));
+        return Ct(r);
+    }
+    Ct mul(const fhs_ciphertext* a, const fhs_ciphertext* b) {   // Bootstrapper._mul
+        const int ci = std::max(a->ci, b->ci);
+        Ct ta, tb;
+        if (a->ci < ci) {
+            ta = mod_switch(a, ci);
+            a = ta.p;
+        }
+        if (b->ci < ci) {
+            tb = mod_switch(b, ci);
+            b = tb.p;
+        }
+        fhs_ciphertext *m, *r, *s;
+        em_try(fhs_multiply(c, a, b, &m));
+        Ct M(m);
+        em_try(fhs_relinearize(c, M.p, rk, &r));
+        Ct R(r);
+        em_try(fhs_rescale_to_next(c, R.p, &s));
+        return Ct(s);
+    }
+    Ct add(const fhs_ciphertext* a, const fhs_ciphertext* b) {
+        fhs_ciphertext* r;
+        em_try(fhs_add(c, a, b, &r));
+        return Ct(r);
+    }
+    Ct sub(const fhs_ciphertext* a, const fhs_ciphertext* b) {
+        fhs_ciphertext* r;
+        em_try(fhs_sub(c, a, b, 0, &r));
+        return Ct(r);
+    }
+    Ct add_const(const fhs_ciphertext* a, double v) {
+        fhs_ciphertext* r;
+        em_try(fhs_add_const(c, a, v, &r));
+        return Ct(r);
+    }
+    // value * a landing exactly at (ci, scale): Bootstrapper._scalar
+    Ct scalar(const fhs_ciphertext* a, double value, int ci, double scale) {
+        if (a->ci > ci - 1) throw EmErr{fail(FHS_ERR_LEVEL, "evalmod: scalar product target level too low")};
+        Ct t;
+        if (a->ci < ci - 1) {
+            t = mod_switch(a, ci - 1);
+            a = t.p;
+        }
+        fhs_ciphertext *m, *r;
+        em_try(fhs_multiply_const(c, a, value, scale * q_drop(ci - 1) / a->scale, &m));
+        Ct M(m);
+        em_try(fhs_rescale_to_next(c, M.p, &r));
+        r->scale = scale;
+        return Ct(r);
+    }
+    // Bootstrapper._align: borrowed when already there, else a scalar product by 1.0
+    const fhs_ciphertext* align(const fhs_ciphertext* a, int ci, double scale, Ct& hold) {
+        if (a->ci == ci && std::fabs(a->scale - scale) <= 1e-9 * scale) return a;
+        hold = scalar(a, 1.0, ci, scale);
+        return hold.p;
+    }
+    static int bitlen(int k) {
+        int b = 0;
+        while (k >> b) ++b;
+        return b;
+    }
+    const fhs_ciphertext* get(int k) {   // Bootstrapper._cheb_basis.get
+        auto it = T.find(k);
+        if (it != T.end()) return it->second;
+        const int a = (k & (k - 1)) ? 1 << (bitlen(k) - 1) : k / 2, b = k - a;
+        Ct out;
+        if (a == b) {
+            const fhs_ciphertext* ta = get(a);
+            Ct P = mul(ta, ta);
+            Ct P2 = add(P.p, P.p);
+            out = add_const(P2.p, -1.0);
+        } else {
+            const fhs_ciphertext* ta = get(a);
+            const fhs_ciphertext* tb = get(b);
+            Ct P = mul(ta, tb);
+            Ct P2 = add(P.p, P.p);
+            Ct hold;
+            const fhs_ciphertext* d = align(get(a - b), P2.p->ci, P2.p->scale, hold);
+            out = sub(P2.p, d);
+        }
+        const fhs_ciphertext* r = out.p;
+        own[k] = std::move(out);
+        T[k] = r;
+        return r;
+    }
+    // Bootstrapper._cheb_eval: sum_k c_k T_k landing exactly at (ci, scale)
+    Ct cheb(std::vector<double> cf, int ci, double scale) {
+        int deg = (int)cf.size() - 1;
+        while (deg > 0 && cf[deg] == 0.0) --deg;
+        if (deg < 8) {
+            std::vector<int> ks;
+            for (int k = 1; k <= deg; ++k)
+                if (cf[k] != 0.0) ks.push_back(k);
+            if (ks.empty()) ks.push_back(1);
+            Ct acc;
+            for (int k : ks) {
+                Ct t = scalar(get(k), k <= deg ? cf[k] : 0.0, ci, scale);
+                acc = acc.p ? add(acc.p, t.p) : std::move(t);
+            }
+            return cf[0] != 0.0 ? add_const(acc.p, cf[0]) : std::move(acc);
+        }
+        const int m = 1 << (bitlen(deg) - 1);
+        // cheb_split: T_{m+j} = 2 T_m T_j - T_{m-j} (j >= 1), T_m = T_m T_0
+        std::vector<double> c2(cf.begin(), cf.begin() + deg + 1);
+        c2.resize(2 * m, 0.0);
+        std::vector<double> H(m), L(c2.begin(), c2.begin() + m);
+        H[0] = c2[m];
+        for (int j = 1; j < m; ++j) H[j] = 2.0 * c2[m + j];
+        for (int j = 1; j < m; ++j) L[m - j] -= c2[m + j];
+        const fhs_ciphertext* Tm = get(m);
+        Ct h = cheb(H, ci - 1, scale * q_drop(ci - 1) / Tm->scale);
+        Ct P = mul(h.p, Tm);
+        P.p->scale = scale;
+        Ct Lc = cheb(L, ci, scale);
+        return add(P.p, Lc.p);
+    }
+};
+}  // namespace
+
+extern "C" fhs_status fhs_bootstrap_evalmod(fhs_context* c, const fhs_ciphertext* y, const fhs_relin_key* rk,
+                                            const double* cc, const double* cs, int ncoef, int r, int cheb_depth,
+                                            fhs_ciphertext** out) {
+    ENTER(c);
+    if (!y || !rk || !cc || !cs || !out || ncoef < 1 || r < 1) return fail(FHS_ERR_INVALID, "evalmod: bad argument");
+    try {
+        EvalMod e{c, rk, {}, {}};
+        e.T[1] = y;
+        for (int k : {2, 3, 4, 5, 6, 7, 8, 16, 32}) e.get(k);
+        const int ci = y->ci + cheb_depth;
+        Ct cv = e.cheb(std::vector<double>(cc, cc + ncoef), ci, y->scale);
+        Ct sv = e.cheb(std::vector<double>(cs, cs + ncoef), ci, y->scale);
+        for (int step = 0; step < r; ++step) {   // (c, s) -> ((c + s)(c - s), 2 c s)
+            Ct P = e.mul(cv.p, sv.p);
+            if (step < r - 1) {
+                Ct a = e.add(cv.p, sv.p), b = e.sub(cv.p, sv.p);
+                cv = e.mul(a.p, b.p);
+            }
+            sv = e.add(P.p, P.p);
+        }
+        *out = sv.release();
+        return FHS_OK;
+    } catch (const EmErr& err) {
+        return err.s;
+    }
 }
 
 extern "C" fhs_status fhs_host_alloc(uint64_t bytes, void** ptr) {

@@ -122,6 +122,7 @@ _SIGS = {
     "fhs_multiply_const": (C.c_int, [_vp, _vp, C.c_double, C.c_double, C.POINTER(_vp)]),
     "fhs_add_const": (C.c_int, [_vp, _vp, C.c_double, C.POINTER(_vp)]),
     "fhs_mod_raise": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
+    "fhs_bootstrap_evalmod": (C.c_int, [_vp, _vp, _vp, _dblp, _dblp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     "fhs_encode_precise": (C.c_int, [_vp, _dblp, C.c_size_t, C.c_size_t, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_host_alloc": (C.c_int, [_u64, C.POINTER(_vp)]),
     "fhs_host_free": (C.c_int, [_vp]),
@@ -676,6 +677,16 @@ def add_const(ctx, a, value):
 def mod_raise(ctx, a):
     """Bootstrapping ModRaise: limb q0 lifted (centred) to all L0 data limbs, chain index 1."""
     return _ct(ctx, _lib.fhs_mod_raise, a._h, what="mod_raise")
+
+
+def bootstrap_evalmod(ctx, y, rk, cc, cs, r, cheb_depth):
+    """ckks_bootstrapper EvalMod in one library call (bootstrap.py Bootstrapper._evalmod's op sequence)."""
+    a = np.ascontiguousarray(cc, dtype=np.float64)
+    b = np.ascontiguousarray(cs, dtype=np.float64)
+    if a.shape != b.shape:
+        raise ValueError("bootstrap_evalmod: coefficient arrays differ in length")
+    return _ct(ctx, _lib.fhs_bootstrap_evalmod, y._h, rk._h, a.ctypes.data_as(_dblp), b.ctypes.data_as(_dblp),
+               len(a), int(r), int(cheb_depth), what="bootstrap_evalmod")
 
 
 class _HostPlaintexts(np.ndarray):

@@ -450,9 +450,11 @@ class Bootstrapper:
         unit circle amplifies an error by 2 per step, where the cosine double angle 2c^2 - 1
         amplifies it by up to 4: 2^r instead of 4^r on everything before (measured 2^21 total)."""
         ph, ctx = self._ph, self.ctx
+        cc, cs = self.cheb
+        if hasattr(ph, "bootstrap_evalmod"):      # the same op sequence, orchestrated in the library
+            return ph.bootstrap_evalmod(ctx, y, self.rlk, cc, cs, self.r, CHEB_DEPTH)
         T = self._cheb_basis(y)
         ci = y.chain_index() + CHEB_DEPTH
-        cc, cs = self.cheb
         c = self._cheb_eval(list(cc), T, ci, y.scale())
         s = self._cheb_eval(list(cs), T, ci, y.scale())
         for step in range(self.r):

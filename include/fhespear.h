@@ -189,6 +189,12 @@ fhs_status fhs_add_const(fhs_context* ctx, const fhs_ciphertext* a, double value
 /* ModRaise: limb q0 of a (any level) lifted centred to all L0 data limbs; out at chain index 1,
  * same scale (decrypts to m + q0 I) */
 fhs_status fhs_mod_raise(fhs_context* ctx, const fhs_ciphertext* a, fhs_ciphertext** out);
+/* ckks_bootstrapper EvalMod (pyPhantom/bootstrap.py Bootstrapper._evalmod, the same op sequence):
+ * cos / sin Chebyshev series cc, cs (ncoef coefficients each, scale-exact split, landing at chain
+ * index y + cheb_depth at y's scale) on one basis, then r complex squarings; out = sin(2 pi K y) */
+fhs_status fhs_bootstrap_evalmod(fhs_context* ctx, const fhs_ciphertext* y, const fhs_relin_key* rk,
+                                 const double* cc, const double* cs, int ncoef, int r, int cheb_depth,
+                                 fhs_ciphertext** out);
 
 /* ---- measurement hooks (bench.py) ---- */
 /* fill n plaintexts with i.i.d. uniform limbs mod q_i (SURVEY.md §8d throughput workload) */

@@ -331,3 +331,26 @@ def test_bootstrap_precision_cfg_rings(ph, N):
           f"out chain_index {res.chain_index()}")
     assert res.chain_index() == 1 + bt.bootstrap_depth(N, budget)
     assert err < (1e-4 if N == 16384 else 5e-4)
+
+
+@pytest.mark.gpu
+def test_fully_encrypted_chain_with_bootstrap(ph):
+    """tf:233-298 at the cfg2 ring (N = 16384, L0 = 36, P = 3, budget [2, 2]) with small D/F: 14
+    calibrated FFN blocks, so the chain runs out of levels after block 10 and bootstraps once
+    (tf:243-262); the reference's pass criterion is corr > 0.999 (tf:298)."""
+    import sys
+    from pathlib import Path
+    tools = str(Path(__file__).resolve().parents[1] / "tools")
+    if tools not in sys.path:
+        sys.path.insert(0, tools)
+    import ffn_block as fb
+    N, L0, P, D, F, blocks = 16384, 36, 3, 64, 128, 14
+    rng = np.random.default_rng(42)
+    ck = fb.Ckks(ph, N, L0, P, D, seed=3, bootstrap=True)
+    x_cal, Wk, Wv = fb.calibrated_weights(rng, D, F, blocks)
+    recs = fb.run_chain(ck, x_cal, Wk, Wv, D, F, True)
+    assert len(recs) == blocks
+    assert sum(1 for r in recs if r["bootstrap_seconds"]) == 1
+    assert recs[11]["bootstrap_seconds"] is not None
+    assert all(r["corr"] > 0.999999 for r in recs)
+    assert recs[-1]["max_err"] < 1e-3 * recs[-1]["mag"]
