@@ -37,6 +37,11 @@ CONFIGS = {
     "small": dict(N=4096, L0=6, P=3, D=256, workload="BSGS matvec d=256 N=4096 L0=6 P=3 (smoke size)"),
     # BASELINE configs[4] ring (tf --N 32768 --L0 36 --P 3): one BSGS matvec of that 24-block run
     "cfg5mv": dict(N=32768, L0=36, P=3, D=2048, workload="BSGS matvec d=2048 N=32768 L0=36 P=3 (cfg5 ring)"),
+    # BASELINE configs[2]/[3]: one client-aided RWKV-7 block (8 BSGS projections, bg:756-899);
+    # N GPUs = the block's projections dealt over ranks (strong scaling, sec/block)
+    "cfg3": dict(N=16384, L0=36, P=3, D=2048, F=8192,
+                 workload="client-aided RWKV-7 block d=2048 F=8192 N=16384 L0=36 P=3: 8 BSGS projections, "
+                          "pre-encoded diagonals resident in HBM"),
 }
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 BFLY_PEAK_GOPS = 1466.6        # measured lazy NTT butterflies/s, registers only (tools/microbench/bfly.hip)
@@ -109,6 +114,8 @@ def main():
 
     import pyPhantom as ph
 
+    if args.config == "cfg3":
+        return bench_block(args, ph, dist, rank, world, local)
     cfg = CONFIGS[args.config]
     N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
@@ -143,6 +150,9 @@ def main():
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
         if dist is not None:     # cfg4: output ciphertexts to rank 0 over RCCL (xGMI)
+            # the previous step's gather (torch/RCCL stream) must have read the buffer before the
+            # library's stream overwrites it; it finished long before this step's kernels did
+            torch.cuda.current_stream().synchronize()
             ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
             fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
         return y
@@ -262,6 +272,74 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args)
+        print(json.dumps(res))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def bench_block(args, ph, dist, rank, world, local):
+    """cfg3 / cfg4: one step = the server side of one client-aided RWKV-7 block (tools/rwkv_block.py,
+    bg:756-899): 8 BSGS projections in 4 dependent stages, each input encrypted and each output
+    decrypted by rank 0 (the client), diagonals pre-encoded and resident.  N ranks deal each stage's
+    projections round-robin (RCCL broadcast of the input ciphertexts, gather of the outputs)."""
+    sys.path.insert(0, str(REPO / "tools"))
+    import rwkv_block as rb
+    cfg = CONFIGS["cfg3"]
+    D, F = cfg["D"], cfg["F"]
+    H = D // 64
+    rng = np.random.default_rng(5)
+    block = rb.BlockWeights(rng, 1, D, F, H)
+    srv = rb.Server(ph, cfg["N"], cfg["L0"], cfg["P"], D, device=local)
+    run = rb.BlockRunner(srv, block, True, dist, rank, world)
+    x = rng.standard_normal(D)
+    st = (x, np.zeros(D), np.zeros(D), np.zeros((H, 64, 64)), rng.standard_normal(D))
+
+    def barrier():
+        srv.ctx.synchronize()
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        out = rb.client_aided_block(run, *st)
+    barrier()
+    t0 = time.perf_counter()
+    stage = {}
+    for _ in range(args.steps):
+        out = rb.client_aided_block(run, *st)
+        for k, v in out[5].items():
+            stage[k] = stage.get(k, 0.0) + v
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank == 0:
+        ref = rb.plaintext_block(block, *st)
+        err = float(np.max(np.abs(out[0] - ref[0])))
+        if not err < 1e-6 * max(1.0, float(np.max(np.abs(ref[0])))):
+            raise AssertionError(f"bench cfg3: decrypted block output off the plaintext block by {err:.3e}")
+        sec = elapsed / args.steps
+        l = cfg["L0"]
+        mv = matvec_bytes(dict(cfg), l)
+        res = {
+            "metric": "BSGS matvecs/sec at d=2048,N=16384,L0=36; sec/RWKV-block at 1/2/4/8 GPU",
+            "value": round(sec, 5), "unit": "s/RWKV-block", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1e3 * sec, 3), "higher_is_better": False,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (random-init RWKV-7 block weights, random token state); max |x - plaintext block| "
+                    f"= {err:.2e}",
+            "config": {"workload": cfg["workload"], "N": cfg["N"], "L0": l, "P": cfg["P"], "d": D, "d_ffn": F,
+                       "projections": 8, "parallelism": f"stage-dealt projections x{world}"
+                       + (" + RCCL broadcast/gather" if world > 1 else "")},
+            "stages_ms": {k: round(1e3 * v / args.steps, 2) for k, v in stage.items()},
+            "matvec_roofline": {"bound": "hbm", "bytes_per_block": 8 * mv, "achieved": round(8 * mv / sec / 1e9, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(8 * mv / sec / 1e9 / HBM_PEAK_GBS, 4)},
+        }
         print(json.dumps(res))
     if dist is not None:
         dist.barrier()

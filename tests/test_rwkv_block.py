@@ -1,0 +1,101 @@
+"""Client-aided RWKV-7 block (bg:756-899) restated in tools/rwkv_block.py: BASELINE configs[2]/[3].
+
+CPU: the projection chunking (complex-packed FFN key pairs, conjugate-trick FFN value pairs,
+bg:545-659) checked against plaintext_block (bg:902-980) through an exact stand-in server.
+GPU: the same block through pyPhantom (8 BSGS matvecs) against plaintext_block."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "tools"))
+sys.path.insert(0, str(REPO / "fhe-spear_amd" / "python"))
+
+import rwkv_block as rb  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def ph(require_gpu):
+    import pyPhantom
+    return pyPhantom
+
+
+class _Ctx:
+    def synchronize(self):
+        pass
+
+
+class ExactServer:
+    """Server's interface over plain complex vectors: encryption is the identity, a plaintext
+    'encoding' is the matrix itself, so any chunking / packing mistake shows as a real error."""
+
+    def __init__(self, D, slots):
+        self.D, self.slots, self.level, self.ctx, self.device = D, slots, 1, _Ctx(), 0
+
+    def encrypt_replicated(self, x):
+        return np.asarray(x, dtype=complex)
+
+    def encrypt_replicated_complex(self, xr, xi):
+        return np.asarray(xr) + 1j * np.asarray(xi)
+
+    def decrypt_vec(self, ct, n):
+        return ct.real[:n]
+
+    def decrypt_vec_complex(self, ct, n):
+        return ct[:n]
+
+    def encode_real(self, M):
+        return M.astype(complex)
+
+    def encode_complex(self, M1, M2):
+        return M1 + 1j * M2
+
+    def baby(self, ct):
+        return ct
+
+    def matmul(self, baby, pts):
+        return pts @ baby
+
+
+@pytest.mark.parametrize("preencoded", [False, True])
+def test_block_chunking_matches_plaintext_block(preencoded):
+    D, F, H = 32, 128, 4
+    rng = np.random.default_rng(0)
+    blocks = [rb.BlockWeights(rng, b, D, F, H) for b in range(2)]
+    srv = ExactServer(D, 64)
+    x = rng.standard_normal(D)
+    st = (x, np.zeros(D), np.zeros(D), np.zeros((H, D // H, D // H)), None)
+    ref = st
+    for blk in blocks:
+        run = rb.BlockRunner(srv, blk, preencoded)
+        out = rb.client_aided_block(run, *st)
+        st = out[:5]
+        ref = rb.plaintext_block(blk, *ref)
+        assert set(out[5]) == {"server_rkv", "server_wo", "server_ffn_key", "server_ffn_val"}
+        for a, b in zip(st[:4], ref[:4]):
+            np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12)
+
+
+def test_projection_matrices_shape_and_stages():
+    D, F = 16, 64
+    blk = rb.BlockWeights(np.random.default_rng(1), 0, D, F, 2)
+    names = [n for n, _, _ in rb.projection_matrices(blk)]
+    import fhespear_dist
+    assert names == list(fhespear_dist.RWKV_BLOCK_PROJECTIONS)
+    with pytest.raises(ValueError):
+        rb.BlockRunner(ExactServer(D, 32), rb.BlockWeights(np.random.default_rng(1), 0, D, 3 * D, 2), False)
+
+
+@pytest.mark.gpu
+def test_client_aided_block_on_gpu(ph):
+    """2 blocks, N = 2048, L0 = 4, D = 64, F = 256: every projection a fused BSGS on the GPU."""
+    import argparse
+    a = argparse.Namespace(N=2048, L0=4, P=2, D=64, F=256, head_size=16, blocks=2, reps=1, seed=5,
+                           preencoded=True)
+    recs = rb.run_blocks(ph, a, log=lambda *_: None)
+    assert len(recs) == 2
+    for r in recs:
+        assert r["corr"] > 0.999999, r
+        assert r["max_err"] < 1e-4 * max(1.0, r["mag"]), r
