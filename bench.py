@@ -224,7 +224,7 @@ def main():
             ach = ab / (ms / args.steps * 1e-3) / 1e9
             # traffic: HBM-side bytes per launch from the committed rocprofv3 PMC passes of this
             # workload (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py); null when absent
-            tr = traffic.get(name)
+            tr = traffic.get(name) or traffic.get(name + "_h")   # half-limb variant names
             tr_b = int(tr["traffic_bytes_per_step"] / max(tr["launches_per_step"], 1)) if tr else None
             return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr_b,
