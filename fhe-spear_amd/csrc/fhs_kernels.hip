@@ -43,7 +43,8 @@
 #define FHS_MODUPH_RL 3
 #endif
 #ifndef FHS_MODUP_MAP
-#define FHS_MODUP_MAP 2     // block->(limb, input) map of k_modup: 0 plain, 1 XCD t-inner, 2 XCD m-major
+#define FHS_MODUP_MAP 1     // block->(limb, input) map of k_modup: 0 plain, 1 XCD t-inner, 2 XCD m-major
+                            // (A/B at cfg2, profiles/r01/ab_modup.log: 1 = 2.71 ms, 2 = 2.80, 0 = 2.90)
 #endif
 #ifndef FHS_MODDOWN_MAP
 #define FHS_MODDOWN_MAP 0
