@@ -11,6 +11,13 @@ The data path has exactly two exchange steps, both on flat int64 views of cipher
 Projections are assigned round-robin (projection p -> rank p % world).  The reference runs the
 block's 8 BSGS calls serially in one process (bg:784-892); which of them are independent:
 r, k, v (same input x) -> o -> ffn key pair (shared input, shared baby steps) -> ffn value pair.
+
+Latency mode: one matvec's B giant groups split over the ranks
+(`giant_groups`); each rank computes its groups' rotated inner sums without the rescale
+(`bsgs_giant_partial`, one fused linear transform), the partial ciphertexts are summed mod q_i on
+the root (`modular_reduce_sum`: RCCL int64 sum, then one reduction) and the root rescales.  Every
+giant term is an exact residue (the library sums giant steps before ModDown exactly), so the result
+is limb-identical to the one-GPU fused BSGS.
 """
 from __future__ import annotations
 
@@ -61,3 +68,58 @@ def modular_reduce_sum(dist, tensor, moduli_per_row, root: int = 0):
         t = tensor.view(q.shape[0], -1)
         t.remainder_(q)
     return tensor
+
+
+# ------------------------------------------------------------------ giant-step sharding (§8e(2))
+def giant_groups(B: int, world: int, rank: int) -> list[int]:
+    """Contiguous, balanced share of the giant groups 0..B-1 for `rank` (sizes differ by <= 1)."""
+    if world > B:
+        raise ValueError(f"giant_groups: {world} ranks for {B} giant groups")
+    base, extra = divmod(B, world)
+    lo = rank * base + min(rank, extra)
+    return list(range(lo, lo + base + (1 if rank < extra else 0)))
+
+
+def bsgs_giant_partial(ph, ctx, baby, pts, G: int, D: int, groups, gk, zero_pts):
+    """sum_{g in groups} rot_{gG}( sum_b baby[b] (.) pts[gG + b] ), not rescaled (bg:468-483 for a
+    subset of g).  `pts` maps a diagonal index to its plaintext (a list, or a dict holding only this
+    rank's diagonals); `zero_pts` = G encodings of 0 at the diagonals' level, which fill the identity
+    group fhs_linear_transform requires when g = 0 is not ours and pad a short last group."""
+    elts, flat = [1], []
+    if groups and groups[0] == 0:
+        first, rest = [0], groups[1:]
+    else:
+        first, rest = [], groups
+        flat.extend(zero_pts[:G])
+    for g in first + list(rest):
+        if g:
+            elts.append(ph.get_elt_from_step(g * G, ctx.N))
+        for b in range(G):
+            k = g * G + b
+            flat.append(pts[k] if k < D else zero_pts[b])
+    return ph.linear_transform(ctx, baby, flat, G, elts, gk, rescale=False)
+
+
+def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts, dist, device="cuda"):
+    """One matvec with its giant groups split over the ranks of `dist` (gloo stages through host
+    memory).  Returns the rescaled output ciphertext on rank 0, None elsewhere; limb-identical to
+    ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    part = bsgs_giant_partial(ph, ctx, baby, pts, G, D, giant_groups(B, world, rank), gk, zero_pts)
+    ci, scale, l = part.chain_index(), part.scale(), part.coeff_modulus_size()
+    buf = torch.empty(2 * l * ctx.N, dtype=torch.int64, device=device)
+    torch.cuda.synchronize()                      # torch's earlier use of the allocation is done
+    ph.ciphertext_copy_to_device(ctx, part, buf.data_ptr())
+    rows = [int(q) for q in ctx.primes[:l]] * 2   # [comp][limb] rows, limb t mod q_t
+    if dist.get_backend() == "gloo":
+        h = buf.cpu()
+        modular_reduce_sum(dist, h, rows)
+        buf.copy_(h)
+    else:
+        modular_reduce_sum(dist, buf, rows)
+    if rank != 0:
+        return None
+    torch.cuda.synchronize()
+    total = ph.ciphertext_from_device(ctx, buf.data_ptr(), 2, ci, scale)
+    return ph.rescale_to_next(ctx, total)

@@ -1,0 +1,41 @@
+"""Giant-step sharding of one BSGS matvec over ranks (fhespear_dist)."""
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "fhe-spear_amd" / "python"))
+
+import fhespear_dist as fd  # noqa: E402
+
+
+@pytest.mark.parametrize("B,world", [(45, 1), (45, 2), (45, 8), (32, 8), (7, 7), (16, 3)])
+def test_giant_groups_partition(B, world):
+    shares = [fd.giant_groups(B, world, r) for r in range(world)]
+    assert sorted(g for s in shares for g in s) == list(range(B))
+    sizes = [len(s) for s in shares]
+    assert max(sizes) - min(sizes) <= 1 and min(sizes) >= 1
+    assert all(s == list(range(s[0], s[0] + len(s))) for s in shares)
+
+
+def test_giant_groups_rejects_more_ranks_than_groups():
+    with pytest.raises(ValueError):
+        fd.giant_groups(4, 8, 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [256, 200])   # 200: short last giant group, padded with zero diagonals
+def test_giant_sharded_bsgs_bit_exact_two_ranks(require_gpu, D):
+    """Two ranks on one GPU (gloo, host-staged reduce): the root's rescaled sum of the ranks'
+    partial giant sums equals the one-GPU fused BSGS limb for limb."""
+    env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29551 + D % 7), str(REPO / "tools" / "giant_shard.py"),
+           "--backend", "gloo", "--N", "4096", "--L0", "6", "--P", "3", "--D", str(D), "--reps", "1"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert re.search(r"bit-exact vs one-GPU fused BSGS: True", out.stdout), out.stdout[-2000:]

@@ -1,0 +1,120 @@
+"""Latency-mode BSGS: one matvec's giant groups split over the ranks, partial
+ciphertexts summed mod q_i on rank 0 over RCCL (fhespear_dist.bsgs_giant_sharded), checked
+limb-for-limb against the one-GPU fused BSGS (bg:459) on rank 0.
+
+Every rank builds the same context, keys, input encryption (deterministic from the seeds) and
+diagonals; each computes the baby steps of the input (hoisted) and its share of the giant groups.
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/giant_shard.py            # RCCL
+    FHESPEAR_DEVICE=0 torchrun --nproc-per-node 2 ... tools/giant_shard.py --backend gloo --N 4096 --L0 6 --D 256
+"""
+import argparse
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "fhe-spear_amd" / "python"))
+
+import fhespear_dist as fd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=16384)
+    ap.add_argument("--L0", type=int, default=36)
+    ap.add_argument("--P", type=int, default=3)
+    ap.add_argument("--D", type=int, default=2048)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--simulate-world", type=int, nargs="*", default=[],
+                    help="also time one rank's share of the compute at these world sizes (on this GPU alone)")
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+        local = int(os.environ.get("FHESPEAR_DEVICE", local % max(1, torch.cuda.device_count())))
+    rank = dist.get_rank()
+    import pyPhantom as ph
+
+    N, D = a.N, a.D
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(a.P)
+    parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(list(range(1, G)) + [g * G for g in range(1, B)], N))))
+    parms.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * (a.L0 + a.P)))
+    ctx = ph.context(parms, device=local)
+    sk = ph.secret_key(ctx, seed=77)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    scale = 2.0 ** 59
+    x = np.random.default_rng(1).normal(0, 0.1, D)
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), scale))
+    level = ct.chain_index()
+    pts = ph.random_plaintexts(ctx, 5, D, level, scale)
+    zero = enc.encode_double_vector_batch(ctx, np.zeros((G, N // 2)), scale, chain_index=level)
+    dev = f"cuda:{local}"
+
+    def sharded():
+        baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+        return fd.bsgs_giant_sharded(ph, ctx, baby, pts, G, B, D, gk, zero, dist, dev)
+
+    def barrier():
+        ctx.synchronize()
+        dist.barrier()
+
+    y = sharded()
+    exact = None
+    if rank == 0:
+        baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+        ref = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+        exact = bool(np.array_equal(y.to_numpy(), ref.to_numpy())) and y.scale() == ref.scale() \
+            and y.chain_index() == ref.chain_index()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.reps):
+        sharded()
+    barrier()
+    t_sh = (time.perf_counter() - t0) / a.reps
+    if rank == 0:
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+            ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+        ctx.synchronize()
+        t_one = (time.perf_counter() - t0) / a.reps
+        print(f"giant-sharded BSGS N={N} L0={a.L0} D={D} (G={G}, B={B}) over {world} ranks "
+              f"({a.backend}): bit-exact vs one-GPU fused BSGS: {exact}; "
+              f"sharded {1e3 * t_sh:.2f} ms/matvec, one GPU {1e3 * t_one:.2f} ms/matvec", flush=True)
+    if rank == 0 and a.simulate_world:
+        # one rank's compute at world size W (rank 0 holds the largest share), measured alone:
+        # baby steps + its giant groups + the root's rescale; the RCCL reduce is not included
+        for W in a.simulate_world:
+            grp = fd.giant_groups(B, W, 0)
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+                ph.rescale_to_next(ctx, fd.bsgs_giant_partial(ph, ctx, baby, pts, G, D, grp, gk, zero))
+            ctx.synchronize()
+            print(f"  per-rank compute at world {W} ({len(grp)} of {B} giant groups): "
+                  f"{1e3 * (time.perf_counter() - t0) / a.reps:.2f} ms/matvec", flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    if rank == 0 and not exact:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()
