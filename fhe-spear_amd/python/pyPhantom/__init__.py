@@ -748,6 +748,16 @@ def bsgs_from_cpu(ctx, ct_baby, data, chain_index, scale, coeff_modulus_size, po
                gk._h, what="bsgs_from_cpu")
 
 
+def bsgs_complete_from_cpu(ctx, ct_x, data, chain_index, scale, coeff_modulus_size, poly_modulus_degree, G, B, D,
+                           gk):
+    """bg:244 (fork-only, called from _parallel_bsgs_projections' thread pool): the baby steps of
+    ct_x (bg:215-220, one hoisted key-switch inside the library) then bsgs_from_cpu.  Safe from
+    several threads on one context: every library call holds the context's lock."""
+    G = int(G)
+    baby = [ct_x] + [rotate(ctx, ct_x, b, gk) for b in range(1, G)]
+    return bsgs_from_cpu(ctx, baby, data, chain_index, scale, coeff_modulus_size, poly_modulus_degree, G, B, D, gk)
+
+
 # ------------------------------------------------------------------ measurement helpers
 def random_plaintexts(ctx, seed, count, chain_index, scale):
     hs = (_vp * count)()

@@ -220,6 +220,31 @@ def test_bsgs_fused_equals_op_by_op_loop(ph):
     assert np.array_equal(fused.to_numpy(), res.to_numpy())
 
 
+def test_bsgs_complete_from_cpu_thread_pool(ph):
+    """bg:226-249 _parallel_bsgs_projections: ph.bsgs_complete_from_cpu (baby steps + host-streamed
+    BSGS in one call) issued from a 4-worker thread pool on one context equals the sequential
+    rotate + bsgs_multiply_accumulate for each input, limb for limb."""
+    from concurrent.futures import ThreadPoolExecutor
+    N, L0, P, D = 2048, 6, 3, 64
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=6)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(9)
+    cts = [sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(rng.normal(0, 0.1, D), (N // 2) // D),
+                                                              2.0 ** 59)) for _ in range(4)]
+    pts = [ph.random_plaintexts(ctx, 10 + i, D, cts[0].chain_index(), 2.0 ** 59) for i in range(4)]
+    host = [ph.offload_plaintexts(p) for p in pts]
+    with ThreadPoolExecutor(max_workers=4) as pool:
+        futs = [pool.submit(ph.bsgs_complete_from_cpu, ctx, ct, *h, G, B, D, gk) for ct, h in zip(cts, host)]
+        got = [f.result() for f in futs]
+    for ct, p, y in zip(cts, pts, got):
+        baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+        assert np.array_equal(y.to_numpy(), ph.bsgs_multiply_accumulate(ctx, baby, p, G, B, D, gk).to_numpy())
+
+
 def test_bsgs_decrypts_to_matvec(ph):
     """Accuracy contract of tf:272-298 (corr > 0.999) on the reference's diagonal layout."""
     import __graft_entry__ as ge
