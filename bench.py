@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--cpu-sample-rotations", type=int, default=24)
     ap.add_argument("--cpu-sample-diagonals", type=int, default=512)
     ap.add_argument("--cpu-workers", type=int, default=16)
+    ap.add_argument("--split", action="store_true",
+                    help="cfg3 over N GPUs: latency mode, giant steps of each projection sharded over a rank group")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -291,7 +293,7 @@ def bench_block(args, ph, dist, rank, world, local):
     rng = np.random.default_rng(5)
     block = rb.BlockWeights(rng, 1, D, F, H)
     srv = rb.Server(ph, cfg["N"], cfg["L0"], cfg["P"], D, device=local)
-    run = rb.BlockRunner(srv, block, True, dist, rank, world)
+    run = rb.BlockRunner(srv, block, True, dist, rank, world, split=args.split)
     x = rng.standard_normal(D)
     st = (x, np.zeros(D), np.zeros(D), np.zeros((H, 64, 64)), rng.standard_normal(D))
 
@@ -334,7 +336,8 @@ def bench_block(args, ph, dist, rank, world, local):
             "data": "synthetic (random-init RWKV-7 block weights, random token state); max |x - plaintext block| "
                     f"= {err:.2e}",
             "config": {"workload": cfg["workload"], "N": cfg["N"], "L0": l, "P": cfg["P"], "d": D, "d_ffn": F,
-                       "projections": 8, "parallelism": f"stage-dealt projections x{world}"
+                       "projections": 8, "parallelism": (f"giant-step-split projections x{world}" if args.split
+                                                         else f"stage-dealt projections x{world}")
                        + (" + RCCL broadcast/gather" if world > 1 else "")},
             "stages_ms": {k: round(1e3 * v / args.steps, 2) for k, v in stage.items()},
             "matvec_roofline": {"bound": "hbm", "bytes_per_block": 8 * mv, "achieved": round(8 * mv / sec / 1e9, 1),

@@ -55,19 +55,35 @@ def broadcast_from(dist, tensor, src: int):
     return tensor
 
 
-def modular_reduce_sum(dist, tensor, moduli_per_row, root: int = 0):
-    """Sum of residues across ranks, reduced mod q_i per limb row (giant-step sharding, §8e(2)).
-    RCCL's integer sum is not modular; with < 8 ranks and 59-bit residues the plain int64 sum
-    stays < 2^63, so one final reduction on the root is exact."""
+def modular_reduce_sum(dist, tensor, moduli_per_row, root: int = 0, group=None):
+    """Sum of residues across the ranks of `group` (default: all), reduced mod q_i per limb row on
+    the global rank `root` (giant-step sharding, §8e(2)).  RCCL's integer sum is not modular; with
+    <= 15 ranks and 59-bit residues the plain int64 sum stays < 2^63, so one final reduction on the
+    root is exact."""
     import torch
-    if dist.get_world_size() > 15:
+    if dist.get_world_size(group) > 15:
         raise ValueError("modular_reduce_sum: > 15 ranks could overflow int64 with 59-bit residues")
-    dist.reduce(tensor, dst=root)
+    dist.reduce(tensor, dst=root, group=group)
     if dist.get_rank() == root:
         q = torch.as_tensor(moduli_per_row, dtype=torch.int64, device=tensor.device).view(-1, 1)
         t = tensor.view(q.shape[0], -1)
         t.remainder_(q)
     return tensor
+
+
+def stage_groups(n_proj: int, world: int):
+    """Latency mode for one block stage: its n_proj projections -> contiguous, balanced groups of
+    ranks (sizes differ by <= 1), each group sharding one projection's giant steps.  None when
+    there are fewer ranks than projections (the stage is dealt round-robin instead)."""
+    if world < n_proj:
+        return None
+    base, extra = divmod(world, n_proj)
+    out, lo = [], 0
+    for i in range(n_proj):
+        s = base + (1 if i < extra else 0)
+        out.append(list(range(lo, lo + s)))
+        lo += s
+    return out
 
 
 # ------------------------------------------------------------------ giant-step sharding (§8e(2))
@@ -100,25 +116,29 @@ def bsgs_giant_partial(ph, ctx, baby, pts, G: int, D: int, groups, gk, zero_pts)
     return ph.linear_transform(ctx, baby, flat, G, elts, gk, rescale=False)
 
 
-def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts, dist, device="cuda"):
-    """One matvec with its giant groups split over the ranks of `dist` (gloo stages through host
-    memory).  Returns the rescaled output ciphertext on rank 0, None elsewhere; limb-identical to
-    ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)."""
+def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts, dist, device="cuda",
+                       ranks=None, group=None):
+    """One matvec with its giant groups split over `ranks` (global ranks of process group `group`;
+    default: every rank), gloo staging through host memory.  Returns the rescaled output ciphertext
+    on ranks[0], None elsewhere; limb-identical to ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B,
+    D, gk).  `pts` need only hold this rank's diagonals."""
     import torch
-    world, rank = dist.get_world_size(), dist.get_rank()
-    part = bsgs_giant_partial(ph, ctx, baby, pts, G, D, giant_groups(B, world, rank), gk, zero_pts)
+    me = dist.get_rank()
+    ranks = list(range(dist.get_world_size())) if ranks is None else list(ranks)
+    share = giant_groups(B, len(ranks), ranks.index(me))
+    part = bsgs_giant_partial(ph, ctx, baby, pts, G, D, share, gk, zero_pts)
     ci, scale, l = part.chain_index(), part.scale(), part.coeff_modulus_size()
     buf = torch.empty(2 * l * ctx.N, dtype=torch.int64, device=device)
     torch.cuda.synchronize()                      # torch's earlier use of the allocation is done
     ph.ciphertext_copy_to_device(ctx, part, buf.data_ptr())
     rows = [int(q) for q in ctx.primes[:l]] * 2   # [comp][limb] rows, limb t mod q_t
-    if dist.get_backend() == "gloo":
+    if dist.get_backend(group) == "gloo":
         h = buf.cpu()
-        modular_reduce_sum(dist, h, rows)
+        modular_reduce_sum(dist, h, rows, root=ranks[0], group=group)
         buf.copy_(h)
     else:
-        modular_reduce_sum(dist, buf, rows)
-    if rank != 0:
+        modular_reduce_sum(dist, buf, rows, root=ranks[0], group=group)
+    if me != ranks[0]:
         return None
     torch.cuda.synchronize()
     total = ph.ciphertext_from_device(ctx, buf.data_ptr(), 2, ci, scale)

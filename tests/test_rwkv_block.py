@@ -89,21 +89,25 @@ def test_projection_matrices_shape_and_stages():
 
 
 @pytest.mark.gpu
-def test_block_dealt_over_two_ranks(require_gpu):
-    """cfg4's exchange (stage inputs broadcast from the client rank, output ciphertexts gathered to
-    it) with world size 2 on one GPU: gloo stages the limbs through host memory, both ranks' contexts
-    share cuda:0.  The decrypted block must match the plaintext block as in the one-rank case."""
+@pytest.mark.parametrize("world,split", [(2, False), (2, True), (4, True)])
+def test_block_over_ranks(require_gpu, world, split):
+    """cfg4's exchange (stage inputs broadcast from the client rank, output ciphertexts to it) on one
+    GPU: gloo stages the limbs through host memory, every rank's context shares cuda:0.  split=True
+    is latency mode (giant steps of a projection sharded over a rank group: at world 4 the stages
+    split 2+1+1 / 4 / 2+2 / 2+2; at world 2 stage 1 is dealt).  The decrypted block must match the
+    plaintext block as in the one-rank case."""
     import os
     import re
     import subprocess
     env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29541", str(REPO / "tools" / "rwkv_block.py"),
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(29541 + world + 10 * split),
+           str(REPO / "tools" / "rwkv_block.py"),
            "--backend", "gloo", "--N", "2048", "--L0", "4", "--P", "2", "--D", "64", "--F", "256",
-           "--head-size", "16", "--blocks", "2", "--reps", "1", "--preencoded"]
+           "--head-size", "16", "--blocks", "2", "--reps", "1", "--preencoded"] + (["--split"] if split else [])
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
-    m = re.search(r"world 2: .* final max_err ([0-9.e+-]+)", out.stdout)
+    m = re.search(rf"world {world}.*: .* final max_err ([0-9.e+-]+)", out.stdout)
     assert m, out.stdout[-2000:]
     assert float(m.group(1)) < 1e-4
     assert all(float(c) > 0.999999 for c in re.findall(r"corr=([0-9.]+)", out.stdout))

@@ -178,13 +178,15 @@ class Server:
         return np.array(self.encoder.decode_complex_vector(self.ctx, self.sk.decrypt(self.ctx, ct)))[:n]
 
     # bg:361-432
-    def encode_real(self, M):
-        return self.encoder.encode_double_vector_batch(self.ctx, _diag_rows(M, self.D, self.G, self.slots),
-                                                       self.diag_scale, chain_index=self.level)
+    def encode_real(self, M, rows=None):
+        d = _diag_rows(M, self.D, self.G, self.slots)
+        return self.encoder.encode_double_vector_batch(self.ctx, d if rows is None else d[rows], self.diag_scale,
+                                                       chain_index=self.level)
 
-    def encode_complex(self, M1, M2):
+    def encode_complex(self, M1, M2, rows=None):
         z = _diag_rows(M1, self.D, self.G, self.slots) + 1j * _diag_rows(M2, self.D, self.G, self.slots)
-        return self.encoder.encode_complex_vector_batch(self.ctx, z, self.diag_scale, chain_index=self.level)
+        return self.encoder.encode_complex_vector_batch(self.ctx, z if rows is None else z[rows], self.diag_scale,
+                                                        chain_index=self.level)
 
     def baby(self, ct):
         """bg:215-220"""
@@ -223,25 +225,57 @@ def projection_matrices(block):
 
 
 class BlockRunner:
-    """Server projections of client_aided_block, local or dealt over ranks (cfg4)."""
+    """Server projections of client_aided_block, local or over ranks (cfg4).  Over ranks, a stage's
+    projections are dealt round-robin (one projection per rank: throughput), or with split=True
+    (latency mode) each projection gets a group of ranks that shard its giant
+    steps (fhespear_dist.stage_groups / bsgs_giant_sharded); a stage with more projections than
+    ranks is dealt."""
 
-    def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1):
+    def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1, split=False):
         self.srv, self.block, self.pre, self.dist, self.rank, self.world = srv, block, preencoded, dist, rank, world
         self.mats = {n: (k, m) for n, k, m in projection_matrices(block)}
         if set(self.mats) != set(fhespear_dist.RWKV_BLOCK_PROJECTIONS):
             raise ValueError("rwkv_block: this runner expects F = 4 D (8 projections, RWKV-7)")
         self.assign = fhespear_dist.stage_assignment(world, rank)
         self.host_coll = dist is not None and dist.get_backend() == "gloo"
+        # latency mode: per stage, [(projection, ranks, process group)] or None (dealt)
+        self.layout = [None] * len(fhespear_dist.RWKV_BLOCK_STAGES)
+        self.share = {}                      # projection -> giant groups this rank computes
+        if split and dist is not None:
+            for i, names in enumerate(fhespear_dist.RWKV_BLOCK_STAGES):
+                groups = fhespear_dist.stage_groups(len(names), world)
+                if groups is None:
+                    continue
+                lay = []
+                for n, ranks in zip(names, groups):   # every rank creates every group, same order
+                    pg = dist.new_group(ranks) if len(ranks) > 1 else None
+                    lay.append((n, ranks, pg))
+                    if rank in ranks:
+                        self.share[n] = fhespear_dist.giant_groups(srv.B, len(ranks), ranks.index(rank))
+                self.layout[i] = lay
+                self.assign[i] = [n for n, ranks, _ in lay if rank in ranks]
+            self.zero = srv.encoder.encode_double_vector_batch(srv.ctx, np.zeros((srv.G, srv.slots)), srv.diag_scale,
+                                                               chain_index=srv.level)
         mine = {n for st in self.assign for n in st}
         self.pts = {}
         if preencoded:                       # bg:1124-1174 --preencoded, resident in HBM
             for n in mine:
                 self.pts[n] = self._encode(n)
-        self.timings = {}
+
+    def _rows(self, name):
+        """diagonal indices this rank needs for `name` (its giant groups' share, or all D)"""
+        if name not in self.share:
+            return None
+        G, D = self.srv.G, self.srv.D
+        return [g * G + b for g in self.share[name] for b in range(G) if g * G + b < D]
 
     def _encode(self, name):
         kind, ms = self.mats[name]
-        return self.srv.encode_real(*ms) if kind == "real" else self.srv.encode_complex(*ms)
+        rows = self._rows(name)
+        if rows is None:
+            return self.srv.encode_real(*ms) if kind == "real" else self.srv.encode_complex(*ms)
+        pts = self.srv.encode_real(*ms, rows=rows) if kind == "real" else self.srv.encode_complex(*ms, rows=rows)
+        return dict(zip(rows, pts))
 
     def _pts(self, name):
         return self.pts[name] if self.pre else self._encode(name)
@@ -291,6 +325,8 @@ class BlockRunner:
             key = inputs[n][1]
             if key not in cts:
                 cts[key] = inputs[n][0] if self.dist is None else self._bcast_ct(inputs[n][0])
+        if self.layout[idx] is not None:
+            return self._stage_split(idx, inputs, cts)
         mine = names if self.dist is None else self.assign[idx]
         babies = {}
         outs = {}
@@ -302,6 +338,52 @@ class BlockRunner:
         if self.dist is None:
             return outs
         return self._gather(names, outs)
+
+    def _stage_split(self, idx, inputs, cts):
+        """Latency mode: each projection's rank group shards its giant steps; the group roots send
+        the rescaled outputs to rank 0 (the client)."""
+        import torch
+        srv, ph = self.srv, self.srv.ph
+        dev = f"cuda:{srv.device}"
+        res = {}
+        for n, ranks, pg in self.layout[idx]:
+            if self.rank not in ranks:
+                continue
+            baby = srv.baby(cts[inputs[n][1]])
+            pts = self._pts(n)
+            if len(ranks) == 1:
+                out = srv.matmul(baby, [pts[k] for k in range(srv.D)] if isinstance(pts, dict) else pts)
+            else:
+                out = fhespear_dist.bsgs_giant_sharded(ph, srv.ctx, baby, pts, srv.G, srv.B, srv.D, srv.gk,
+                                                       self.zero, self.dist, dev, ranks=ranks, group=pg)
+            if out is not None:
+                res[n] = out
+        ci = srv.level + 1
+        got = {}
+        for n, ranks, _ in self.layout[idx]:          # group roots -> rank 0 (point to point)
+            src = ranks[0]
+            if src == 0:
+                if self.rank == 0:
+                    got[n] = res[n]
+                continue
+            if self.rank == src:
+                buf = self._buf(ci)
+                self._pack(res[n], buf)
+                srv.ctx.synchronize()
+                if self.host_coll:
+                    self.dist.send(buf.cpu(), dst=0)
+                else:
+                    self.dist.send(buf, dst=0)
+            elif self.rank == 0:
+                buf = self._buf(ci)
+                if self.host_coll:
+                    h = buf.cpu()
+                    self.dist.recv(h, src=src)
+                    buf.copy_(h)
+                else:
+                    self.dist.recv(buf, src=src)
+                got[n] = self._unpack(buf, ci)
+        return got
 
     def _gather(self, names, outs):
         """Output ciphertexts -> rank 0 (RCCL gather); projection i of the stage lives on rank i % world."""
@@ -414,7 +496,8 @@ def run_blocks(ph, args, dist=None, rank=0, world=1, device=0, log=print):
     blocks = [BlockWeights(rng, b, args.D, args.F, H) for b in range(args.blocks)]
     t0 = time.perf_counter()
     srv = Server(ph, args.N, args.L0, args.P, args.D, device=device)
-    runs = [BlockRunner(srv, b, args.preencoded, dist, rank, world) for b in blocks]
+    runs = [BlockRunner(srv, b, args.preencoded, dist, rank, world, split=getattr(args, "split", False))
+            for b in blocks]
     srv.ctx.synchronize()
     if rank == 0:
         log(f"setup (keys{', pre-encoded diagonals' if args.preencoded else ''}): {time.perf_counter() - t0:.2f} s")
@@ -453,6 +536,8 @@ def main():
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--preencoded", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--split", action="store_true",
+                    help="latency mode: each stage's projections shard their giant steps over rank groups")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -471,7 +556,7 @@ def main():
     recs = run_blocks(ph, a, dist, rank, world, local)
     if rank == 0:
         s = [r["server_seconds"] for r in recs]
-        print(f"world {world}: mean server time per block {np.mean(s):.4f} s over {len(s)} block(s), "
+        print(f"world {world}{' split' if a.split else ''}: mean server time per block {np.mean(s):.4f} s over {len(s)} block(s), "
               f"final max_err {recs[-1]['max_err']:.3e}")
     if dist is not None:
         dist.barrier()
