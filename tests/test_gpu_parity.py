@@ -287,6 +287,74 @@ def test_errors(ph):
         ph.context(parms)
 
 
+@pytest.mark.parametrize("N,L0,P,D", [(8192, 24, 3, 1024), (16384, 36, 3, 2048)])
+def test_fused_bsgs_equals_loop_at_baseline_configs(ph, N, L0, P, D):
+    """BASELINE configs[0] / configs[1] at full size (d=1024 N=8192 L0=24; d=2048 N=16384 L0=36):
+    the fused bsgs_multiply_accumulate equals the reference loop bg:464-485 issued op by op
+    (D multiply_plain, D-1 add, B-1 rotate, 1 rescale) limb for limb, and the decrypted result is
+    the matvec (tf:272-298's corr criterion, tighter)."""
+    import __graft_entry__ as ge
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=13)
+    enc = ph.ckks_encoder(ctx)
+    gk = sk.create_galois_keys(ctx)
+    rng = np.random.default_rng(14)
+    x = rng.normal(0, 0.1, D)
+    W = rng.normal(0, 0.02, (D, D))
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), 2.0 ** 59))
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    pts = enc.encode_double_vector_batch(ctx, ge._rolled_diagonals(W, D, G, N // 2), 2.0 ** 59,
+                                         chain_index=ct.chain_index())
+    res = None
+    for g in range(B):
+        inner = None
+        for b in range(G):
+            k = g * G + b
+            if k >= D:
+                continue
+            term = ph.multiply_plain(ctx, baby[b], pts[k])
+            inner = term if inner is None else ph.add(ctx, inner, term)
+        if g > 0:
+            inner = ph.rotate(ctx, inner, g * G, gk)
+        res = inner if res is None else ph.add(ctx, res, inner)
+    res = ph.rescale_to_next(ctx, res)
+    fused = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    assert np.array_equal(fused.to_numpy(), res.to_numpy())
+    dec = np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, fused)))[:D]
+    ref = W @ x
+    assert np.corrcoef(dec, ref)[0, 1] > 0.999999
+    assert np.max(np.abs(dec - ref)) < 1e-8
+
+
+def test_bsgs_matches_oracle_on_cfg2_ring(ph):
+    """The cfg2 ring and chain (N = 16384, 36 + 3 primes) with a small D = 16 so the C oracle
+    finishes in seconds: keys, encryption, hoisted baby rotations and the fused BSGS are
+    bit-identical to the oracle's restatement of bg:215-220 + bg:464-485 at full size."""
+    N, L0, P, D, seed = 16384, 36, 3, 16, 31
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=seed)
+    gk = sk.create_galois_keys(ctx)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(seed)
+    rng = np.random.default_rng(15)
+    a = rand_ct(o, rng, 2, L0)
+    ct = ph.ciphertext_from_numpy(ctx, a, 1, 2.0 ** 59)
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    bkeys = {b: o.gen_galois_key(seed, s, ph.get_elt_from_step(b, N)) for b in range(1, G)}
+    want_baby = [a] + [o.rotate_elt(a, bkeys[b], ph.get_elt_from_step(b, N)) for b in range(1, G)]
+    for b in range(G):
+        assert np.array_equal(baby[b].to_numpy(), want_baby[b]), f"baby step {b}"
+    pts = ph.random_plaintexts(ctx, 16, D, 1, 2.0 ** 59)
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    gkeys = [None] + [o.gen_galois_key(seed, s, ph.get_elt_from_step(g * G, N)) for g in range(1, B)]
+    want = o.bsgs_loop(want_baby, [p.to_numpy() for p in pts], gkeys, G, B, D)
+    assert np.array_equal(y.to_numpy(), want)
+
+
 def test_n32768_encode_bsgs_and_fused_equals_loop(ph):
     """cfg5's ring size (N = 32768, BASELINE configs[4]): every NTT runs in its half-limb form and
     the encoder FFT in its split form; decode accuracy, fused BSGS == op-by-op loop, and the
