@@ -1166,12 +1166,37 @@ static void fft_inplace(std::vector<std::complex<double>>& a, const std::vector<
 
 // values: count vectors of n complex (re,im) (or real when is_real); produces rounded coefficients
 
-static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, size_t n, bool is_real, double scale,
-                              int ci, fhs_plaintext** outs) {
+// Encode `cnt` value rows already in HBM (row v at dvals + v * stride doubles) into new plaintexts.
+static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cnt, size_t n, size_t stride,
+                                  bool is_real, double scale, int ci, fhs_plaintext** outs) {
+    const int l = c->L0 + 1 - ci;
+    std::vector<uint64_t*> ptrs(cnt);
+    for (size_t v = 0; v < cnt; ++v) {
+        fhs_plaintext* pt = nullptr;
+        fhs_status s = new_pt(c, ci, scale, &pt);
+        if (s != FHS_OK) return s;
+        outs[v] = pt;
+        ptrs[v] = pt->d;
+    }
+    uint64_t* dptrs = nullptr;
+    hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * cnt, &dptrs);
+    if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * cnt);
+    if (e == hipSuccess)
+        e = fhs::launch_encode(c->T, dvals, (int)cnt, n, stride, is_real, scale, reinterpret_cast<fhs::u64* const*>(dptrs),
+                               l, c->st);
+    return e == hipSuccess ? FHS_OK : hip_fail(e, "encode");
+}
+static fhs_status encode_checks(fhs_context* c, size_t n, double scale, int ci) {
     if (n > c->N / 2) return fail(FHS_ERR_INVALID, "encode: more values than slots");
     if (!(scale > 0) || !std::isfinite(scale)) return fail(FHS_ERR_INVALID, "encode: bad scale");
     const int l = c->L0 + 1 - ci;
     if (ci < 1 || l < 1) return fail(FHS_ERR_LEVEL, "encode: chain index out of range");
+    return FHS_OK;
+}
+static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, size_t n, bool is_real, double scale,
+                              int ci, fhs_plaintext** outs) {
+    fhs_status st = encode_checks(c, n, scale, ci);
+    if (st != FHS_OK) return st;
     if (count == 0) return FHS_OK;
     const size_t stride = is_real ? n : 2 * n;
     // values -> HBM (the copy completes before returning: the caller's buffer may be reused), then
@@ -1188,26 +1213,51 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
             if (e != hipSuccess) { dfree(c, dvals, 8 * cnt * stride); return hip_fail(e, "encode upload"); }
         }
         ht.mark("encode: upload");
-        std::vector<uint64_t*> ptrs(cnt);
-        for (size_t v = 0; v < cnt; ++v) {
-            fhs_plaintext* pt = nullptr;
-            fhs_status s = new_pt(c, ci, scale, &pt);
-            if (s != FHS_OK) { dfree(c, dvals, 8 * cnt * stride); return s; }
-            outs[base + v] = pt;
-            ptrs[v] = pt->d;
-        }
-        uint64_t* dptrs = nullptr;
-        hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * cnt, &dptrs);
-        if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * cnt);
-        if (e == hipSuccess)
-            e = fhs::launch_encode(c->T, reinterpret_cast<const double*>(dvals), (int)cnt, n, stride, is_real, scale,
-                                   reinterpret_cast<fhs::u64* const*>(dptrs), l, c->st);
+        fhs_status s = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci,
+                                       outs + base);
         dfree(c, dvals, std::max<size_t>(8, 8 * cnt * stride));
         ht.mark("encode: objects+launch");
         if (ht.on) { hipStreamSynchronize(c->st); ht.mark("encode: gpu"); }
-        if (e != hipSuccess) return hip_fail(e, "encode");
+        if (s != FHS_OK) return s;
     }
     return FHS_OK;
+}
+
+// Extension (no reference symbol): the whole caller-side diagonal pipeline of bg:198-203 +
+// bg:361-432 on the device -- upload the D x D matrix once (D^2 doubles instead of D x slots),
+// gather the rolled, tiled diagonal rows in HBM, encode them.  Values identical to
+// encode_*_vector_batch on the host-prepared rows, hence identical limbs.
+extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, const double* M2, int D, int G,
+                                           double scale, int ci, fhs_plaintext** out) {
+    ENTER(c);
+    if (!M1 || !out) return fail(FHS_ERR_INVALID, "encode_diagonals: null argument");
+    if (D < 1 || G < 1 || G > D) return fail(FHS_ERR_INVALID, "encode_diagonals: need 1 <= G <= D");
+    const size_t n = c->N / 2;
+    if ((size_t)D > n) return fail(FHS_ERR_INVALID, "encode_diagonals: dimension larger than the slot count");
+    fhs_status st = encode_checks(c, n, scale, ci);
+    if (st != FHS_OK) return st;
+    const bool is_real = M2 == nullptr;
+    const size_t mb = 8ull * D * D, stride = is_real ? n : 2 * n;
+    uint64_t *dm = nullptr, *dvals = nullptr;
+    HIPCHK(dalloc(c, &dm, mb * (is_real ? 1 : 2)), "encode_diagonals matrix");
+    hipError_t e = hipMemcpyAsync(dm, M1, mb, hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess && !is_real) e = hipMemcpyAsync((char*)dm + mb, M2, mb, hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // caller's buffers may be reused on return
+    const size_t chunk = 2048;
+    for (size_t base = 0; e == hipSuccess && st == FHS_OK && base < (size_t)D; base += chunk) {
+        const size_t cnt = std::min(chunk, (size_t)D - base);
+        e = dalloc(c, &dvals, 8 * cnt * stride);
+        if (e != hipSuccess) break;
+        const double* m1 = reinterpret_cast<const double*>(dm);
+        const double* m2 = is_real ? nullptr : reinterpret_cast<const double*>((char*)dm + mb);
+        e = fhs::launch_diag_gather(m1, m2, D, G, (int)n, (int)base, (int)cnt, reinterpret_cast<double*>(dvals), c->st);
+        if (e == hipSuccess)
+            st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci, out + base);
+        dfree(c, dvals, 8 * cnt * stride);
+    }
+    dfree(c, dm, mb * (is_real ? 1 : 2));
+    if (e != hipSuccess) return hip_fail(e, "encode_diagonals");
+    return st;
 }
 
 // Extended-precision encoder for constant plaintexts (bootstrapping transforms): the f64 FFT of

@@ -1612,6 +1612,39 @@ hipError_t launch_encode(const DevTables& T, const double* vals, int count, size
     return hipGetLastError();
 }
 
+// Diagonal extraction + giant-group roll + tiling on the device (bg:198-203 _extract_diagonals and
+// bg:361-378 / 394-421 _batch_encode_diags_*): row k of the encoder input, slot j, is
+//   d_k[m'] = M[m', (m' + k) mod D],  m' = (j mod D - g G) mod D,  g = k / G
+// (np.roll of group g's rows by g G, then np.tile / the remainder columns -- both are j mod D).
+// Complex (M2 != null): re = M1, im = M2, interleaved as the complex encoder reads them.
+__global__ void k_diag_gather(const double* __restrict__ M1, const double* __restrict__ M2, int D, int G, int n,
+                              int k0, int rows, double* __restrict__ out) {
+    const size_t total = (size_t)rows * n;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(idx / n), j = (int)(idx % n), k = k0 + r;
+        const int shift = (k / G) * G % D;
+        int m = j % D - shift;
+        if (m < 0) m += D;
+        int col = m + k % D;
+        if (col >= D) col -= D;
+        const size_t src = (size_t)m * D + col;
+        if (M2) {
+            out[2 * idx] = M1[src];
+            out[2 * idx + 1] = M2[src];
+        } else {
+            out[idx] = M1[src];
+        }
+    }
+}
+hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, double* out,
+                              hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_diag_gather, dim3(eltwise_grid((size_t)rows * n)), dim3(256), 0, st, M1, M2, D, G, n, k0,
+                       rows, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st) {
     hipLaunchKernelGGL(k_encode_reduce, dim3(eltwise_grid((size_t)count * l * T.N)), dim3(256), 0, st, T, coef, count,
                        out, l);

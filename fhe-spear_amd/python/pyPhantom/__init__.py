@@ -124,6 +124,7 @@ _SIGS = {
     "fhs_mod_raise": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     "fhs_bootstrap_evalmod": (C.c_int, [_vp, _vp, _vp, _dblp, _dblp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     "fhs_encode_precise": (C.c_int, [_vp, _dblp, C.c_size_t, C.c_size_t, C.c_double, C.c_int, C.POINTER(_vp)]),
+    "fhs_encode_diagonals": (C.c_int, [_vp, _dblp, _dblp, C.c_int, C.c_int, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_host_alloc": (C.c_int, [_u64, C.POINTER(_vp)]),
     "fhs_host_free": (C.c_int, [_vp]),
     "fhs_random_plaintexts": (C.c_int, [_vp, _u64, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
@@ -546,6 +547,25 @@ class ckks_encoder:
         """bg:423.  precise=True (extension): long-double canonical embedding with exact rounding
         (fhs_encode_precise), for constant plaintexts such as the bootstrap transforms."""
         return self._batch(ctx, mat, scale, chain_index, True, precise)
+
+    def encode_matrix_diagonals(self, ctx, M, G, scale, chain_index=1, M2=None):
+        """Extension (no reference symbol): the caller-side pipeline of bg:198-203 + bg:361-432 --
+        diagonals of the D x D matrix M (complex-packed with M2: bg:394-432), giant group g rolled by
+        g G, tiled to the slots, encoded -- on the GPU from the matrix itself.  Limb-identical to
+        encode_double_vector_batch / encode_complex_vector_batch of the numpy-prepared rows."""
+        A = np.ascontiguousarray(M, dtype=np.float64)
+        if A.ndim != 2 or A.shape[0] != A.shape[1]:
+            raise ValueError("encode_matrix_diagonals: M must be square")
+        B2 = None
+        if M2 is not None:
+            B2 = np.ascontiguousarray(M2, dtype=np.float64)
+            if B2.shape != A.shape:
+                raise ValueError("encode_matrix_diagonals: M and M2 differ in shape")
+        D = A.shape[0]
+        hs = (_vp * D)()
+        _check(_lib.fhs_encode_diagonals(ctx._h, A.ctypes.data_as(_dblp), None if B2 is None else B2.ctypes.data_as(_dblp),
+                                         D, int(G), float(scale), int(chain_index), hs), "encode_matrix_diagonals")
+        return [plaintext(ctx, _vp(hs[i])) for i in range(D)]
 
     def _decode(self, ctx, pt):
         out = np.empty((ctx.N // 2, 2), dtype=np.float64)

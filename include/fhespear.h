@@ -175,6 +175,12 @@ fhs_status fhs_host_free(void* ptr);
 fhs_status fhs_linear_transform(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
                                 const fhs_plaintext* const* pts, int D, int B, const uint64_t* giant_elts,
                                 const fhs_galois_keys* gk, int rescale, fhs_ciphertext** out);
+/* Extension (no reference symbol): bg:198-203 + bg:361-432 on the device -- the D diagonals of the
+ * D x D row-major matrix M1 (complex: M1 + i M2; M2 = NULL for real), group g = k / G rolled by g G,
+ * tiled to N/2 slots, encoded at `scale` / `chain_index`.  Limb-identical to encode_*_vector_batch
+ * of the host-prepared rows; uploads D^2 doubles instead of D x N/2.  out_array: D plaintexts. */
+fhs_status fhs_encode_diagonals(fhs_context* ctx, const double* M1, const double* M2, int D, int G, double scale,
+                                int chain_index, fhs_plaintext** out_array);
 /* encode_complex_vector_batch with an extended-precision (long double) canonical-embedding FFT on the
  * host and exact 128-bit rounding: for constant plaintexts whose f64 encoding error (~2^-52 log n
  * relative) matters -- the bootstrap's CoeffToSlot / SlotToCoeff diagonals.  |values x scale| < 2^126. */

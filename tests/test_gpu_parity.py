@@ -328,6 +328,41 @@ def test_fused_bsgs_equals_loop_at_baseline_configs(ph, N, L0, P, D):
     assert np.max(np.abs(dec - ref)) < 1e-8
 
 
+def _bg_rows(W, D, G, slots):
+    """numpy restatement of bg:198-203 (_extract_diagonals) + bg:361-378 (roll, tile, remainder)"""
+    j = np.arange(D)
+    d = W[j[None, :], (j[None, :] + j[:, None]) % D]
+    r = d.copy()
+    for g in range(1, (D + G - 1) // G):
+        s, e = g * G, min((g + 1) * G, D)
+        r[s:e, g * G:] = d[s:e, :D - g * G]
+        r[s:e, :g * G] = d[s:e, D - g * G:]
+    reps, rem = divmod(slots, D)
+    return np.concatenate([np.tile(r, (1, reps)), r[:, :rem]], axis=1) if rem else np.tile(r, (1, reps))
+
+
+@pytest.mark.parametrize("N,D", [(1024, 32), (1024, 48), (16384, 2048)])
+def test_encode_matrix_diagonals_equals_host_rows(ph, N, D):
+    """Extension fhs_encode_diagonals (diagonal extraction, roll, tiling on the GPU) yields the same
+    plaintext limbs as the batch encoder fed the reference caller's numpy rows (real and complex,
+    slot count a multiple of D or not)."""
+    G = int(np.ceil(np.sqrt(D)))
+    ctx, sk, primes = make_ctx(ph, N, 6 if N < 16384 else 36, 3, seed=17)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(18)
+    W1, W2 = rng.normal(0, 0.02, (D, D)), rng.normal(0, 0.02, (D, D))
+    slots = N // 2
+    got = enc.encode_matrix_diagonals(ctx, W1, G, 2.0 ** 59, chain_index=2)
+    want = enc.encode_double_vector_batch(ctx, _bg_rows(W1, D, G, slots), 2.0 ** 59, chain_index=2)
+    for k in (0, 1, G - 1, G, D // 2, D - 1):
+        assert np.array_equal(got[k].to_numpy(), want[k].to_numpy()), f"real diagonal {k}"
+    gotc = enc.encode_matrix_diagonals(ctx, W1, G, 2.0 ** 59, chain_index=2, M2=W2)
+    wantc = enc.encode_complex_vector_batch(ctx, _bg_rows(W1, D, G, slots) + 1j * _bg_rows(W2, D, G, slots),
+                                            2.0 ** 59, chain_index=2)
+    for k in (0, G, D - 1):
+        assert np.array_equal(gotc[k].to_numpy(), wantc[k].to_numpy()), f"complex diagonal {k}"
+
+
 def test_bsgs_matches_oracle_on_cfg2_ring(ph):
     """The cfg2 ring and chain (N = 16384, 36 + 3 primes) with a small D = 16 so the C oracle
     finishes in seconds: keys, encryption, hoisted baby rotations and the fused BSGS are

@@ -81,6 +81,7 @@ class Ckks:
 
 
 HOST_PREP_S = [0.0]   # numpy diagonal extraction / roll / tile (the reference caller's own work)
+HOST_DIAGONALS = [False]   # --host-diagonals: prepare the rows with numpy as tf does (tf:48, 76)
 
 
 def matmul(ck, ct, M, D, baby):
@@ -88,10 +89,13 @@ def matmul(ck, ct, M, D, baby):
     bsgs_multiply_accumulate (one rescale inside)."""
     ph = ck.ph
     G, B = bsgs_params(D)
-    t0 = time.perf_counter()
-    diags = rolled_diagonals(M, D, G, ck.slots)
-    HOST_PREP_S[0] += time.perf_counter() - t0
-    pts = ck.encoder.encode_double_vector_batch(ck.ctx, diags, ck.scale, chain_index=ct.chain_index())
+    if HOST_DIAGONALS[0]:   # the reference caller's numpy roll/tile, then the batch encoder
+        t0 = time.perf_counter()
+        diags = rolled_diagonals(M, D, G, ck.slots)
+        HOST_PREP_S[0] += time.perf_counter() - t0
+        pts = ck.encoder.encode_double_vector_batch(ck.ctx, diags, ck.scale, chain_index=ct.chain_index())
+    else:                   # the same rows built and encoded on the GPU (limb-identical)
+        pts = ck.encoder.encode_matrix_diagonals(ck.ctx, M, G, ck.scale, chain_index=ct.chain_index())
     return ph.bsgs_multiply_accumulate(ck.ctx, baby, pts, G, B, D, ck.gk)
 
 
@@ -203,7 +207,10 @@ def main():
     ap.add_argument("--F", type=int, default=4096)
     ap.add_argument("--blocks", type=int, default=2)
     ap.add_argument("--bootstrap", action="store_true")
+    ap.add_argument("--host-diagonals", action="store_true",
+                    help="numpy diagonal prep as the reference caller does (default: pyPhantom encode_matrix_diagonals)")
     a = ap.parse_args()
+    HOST_DIAGONALS[0] = a.host_diagonals
     import pyPhantom as ph
     rng = np.random.default_rng(42)
     if a.bootstrap:

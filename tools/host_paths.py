@@ -6,6 +6,8 @@
   encode     float64 rolled diagonals (D x slots, from the host) encoded on the GPU per matvec, as
              test_fully_enc_bsgs.py does (tf:48, 76 via bg:382) -- the caller's numpy roll/tile is
              not included
+  matrix     the D x D matrix itself uploaded (D^2 doubles) and its rolled, tiled diagonals built and
+             encoded on the GPU (pyPhantom encode_matrix_diagonals, an extension): no caller numpy
 
     python tools/host_paths.py [--N 16384 --L0 36 --P 3 --D 2048 --reps 3]
 """
@@ -68,8 +70,11 @@ def main():
     t_cpu = timed(lambda: ph.bsgs_from_cpu(ctx, baby(), *host, G, B, D, gk))
     t_enc = timed(lambda: ph.bsgs_multiply_accumulate(
         ctx, baby(), enc.encode_double_vector_batch(ctx, diag_f64, scale, chain_index=level), G, B, D, gk))
+    W = rng.normal(0, 0.02, (D, D))
+    t_mat = timed(lambda: ph.bsgs_multiply_accumulate(
+        ctx, baby(), enc.encode_matrix_diagonals(ctx, W, G, scale, chain_index=level), G, B, D, gk))
     print(f"N={N} L0={a.L0} P={a.P} D={D}: diagonals {nbytes / 1e9:.2f} GB (offload once: {t_off:.2f} s)")
-    for name, t in (("resident", t_res), ("from_cpu", t_cpu), ("encode", t_enc)):
+    for name, t in (("resident", t_res), ("from_cpu", t_cpu), ("encode", t_enc), ("matrix", t_mat)):
         extra = f", {nbytes / (t - t_res) / 1e9:.1f} GB/s host->device beyond resident" if name == "from_cpu" else ""
         print(f"  {name:9s} {1e3 * t:8.2f} ms/matvec  {1.0 / t:7.2f} matvec/s{extra}", flush=True)
 

@@ -179,11 +179,16 @@ class Server:
 
     # bg:361-432
     def encode_real(self, M, rows=None):
+        if rows is None:   # rows built on the GPU from M (limb-identical to the numpy rows below)
+            return self.encoder.encode_matrix_diagonals(self.ctx, M, self.G, self.diag_scale, chain_index=self.level)
         d = _diag_rows(M, self.D, self.G, self.slots)
         return self.encoder.encode_double_vector_batch(self.ctx, d if rows is None else d[rows], self.diag_scale,
                                                        chain_index=self.level)
 
     def encode_complex(self, M1, M2, rows=None):
+        if rows is None:
+            return self.encoder.encode_matrix_diagonals(self.ctx, M1, self.G, self.diag_scale, chain_index=self.level,
+                                                        M2=M2)
         z = _diag_rows(M1, self.D, self.G, self.slots) + 1j * _diag_rows(M2, self.D, self.G, self.slots)
         return self.encoder.encode_complex_vector_batch(self.ctx, z if rows is None else z[rows], self.diag_scale,
                                                         chain_index=self.level)
