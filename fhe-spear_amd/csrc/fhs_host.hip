@@ -247,6 +247,7 @@ struct fhs_context {
     std::set<const void*> pending_refs;   // inputs and outputs of queued rotations (destroy must flush)
     std::set<const void*> pending_outs;   // outputs of queued rotations (a consumer must flush)
     std::vector<std::complex<double>> fft_w;   // exp(2 pi i k / N), k < N
+    std::vector<std::complex<double>> dec_twist;   // (cos, sin)(pi k / N), k < N
     std::vector<uint64_t> slot_index;          // (5^j mod 2N - 1)/2, j < N/2
     std::atomic<uint64_t> bytes_live{0};
     // lifetime: the caller's reference + one per live object (ciphertext, plaintext, key), so objects
@@ -756,6 +757,9 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     // encoder tables
     c->fft_w.resize(N);
     for (uint64_t k = 0; k < N; ++k) c->fft_w[k] = std::polar(1.0, 2.0 * M_PI * (double)k / (double)N);
+    c->dec_twist.resize(N);
+    for (uint64_t k = 0; k < N; ++k)
+        c->dec_twist[k] = {std::cos(M_PI * (double)k / (double)N), std::sin(M_PI * (double)k / (double)N)};
     c->slot_index.resize(N / 2);
     uint64_t e5 = 1;
     for (uint64_t j = 0; j < N / 2; ++j) {
@@ -1143,22 +1147,29 @@ extern "C" fhs_status fhs_ciphertext_device_ptr(const fhs_ciphertext* ct, void**
 // ============================================================================ encoder
 // slots z_j sit at the evaluation point zeta^(5^j); encode solves m(zeta^(5^j)) = scale z_j with
 // a length-N complex DFT over the odd exponents (pb:141-149).
+// Forward N-point complex FFT for decode (the only user): iterative radix-2, products written out
+// as (ac - bd, ad + bc) so no __muldc3 call (std::complex's NaN-recovering multiply) is made.
 static void fft_inplace(std::vector<std::complex<double>>& a, const std::vector<std::complex<double>>& w, int logN,
-                        bool inverse) {
+                        size_t wstride = 1) {
     const size_t n = a.size();
     for (size_t i = 0; i < n; ++i) {
         const size_t r = h_bitrev((uint32_t)i, logN);
         if (r > i) std::swap(a[i], a[r]);
     }
+    double* x = reinterpret_cast<double*>(a.data());
+    const double* wt = reinterpret_cast<const double*>(w.data());
     for (size_t len = 2; len <= n; len <<= 1) {
-        const size_t step = n / len;
+        const size_t step = n / len * wstride, h = len / 2;
         for (size_t i = 0; i < n; i += len) {
-            for (size_t k = 0; k < len / 2; ++k) {
-                std::complex<double> wk = w[k * step];
-                if (inverse) wk = std::conj(wk);
-                const std::complex<double> u = a[i + k], v = a[i + k + len / 2] * wk;
-                a[i + k] = u + v;
-                a[i + k + len / 2] = u - v;
+            for (size_t k = 0; k < h; ++k) {
+                const double wr = wt[2 * k * step], wi = wt[2 * k * step + 1];
+                double* u = x + 2 * (i + k);
+                double* v = x + 2 * (i + k + h);
+                const double vr = v[0] * wr - v[1] * wi, vi = v[0] * wi + v[1] * wr;
+                v[0] = u[0] - vr;
+                v[1] = u[1] - vi;
+                u[0] += vr;
+                u[1] += vi;
             }
         }
     }
@@ -1406,10 +1417,12 @@ static void crt_compose(const fhs_context* c, const std::vector<uint64_t>& limbs
         }
         ihat[i] = h_inv(hm, c->q[i]);
     }
+    std::vector<uint64_t> ihat_s(l);
+    for (int i = 0; i < l; ++i) ihat_s[i] = (uint64_t)(((hu128)ihat[i] << 64) / c->q[i]);
     std::vector<uint64_t> halfQ(W);
     for (int w = 0; w < W; ++w) halfQ[w] = (Q[w] >> 1) | (w + 1 < W ? Q[w + 1] << 63 : 0);
     out.assign(N, 0.0);
-    const unsigned nth = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 32));
+    const unsigned nth = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), l <= 6 ? 8 : 32));
     std::vector<std::thread> th;
     for (unsigned tix = 0; tix < nth; ++tix)
         th.emplace_back([&, tix]() {
@@ -1417,7 +1430,11 @@ static void crt_compose(const fhs_context* c, const std::vector<uint64_t>& limbs
             for (size_t n = tix; n < N; n += nth) {
                 std::fill(x.begin(), x.end(), 0);
                 for (int i = 0; i < l; ++i) {
-                    const uint64_t y = h_mulmod(limbs[(size_t)i * N + n], ihat[i], c->q[i]);
+                    // y = limb * ihat mod q by Shoup (ihat_s = floor(ihat 2^64 / q)); limbs are < q
+                    const uint64_t a = limbs[(size_t)i * N + n], qi = c->q[i];
+                    const uint64_t qh = (uint64_t)(((hu128)a * ihat_s[i]) >> 64);
+                    uint64_t y = a * ihat[i] - qh * qi;
+                    if (y >= qi) y -= qi;
                     hu128 carry = 0;
                     const uint64_t* h = &hat[(size_t)i * W];
                     for (int w = 0; w < W; ++w) {
@@ -1464,29 +1481,72 @@ static void crt_compose(const fhs_context* c, const std::vector<uint64_t>& limbs
     for (auto& t : th) t.join();
 }
 
+// Coefficients of a decrypted plaintext are |x| = |m| scale + noise, far below Q/2: the centred
+// CRT over the first k limbs (prod q_i >= scale 2^72) is the same integer as over all l, hence the
+// same double.  k+1 limbs are composed as a check; a disagreement (|x| beyond the first k limbs'
+// range) falls back to all l limbs, so the result equals the full composition in every case.
+static int decode_limbs(const fhs_context* c, double scale, int l) {
+    double bits = 0, need = std::log2(std::max(scale, 1.0)) + 72.0;
+    for (int i = 0; i < l; ++i) {
+        bits += std::log2((double)c->q[i]);
+        if (bits >= need) return i + 1;
+    }
+    return l;
+}
+static fhs_status decode_coeffs(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<uint64_t>& host) {
+    const size_t N = c->N, bytes = 8ull * k * N;
+    uint64_t* tmp = nullptr;
+    HIPCHK(dalloc(c, &tmp, bytes), "decode");
+    HIPCHK(hipMemcpyAsync(tmp, pt->d, bytes, hipMemcpyDeviceToDevice, c->st), "decode");
+    HIPCHK(fhs::launch_ntt_inv(c->T, tmp, k, k, 1, 0, c->st), "decode");
+    host.resize((size_t)k * N);
+    HIPCHK(hipMemcpyAsync(host.data(), tmp, bytes, hipMemcpyDeviceToHost, c->st), "decode");
+    HIPCHK(hipStreamSynchronize(c->st), "decode");
+    dfree(c, tmp, bytes);
+    return FHS_OK;
+}
 extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double* re_im) {
     ENTER(c);
     if (!pt || !re_im) return fail(FHS_ERR_INVALID, "decode: null argument");
     const size_t N = c->N;
     const int l = pt->l;
-    uint64_t* tmp = nullptr;
-    HIPCHK(dalloc(c, &tmp, pt_bytes(pt)), "decode");
-    HIPCHK(hipMemcpyAsync(tmp, pt->d, pt_bytes(pt), hipMemcpyDeviceToDevice, c->st), "decode");
-    HIPCHK(fhs::launch_ntt_inv(c->T, tmp, l, l, 1, 0, c->st), "decode");
-    std::vector<uint64_t> host((size_t)l * N);
-    HIPCHK(hipMemcpyAsync(host.data(), tmp, pt_bytes(pt), hipMemcpyDeviceToHost, c->st), "decode");
-    HIPCHK(hipStreamSynchronize(c->st), "decode");
-    dfree(c, tmp, pt_bytes(pt));
+    static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;   // A/B and test knob
+    const int k = full ? l : decode_limbs(c, pt->scale, l), kk = std::min(l, k + 1);
+    HostTrace ht;
+    std::vector<uint64_t> host;
+    fhs_status s = decode_coeffs(c, pt, kk, host);
+    if (s != FHS_OK) return s;
+    ht.mark("decode: intt + copy");
     std::vector<double> m;
-    crt_compose(c, host, l, m);
-    std::vector<std::complex<double>> v(N);
-    for (size_t k = 0; k < N; ++k) v[k] = std::polar(m[k] / pt->scale, M_PI * (double)k / (double)N);
-    fft_inplace(v, c->fft_w, c->logN, false);
-    for (size_t j = 0; j < N / 2; ++j) {
-        const std::complex<double> z = v[c->slot_index[j]];
+    crt_compose(c, host, kk, m);
+    if (k < kk) {   // |x| < Q_k / 4 (first k limbs) makes the k-limb and kk-limb compositions equal
+        double qk = 1.0;
+        for (int i = 0; i < k; ++i) qk *= (double)c->q[i];
+        double mx = 0;
+        for (size_t i = 0; i < N; ++i) mx = std::max(mx, std::fabs(m[i]));
+        if (!(mx < 0.25 * qk) && kk < l) {   // |x| too large for the shortcut: all l limbs
+            s = decode_coeffs(c, pt, l, host);
+            if (s != FHS_OK) return s;
+            crt_compose(c, host, l, m);
+        }
+    }
+    ht.mark("decode: crt");
+    // slots z_j = m(zeta^(5^j)) = sum_{k < N/2} (m_k + i m_{k+N/2}) zeta^k omega^(s_j k), omega = zeta^4,
+    // 5^j = 4 s_j + 1: an N/2-point FFT of the twisted half-pairs, read at s_j = slot_index[j] / 2
+    const size_t n = N / 2;
+    std::vector<std::complex<double>> v(n);
+    for (size_t k2 = 0; k2 < n; ++k2) {
+        const double a = m[k2] / pt->scale, b = m[k2 + n] / pt->scale;
+        const double cr = c->dec_twist[k2].real(), ci = c->dec_twist[k2].imag();
+        v[k2] = {a * cr - b * ci, a * ci + b * cr};
+    }
+    fft_inplace(v, c->fft_w, c->logN - 1, 2);
+    for (size_t j = 0; j < n; ++j) {
+        const std::complex<double> z = v[c->slot_index[j] >> 1];
         re_im[2 * j] = z.real();
         re_im[2 * j + 1] = z.imag();
     }
+    ht.mark("decode: fft");
     return FHS_OK;
 }
 

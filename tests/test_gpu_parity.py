@@ -10,6 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
+REPO = Path(__file__).resolve().parents[1]
 
 
 @pytest.fixture(scope="module")
@@ -326,6 +327,55 @@ def test_fused_bsgs_equals_loop_at_baseline_configs(ph, N, L0, P, D):
     ref = W @ x
     assert np.corrcoef(dec, ref)[0, 1] > 0.999999
     assert np.max(np.abs(dec - ref)) < 1e-8
+
+
+_DECODE_SCRIPT = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[2])
+import pyPhantom as ph
+N, L0, P = 4096, 12, 3
+parms = ph.params(ph.scheme_type.ckks)
+parms.set_poly_modulus_degree(N); parms.set_special_modulus_size(P)
+parms.set_galois_elts(ph.get_elts_from_steps([1], N))
+parms.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * (L0 + P)))
+ctx = ph.context(parms); sk = ph.secret_key(ctx, seed=4); enc = ph.ckks_encoder(ctx)
+rng = np.random.default_rng(6)
+x = rng.normal(0, 1, N // 2)
+pt = enc.encode_double_vector(ctx, x, 2.0 ** 40)
+ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, x, 2.0 ** 59))
+prod = ph.multiply(ctx, ct, ct)                       # scale 2^118, 3 components
+rk = sk.gen_relinkey(ctx)
+sq = ph.relinearize(ctx, prod, rk)
+q = [int(v) for v in ph.create_coeff_modulus(N, [59] * (L0 + P))][:L0]
+junk = ph.plaintext_from_numpy(ctx, np.stack([rng.integers(0, q[i], N, dtype=np.uint64) for i in range(L0)]), 1, 2.0 ** 40)
+out = [np.array(enc.decode_complex_vector(ctx, p)) for p in (pt, sk.decrypt(ctx, ct), sk.decrypt(ctx, sq), junk)]
+np.save(sys.argv[1], np.stack(out))
+'''
+
+
+def test_decode_shortcut_equals_full_crt(require_gpu, tmp_path):
+    """fhs_decode composes the centred CRT from the first k limbs (+1 as a check, full fallback);
+    its output must be bitwise identical to composing all limbs (FHESPEAR_DECODE_FULL=1): a
+    plaintext at 2^40, a fresh decryption at 2^59, a squared one at 2^118 and uniformly random limbs
+    (|x| ~ Q/2, which takes the fallback)."""
+    import os
+    import subprocess
+    import sys as _sys
+    script = tmp_path / "dec.py"
+    script.write_text(_DECODE_SCRIPT)
+    pyp = str(REPO / "fhe-spear_amd" / "python")
+    outs = []
+    for full in (False, True):
+        env = dict(os.environ)
+        env.pop("FHESPEAR_DECODE_FULL", None)
+        if full:
+            env["FHESPEAR_DECODE_FULL"] = "1"
+        f = tmp_path / f"dec_{int(full)}.npy"
+        r = subprocess.run([_sys.executable, str(script), str(f), pyp], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
 
 
 def _bg_rows(W, D, G, slots):
