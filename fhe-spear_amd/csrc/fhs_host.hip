@@ -1238,11 +1238,12 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
 // bg:361-432 on the device -- upload the D x D matrix once (D^2 doubles instead of D x slots),
 // gather the rolled, tiled diagonal rows in HBM, encode them.  Values identical to
 // encode_*_vector_batch on the host-prepared rows, hence identical limbs.
-extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, const double* M2, int D, int G,
-                                           double scale, int ci, fhs_plaintext** out) {
+extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, const double* M2, int64_t ld, int trans,
+                                              int D, int G, double scale, int ci, fhs_plaintext** out) {
     ENTER(c);
     if (!M1 || !out) return fail(FHS_ERR_INVALID, "encode_diagonals: null argument");
     if (D < 1 || G < 1 || G > D) return fail(FHS_ERR_INVALID, "encode_diagonals: need 1 <= G <= D");
+    if (ld < D) return fail(FHS_ERR_INVALID, "encode_diagonals: leading dimension below D");
     const size_t n = c->N / 2;
     if ((size_t)D > n) return fail(FHS_ERR_INVALID, "encode_diagonals: dimension larger than the slot count");
     fhs_status st = encode_checks(c, n, scale, ci);
@@ -1251,8 +1252,10 @@ extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, con
     const size_t mb = 8ull * D * D, stride = is_real ? n : 2 * n;
     uint64_t *dm = nullptr, *dvals = nullptr;
     HIPCHK(dalloc(c, &dm, mb * (is_real ? 1 : 2)), "encode_diagonals matrix");
-    hipError_t e = hipMemcpyAsync(dm, M1, mb, hipMemcpyHostToDevice, c->st);
-    if (e == hipSuccess && !is_real) e = hipMemcpyAsync((char*)dm + mb, M2, mb, hipMemcpyHostToDevice, c->st);
+    // D rows of D doubles, `ld` apart on the host, packed on the device (no host-side copy of a view)
+    hipError_t e = hipMemcpy2DAsync(dm, 8ull * D, M1, 8ull * ld, 8ull * D, D, hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess && !is_real)
+        e = hipMemcpy2DAsync((char*)dm + mb, 8ull * D, M2, 8ull * ld, 8ull * D, D, hipMemcpyHostToDevice, c->st);
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // caller's buffers may be reused on return
     const size_t chunk = 2048;
     for (size_t base = 0; e == hipSuccess && st == FHS_OK && base < (size_t)D; base += chunk) {
@@ -1261,7 +1264,8 @@ extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, con
         if (e != hipSuccess) break;
         const double* m1 = reinterpret_cast<const double*>(dm);
         const double* m2 = is_real ? nullptr : reinterpret_cast<const double*>((char*)dm + mb);
-        e = fhs::launch_diag_gather(m1, m2, D, G, (int)n, (int)base, (int)cnt, reinterpret_cast<double*>(dvals), c->st);
+        e = fhs::launch_diag_gather(m1, m2, D, G, (int)n, (int)base, (int)cnt, trans ? 1 : 0,
+                                    reinterpret_cast<double*>(dvals), c->st);
         if (e == hipSuccess)
             st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci, out + base);
         dfree(c, dvals, 8 * cnt * stride);
@@ -1269,6 +1273,10 @@ extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, con
     dfree(c, dm, mb * (is_real ? 1 : 2));
     if (e != hipSuccess) return hip_fail(e, "encode_diagonals");
     return st;
+}
+extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, const double* M2, int D, int G,
+                                           double scale, int ci, fhs_plaintext** out) {
+    return fhs_encode_diagonals_ex(c, M1, M2, D, 0, D, G, scale, ci, out);
 }
 
 // Extended-precision encoder for constant plaintexts (bootstrapping transforms): the f64 FFT of

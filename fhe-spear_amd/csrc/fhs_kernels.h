@@ -102,8 +102,8 @@ hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int l
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
                                   const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st);
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);
-hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, double* out,
-                              hipStream_t st);
+hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, int trans,
+                              double* out, hipStream_t st);
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st);
 hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st);
 

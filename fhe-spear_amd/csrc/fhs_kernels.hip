@@ -1618,7 +1618,7 @@ hipError_t launch_encode(const DevTables& T, const double* vals, int count, size
 // (np.roll of group g's rows by g G, then np.tile / the remainder columns -- both are j mod D).
 // Complex (M2 != null): re = M1, im = M2, interleaved as the complex encoder reads them.
 __global__ void k_diag_gather(const double* __restrict__ M1, const double* __restrict__ M2, int D, int G, int n,
-                              int k0, int rows, double* __restrict__ out) {
+                              int k0, int rows, int trans, double* __restrict__ out) {
     const size_t total = (size_t)rows * n;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
          idx += (size_t)gridDim.x * blockDim.x) {
@@ -1628,7 +1628,7 @@ __global__ void k_diag_gather(const double* __restrict__ M1, const double* __res
         if (m < 0) m += D;
         int col = m + k % D;
         if (col >= D) col -= D;
-        const size_t src = (size_t)m * D + col;
+        const size_t src = trans ? (size_t)col * D + m : (size_t)m * D + col;   // trans: M^T stored
         if (M2) {
             out[2 * idx] = M1[src];
             out[2 * idx + 1] = M2[src];
@@ -1637,11 +1637,11 @@ __global__ void k_diag_gather(const double* __restrict__ M1, const double* __res
         }
     }
 }
-hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, double* out,
-                              hipStream_t st) {
+hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, int trans,
+                              double* out, hipStream_t st) {
     if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_diag_gather, dim3(eltwise_grid((size_t)rows * n)), dim3(256), 0, st, M1, M2, D, G, n, k0,
-                       rows, out);
+                       rows, trans, out);
     return hipGetLastError();
 }
 

@@ -125,6 +125,8 @@ _SIGS = {
     "fhs_bootstrap_evalmod": (C.c_int, [_vp, _vp, _vp, _dblp, _dblp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     "fhs_encode_precise": (C.c_int, [_vp, _dblp, C.c_size_t, C.c_size_t, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_encode_diagonals": (C.c_int, [_vp, _dblp, _dblp, C.c_int, C.c_int, C.c_double, C.c_int, C.POINTER(_vp)]),
+    "fhs_encode_diagonals_ex": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int,
+                                          C.POINTER(_vp)]),
     "fhs_host_alloc": (C.c_int, [_u64, C.POINTER(_vp)]),
     "fhs_host_free": (C.c_int, [_vp]),
     "fhs_random_plaintexts": (C.c_int, [_vp, _u64, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
@@ -553,18 +555,29 @@ class ckks_encoder:
         diagonals of the D x D matrix M (complex-packed with M2: bg:394-432), giant group g rolled by
         g G, tiled to the slots, encoded -- on the GPU from the matrix itself.  Limb-identical to
         encode_double_vector_batch / encode_complex_vector_batch of the numpy-prepared rows."""
-        A = np.ascontiguousarray(M, dtype=np.float64)
-        if A.ndim != 2 or A.shape[0] != A.shape[1]:
-            raise ValueError("encode_matrix_diagonals: M must be square")
-        B2 = None
-        if M2 is not None:
-            B2 = np.ascontiguousarray(M2, dtype=np.float64)
-            if B2.shape != A.shape:
-                raise ValueError("encode_matrix_diagonals: M and M2 differ in shape")
+        def view(X):   # (pointer, leading dimension, transposed) of a float64 2-D view, copying only if needed
+            X = np.asarray(X)
+            if X.dtype != np.float64:
+                X = X.astype(np.float64)
+            if X.ndim != 2 or X.shape[0] != X.shape[1]:
+                raise ValueError("encode_matrix_diagonals: M must be square")
+            s0, s1 = X.strides
+            if s1 == 8 and s0 >= 8 * X.shape[1] and s0 % 8 == 0:
+                return X, s0 // 8, 0
+            if s0 == 8 and s1 >= 8 * X.shape[0] and s1 % 8 == 0:   # e.g. W[:, lo:hi].T
+                return X, s1 // 8, 1
+            X = np.ascontiguousarray(X)
+            return X, X.shape[1], 0
+        A, lda, ta = view(M)
+        B2, ldb, tb = view(M2) if M2 is not None else (None, lda, ta)
+        if B2 is not None and (B2.shape != A.shape or (ldb, tb) != (lda, ta)):
+            A, B2 = np.ascontiguousarray(A), np.ascontiguousarray(B2)
+            lda, ta = A.shape[1], 0
         D = A.shape[0]
         hs = (_vp * D)()
-        _check(_lib.fhs_encode_diagonals(ctx._h, A.ctypes.data_as(_dblp), None if B2 is None else B2.ctypes.data_as(_dblp),
-                                         D, int(G), float(scale), int(chain_index), hs), "encode_matrix_diagonals")
+        _check(_lib.fhs_encode_diagonals_ex(ctx._h, _vp(A.ctypes.data), None if B2 is None else _vp(B2.ctypes.data),
+                                            int(lda), int(ta), D, int(G), float(scale), int(chain_index), hs),
+               "encode_matrix_diagonals")
         return [plaintext(ctx, _vp(hs[i])) for i in range(D)]
 
     def _decode(self, ctx, pt):

@@ -181,6 +181,10 @@ fhs_status fhs_linear_transform(fhs_context* ctx, const fhs_ciphertext* const* b
  * of the host-prepared rows; uploads D^2 doubles instead of D x N/2.  out_array: D plaintexts. */
 fhs_status fhs_encode_diagonals(fhs_context* ctx, const double* M1, const double* M2, int D, int G, double scale,
                                 int chain_index, fhs_plaintext** out_array);
+/* the same for a strided or transposed view: row r of the D x D block starts at A + r * ld (ld >= D);
+ * trans = 1 means the block holds M^T (M[m][c] = A[c * ld + m]), e.g. numpy's W[:, lo:hi].T */
+fhs_status fhs_encode_diagonals_ex(fhs_context* ctx, const double* A1, const double* A2, int64_t ld, int trans, int D,
+                                   int G, double scale, int chain_index, fhs_plaintext** out_array);
 /* encode_complex_vector_batch with an extended-precision (long double) canonical-embedding FFT on the
  * host and exact 128-bit rounding: for constant plaintexts whose f64 encoding error (~2^-52 log n
  * relative) matters -- the bootstrap's CoeffToSlot / SlotToCoeff diagonals.  |values x scale| < 2^126. */

@@ -411,6 +411,14 @@ def test_encode_matrix_diagonals_equals_host_rows(ph, N, D):
                                             2.0 ** 59, chain_index=2)
     for k in (0, G, D - 1):
         assert np.array_equal(gotc[k].to_numpy(), wantc[k].to_numpy()), f"complex diagonal {k}"
+    # strided and transposed numpy views are read in place (fhs_encode_diagonals_ex)
+    big = rng.normal(0, 0.02, (D, 2 * D + 3))
+    for view in (big[:, 3:3 + D], big[:, 3:3 + D].T):
+        gv = enc.encode_matrix_diagonals(ctx, view, G, 2.0 ** 59, chain_index=2)
+        wv = enc.encode_double_vector_batch(ctx, _bg_rows(np.ascontiguousarray(view), D, G, slots), 2.0 ** 59,
+                                            chain_index=2)
+        for k in (0, G, D - 1):
+            assert np.array_equal(gv[k].to_numpy(), wv[k].to_numpy()), f"view diagonal {k}"
 
 
 def test_bsgs_matches_oracle_on_cfg2_ring(ph):

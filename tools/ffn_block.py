@@ -120,8 +120,11 @@ def ffn_block(ck, ct_x, W_key, W_val, D, F):
     keys = []
     for c in range(chunks):
         lo, hi = c * D, min(c * D + D, F)
-        M = np.zeros((D, D))
-        M[:hi - lo, :] = W_key[:, lo:hi].T
+        if hi - lo == D and not HOST_DIAGONALS[0]:
+            M = W_key[:, lo:hi].T          # a view: the GPU encoder reads it strided, no host copy
+        else:
+            M = np.zeros((D, D))
+            M[:hi - lo, :] = W_key[:, lo:hi].T
         keys.append(matmul(ck, ct_x, M, D, baby))
     sq = []
     for k in keys:   # tf:57-61
@@ -130,8 +133,11 @@ def ffn_block(ck, ct_x, W_key, W_val, D, F):
     acc = None
     for c, s in enumerate(sq):   # tf:65-91
         lo, hi = c * D, min(c * D + D, F)
-        M = np.zeros((D, D))
-        M[:, :hi - lo] = W_val[lo:hi, :].T
+        if hi - lo == D and not HOST_DIAGONALS[0]:
+            M = W_val[lo:hi, :].T
+        else:
+            M = np.zeros((D, D))
+            M[:, :hi - lo] = W_val[lo:hi, :].T
         part = matmul(ck, s, M, D, baby_steps(ck, s, G))
         if acc is None:
             acc = part
