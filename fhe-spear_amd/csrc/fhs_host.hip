@@ -1192,9 +1192,16 @@ static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cn
     uint64_t* dptrs = nullptr;
     hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * cnt, &dptrs);
     if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * cnt);
+    // fused reduction + NTT through a scratch of rounded coefficients (FHESPEAR_ENCODE_UNFUSED=1: the
+    // encoder reduces into every limb and the NTT runs in place -- same limbs, A/B and test knob)
+    static const bool unfused = getenv("FHESPEAR_ENCODE_UNFUSED") != nullptr;
+    uint64_t* coef = nullptr;
+    const size_t cbytes = 8 * cnt * c->N;
+    if (e == hipSuccess && !unfused) e = dalloc(c, &coef, cbytes);
     if (e == hipSuccess)
         e = fhs::launch_encode(c->T, dvals, (int)cnt, n, stride, is_real, scale, reinterpret_cast<fhs::u64* const*>(dptrs),
-                               l, c->st);
+                               l, c->st, reinterpret_cast<double*>(coef));
+    if (coef) dfree(c, coef, cbytes);
     return e == hipSuccess ? FHS_OK : hip_fail(e, "encode");
 }
 static fhs_status encode_checks(fhs_context* c, size_t n, double scale, int ci) {

@@ -93,7 +93,8 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
 // CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
 // apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
-                         double scale, u64* const* outs_dev, int l, hipStream_t st);
+                         double scale, u64* const* outs_dev, int l, hipStream_t st,
+                         double* coef_scratch = nullptr);
 hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
 // b_j = e - a_j s + [limb in digit j] (P mod q) s_new  (switching-key component 0 of digit j)
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* b_out, const u64* a, const u64* e_ntt, const u64* s_ntt,

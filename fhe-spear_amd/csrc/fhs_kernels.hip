@@ -1526,11 +1526,17 @@ __device__ __forceinline__ void enc_fft_stages(double2* a, int tid, int TH, int 
     }
 }
 template <int LOGN>
-__device__ __forceinline__ void enc_finish(const DevTables& T, double2 v, int k, double scale, u64* out, int l) {
+__device__ __forceinline__ void enc_finish(const DevTables& T, double2 v, int k, double scale, u64* out, int l,
+                                           double* dout) {
     constexpr int N = 1 << LOGN, H = N / 2;
     const double2 z = reinterpret_cast<const double2*>(T.enc_twist)[k];
     const double lo = round((v.x * z.x - v.y * z.y) * scale);
     const double hi = round((v.x * z.y + v.y * z.x) * scale);
+    if (dout) {   // fused path: the rounded coefficients; k_ntt_fwd_from_dbl reduces them per limb
+        dout[k] = lo;
+        dout[H + k] = hi;
+        return;
+    }
     for (int i = 0; i < l; ++i) {
         out[(size_t)i * N + k] = dbl_mod(T, lo, i);
         out[(size_t)i * N + H + k] = dbl_mod(T, hi, i);
@@ -1539,7 +1545,7 @@ __device__ __forceinline__ void enc_finish(const DevTables& T, double2 v, int k,
 template <int LOGN>
 __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024)
     k_encode(DevTables T, const double* vals, size_t n, size_t stride, int is_real, double scale, u64* const* outs,
-             int l) {
+             int l, double* coef_out) {
     constexpr int N = 1 << LOGN, H = N / 2, LOGH = LOGN - 1;
     constexpr int TH = (N / 16) < 1024 ? (N / 16) : 1024;
     constexpr bool SPLIT = LOGN > 14;   // N = 32768: the H-point FFT as two H/2-point halves + a final stage
@@ -1548,6 +1554,7 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
     const double* src = vals + (size_t)blockIdx.x * stride;
     const double2* W = reinterpret_cast<const double2*>(T.enc_w);
     u64* out = outs[blockIdx.x];
+    double* dout = coef_out ? coef_out + (size_t)blockIdx.x * N : nullptr;
     if constexpr (!SPLIT) {
         for (int j = tid; j < H; j += TH) {
             double2 z = {0.0, 0.0};
@@ -1556,7 +1563,7 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
         }
         __syncthreads();
         enc_fft_stages<LOGN>(a, tid, TH, H, LOGH, W, LOGH);
-        for (int k = tid; k < H; k += TH) enc_finish<LOGN>(T, a[k], k, scale, out, l);
+        for (int k = tid; k < H; k += TH) enc_finish<LOGN>(T, a[k], k, scale, out, l, dout);
     } else {
         // bit-reversed input: slots with rev(s_j) < H/2 form the first half's sub-FFT
         constexpr int HH = H / 2, PER = HH / TH;
@@ -1582,8 +1589,8 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
             const int k = tid + c * TH;
             const double2 x = lo[c], y = a[k], w = W[k];
             const double2 t = {y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x};
-            enc_finish<LOGN>(T, double2{x.x + t.x, x.y + t.y}, k, scale, out, l);
-            enc_finish<LOGN>(T, double2{x.x - t.x, x.y - t.y}, k + HH, scale, out, l);
+            enc_finish<LOGN>(T, double2{x.x + t.x, x.y + t.y}, k, scale, out, l, dout);
+            enc_finish<LOGN>(T, double2{x.x - t.x, x.y - t.y}, k + HH, scale, out, l, dout);
         }
     }
 }
@@ -1600,14 +1607,34 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_ptrs(DevTables 
                                [&](int e, u64 v) { p[e] = v; });
 }
 
+// fused exact reduction + forward NTT: limb blockIdx.x of plaintext blockIdx.y from its rounded
+// double coefficients (the same dbl_mod as enc_finish, so the same residues): the l limbs are
+// written once instead of written, read and rewritten
+template <int LOGN>
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_from_dbl(DevTables T, const double* coef,
+                                                                         u64* const* ptrs, int limbs) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int b = blockIdx.x;
+    const RedU R = redu(PK(T, b));
+    const double* cf = coef + (size_t)blockIdx.y * N;
+    u64* p = ptrs[blockIdx.y] + (size_t)b * N;
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
+                               [&](int e) { return dbl_mod(T, cf[e], b); }, [&](int e, u64 v) { p[e] = v; });
+}
+
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
-                         double scale, u64* const* outs_dev, int l, hipStream_t st) {
+                         double scale, u64* const* outs_dev, int l, hipStream_t st, double* coef_scratch) {
     if (count <= 0) return hipSuccess;
     FHS_DISPATCH_LOGN(T.logN, {
         constexpr int TH = ((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024;
         hipLaunchKernelGGL((k_encode<LOGN>), dim3(count), dim3(TH), 0, st, T, vals, n, stride, is_real ? 1 : 0, scale,
-                           outs_dev, l);
-        hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T, outs_dev, l);
+                           outs_dev, l, coef_scratch);
+        if (coef_scratch)
+            hipLaunchKernelGGL((k_ntt_fwd_from_dbl<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T,
+                               static_cast<const double*>(coef_scratch), outs_dev, l);
+        else
+            hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T, outs_dev, l);
     });
     return hipGetLastError();
 }

@@ -378,6 +378,49 @@ def test_decode_shortcut_equals_full_crt(require_gpu, tmp_path):
     assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
 
 
+_ENCODE_SCRIPT = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[2])
+import pyPhantom as ph
+out = []
+for N, L0 in ((4096, 8), (32768, 3)):
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N); parms.set_special_modulus_size(1)
+    parms.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * (L0 + 1)))
+    ctx = ph.context(parms); enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(N)
+    r = enc.encode_double_vector_batch(ctx, rng.normal(0, 3, (3, N // 2)), 2.0 ** 59, chain_index=1)
+    z = rng.normal(0, 3, (2, N // 2)) + 1j * rng.normal(0, 3, (2, N // 2))
+    c = enc.encode_complex_vector_batch(ctx, z, 2.0 ** 70, chain_index=2)
+    out += [p.to_numpy().ravel() for p in r + c]
+np.save(sys.argv[1], np.concatenate(out))
+'''
+
+
+def test_encode_fused_ntt_equals_unfused(require_gpu, tmp_path):
+    """The encoder's fused exact-reduction + NTT (k_ntt_fwd_from_dbl) gives the same limbs as
+    reducing into every limb and transforming in place (FHESPEAR_ENCODE_UNFUSED=1), at N = 4096 and
+    at N = 32768 (split FFT, half-limb NTT), real and complex, scales 2^59 and 2^70."""
+    import os
+    import subprocess
+    import sys as _sys
+    script = tmp_path / "enc.py"
+    script.write_text(_ENCODE_SCRIPT)
+    pyp = str(REPO / "fhe-spear_amd" / "python")
+    outs = []
+    for unfused in (False, True):
+        env = dict(os.environ)
+        env.pop("FHESPEAR_ENCODE_UNFUSED", None)
+        if unfused:
+            env["FHESPEAR_ENCODE_UNFUSED"] = "1"
+        f = tmp_path / f"enc_{int(unfused)}.npy"
+        r = subprocess.run([_sys.executable, str(script), str(f), pyp], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0], outs[1])
+
+
 def _bg_rows(W, D, G, slots):
     """numpy restatement of bg:198-203 (_extract_diagonals) + bg:361-378 (roll, tile, remainder)"""
     j = np.arange(D)
