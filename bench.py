@@ -111,8 +111,14 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("FHESPEAR_DIST_BACKEND", "nccl") == "gloo":
+            # rehearsal only (several ranks sharing one GPU, host-staged exchange); timings meaningless
+            dist.init_process_group("gloo")
+            local = int(os.environ.get("FHESPEAR_DEVICE", "0"))
+            torch.cuda.set_device(local)
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import pyPhantom as ph
 
@@ -156,7 +162,10 @@ def main():
             # library's stream overwrites it; it finished long before this step's kernels did
             torch.cuda.current_stream().synchronize()
             ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
-            fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
+            if dist.get_backend() == "gloo":
+                fhespear_dist.gather_to_root(dist, gather_buf.cpu(), world, rank)
+            else:
+                fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
         return y
 
     for _ in range(args.warmup):
