@@ -132,7 +132,11 @@ constexpr size_t lds_bytes() { return (size_t)((1 << LOGN) + (1 << LOGN) / 16) *
 // ---- one-limb transforms, full limb in LDS (N <= 16384: 136 KiB) or half a limb (N = 32768):
 // the half form does the global first forward stage / last inverse stage, which pairs e with
 // e + N/2, in registers and transforms each half in LDS (k_modup_h explains the scheme).
-template <int LOGN> constexpr bool ntt_half() { return LOGN > 14; }
+#ifndef FHS_NTT_HALF_MIN
+#define FHS_NTT_HALF_MIN 14   // generic NTT kernels use the half-limb form (two workgroups per CU) from this LOGN
+                              // (A/B at N = 16384: 2048-diagonal encode + matvec 18.64 -> 18.12 ms, bench unchanged)
+#endif
+template <int LOGN> constexpr bool ntt_half() { return LOGN >= FHS_NTT_HALF_MIN; }
 template <int LOGN> constexpr int ntt_threads() { return ntt_half<LOGN>() ? (1 << LOGN) / 32 : (1 << LOGN) / 16; }
 template <int LOGN> constexpr int ntt_lds_words() {
     return ntt_half<LOGN>() ? (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16 : (1 << LOGN) + (1 << LOGN) / 16;
