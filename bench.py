@@ -242,6 +242,10 @@ def main():
                     "bytes_per_launch": ab // max(launches, 1), "ms_per_launch": round(ms / n, 4)}
 
         roof = roofline_of(dom)
+        if dom == "k_modup":
+            roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (SQ counters: ~85% VALU-busy, "
+                            "profiles/r01), so its HBM fraction is low by construction; ntt_valu_roofline "
+                            "prices it against the register-only butterfly ceiling")
         had_roof = roofline_of("k_bsgs_inner")
         mu_ms = (ktimes["k_modup"][0] / args.steps if ktimes["k_modup"][1]
                  else kprof["k_modup"][0] / prof_steps)
