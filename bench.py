@@ -243,7 +243,7 @@ def main():
 
         roof = roofline_of(dom)
         if dom == "k_modup":
-            roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (SQ counters: ~85% VALU-busy, "
+            roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (SQ counters: VALU issue ~75-85% of SIMD cycles, "
                             "profiles/r01), so its HBM fraction is low by construction; ntt_valu_roofline "
                             "prices it against the register-only butterfly ceiling")
         had_roof = roofline_of("k_bsgs_inner")
