@@ -27,6 +27,19 @@ def test_giant_groups_rejects_more_ranks_than_groups():
         fd.giant_groups(4, 8, 0)
 
 
+def test_stage_groups_eight_rank_block_layout():
+    """Latency-mode layout of the RWKV block's stages at 8 GPUs: r/k/v 3+3+2,
+    o 8, each FFN pair 4+4; fewer ranks than projections -> None (dealt instead)."""
+    assert fd.stage_groups(3, 8) == [[0, 1, 2], [3, 4, 5], [6, 7]]
+    assert fd.stage_groups(1, 8) == [list(range(8))]
+    assert fd.stage_groups(2, 8) == [[0, 1, 2, 3], [4, 5, 6, 7]]
+    assert fd.stage_groups(3, 2) is None
+    for n, w in [(3, 4), (2, 5), (1, 1), (3, 3)]:
+        gs = fd.stage_groups(n, w)
+        assert sorted(r for g in gs for r in g) == list(range(w))
+        assert max(map(len, gs)) - min(map(len, gs)) <= 1
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("D", [256, 200])   # 200: short last giant group, padded with zero diagonals
 def test_giant_sharded_bsgs_bit_exact_two_ranks(require_gpu, D):
