@@ -44,7 +44,7 @@ struct KsItem {
 
 // Optional per-kernel event timer (bench.py): rec(ctx, id, begin, stream) is called around launches.
 enum KernelId { KID_BSGS_INNER = 0, KID_MODUP = 1, KID_KS_IP = 2, KID_MODDOWN = 3, KID_KS_INTT = 4, KID_SPECIAL_INTT = 5,
-                KID_GIANT_SUM = 6, KID_GIANT_FINAL = 7, KID_RESCALE = 8, KID_COUNT = 9 };
+                KID_GIANT_SUM = 6, KID_GIANT_FINAL = 7, KID_RESCALE = 8, KID_KS_FUSED = 9, KID_COUNT = 10 };
 struct KTimer {
     void* ctx;
     void (*rec)(void* ctx, int id, int begin, hipStream_t st);

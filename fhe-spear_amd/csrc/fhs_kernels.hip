@@ -13,6 +13,8 @@
 #include "fhs_kernels.h"
 #include "fhs_ntt.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include <algorithm>
@@ -54,6 +56,15 @@
 #endif
 #ifndef FHS_MODUP_RL
 #define FHS_MODUP_RL 4         // radix (log2) of the register passes in k_modup's NTT
+#endif
+#ifndef FHS_FUSED_CH
+#define FHS_FUSED_CH 2         // k_ks_giant_fused: coefficients per conversion chunk
+#endif
+#ifndef FHS_FUSED_RL
+#define FHS_FUSED_RL 3         // k_ks_giant_fused: radix (log2) of the NTT register passes
+#endif
+#ifndef FHS_FUSED_GROUP
+#define FHS_FUSED_GROUP 4      // k_ks_giant_fused: key products scheduled in groups of this many coefficients
 #endif
 #ifndef FHS_NTT_RL
 #define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
@@ -744,13 +755,32 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
     }
 }
 
+// Extra (unused) LDS per k_modup_h workgroup, FHESPEAR_MODUP_PAD bytes (A/B knob, default 0): a pad
+// that caps ModUp at one workgroup per CU leaves LDS and registers for the memory-bound kernels of the
+// other stream (launch_bsgs chunks).
+static int modup_pad() {
+    static const int v = [] {
+        const char* e = getenv("FHESPEAR_MODUP_PAD");
+        return e ? std::max(0, std::min(65536, atoi(e))) : 0;
+    }();
+    return v;
+}
 template <int LOGN>
 static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* acoef, const unsigned char* vcnt,
                          u64* ext, int l, int U, hipStream_t st) {
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     const int mgrid = FHS_MODUP_MAP == 1 ? xcd_grid(E, dn * U) : FHS_MODUP_MAP == 2 ? xcd_grid_m(E, dn * U) : E * dn * U;
-    if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>())
-        hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
+        const int pad = modup_pad();
+        static bool attr = false;
+        if (pad && !attr) {
+            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_modup_h<LOGN>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, pad);
+            attr = true;
+        }
+        hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), pad, st, T, uniq, acoef, vcnt, ext, l,
+                           U);
+    }
     else
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
 }
@@ -848,6 +878,171 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
     const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
     acc[((size_t)0 * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
     acc[((size_t)1 * E + t) * N + n] = shoup(s1, pinv, pinv_s, q);
+}
+
+// Giant steps, ModUp fused with the key inner product: one workgroup per (target limb t, rotation r)
+// runs the dnum digits in turn -- centred conversion of digit j's limbs into limb t, forward NTT in
+// LDS -- and multiplies each result straight into the two key components, so the extended limbs
+// never go to HBM and the key stream overlaps the NTT work.  acc[r][c][t][n] = sum_j
+// ext_j[t][sigma_r(n)] key_j[c][t][n] mod q_t: the same residues k_modup + k_ks_ip produce.
+// The products are Shoup multiplications with the NTT value as the fixed operand (its companion
+// floor(e 2^64 / q) - {0,1} from the Barrett constant: e r1 + hi(e r0)), each < 2q; the sums stay
+// below 2^64 without reduction when 2 dnum q < 2^64 (`lazy`), else they are kept below 2q.
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_giant_fused(DevTables T, const KsItem* items,
+                                                                     const u64* const* uniq, const u64* acoef,
+                                                                     const unsigned char* vcnt, u64* acc, int l, int R) {
+    constexpr int N = 1 << LOGN, TH = N / 16;
+    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
+    const int tid = threadIdx.x;
+    const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    int t, r;
+    if (!xcd_tinner(E, R, t, r)) return;
+    const int pt = t < l ? t : T.L0 + (t - l);
+    const PrimeK& PM = PK(T, pt);
+    const RedU RU = redu(PM);
+    const u64 q = RU.q, q2 = 2 * q, r0 = rfl64(PM.r0), r1 = rfl64(PM.r1);
+    const bool lazy = q < (~0ull) / (2 * (u64)dn);
+    const KsItem it = items[r];
+    const u64* keyb = it.key + (size_t)pt * N;
+    const u64* seeds = it.key + (size_t)T.dnum * K * N;
+    const u64* own = uniq[it.src] + (size_t)t * N;
+    const unsigned qb = 64 - __clzll(q);
+    const u64* tw = T.tw_fwd + (size_t)pt * N * 2;
+    // automorphism: output slot n reads slot galois_src(n); for n = tid + c TH the exponent
+    // 2 rev(n) + 1 splits into a per-thread part and a per-c constant, so each source slot costs a
+    // multiply-add and a bit reversal
+    const u64 m2 = (u64)2 << LOGN;
+    const unsigned rt = __brev((unsigned)tid) >> (32 - LOGN);   // rev(tid) (tid < TH: top 4 bits of rev clear)
+    const u64 ebase = ((2 * (u64)rt + 1) * it.elt) & (m2 - 1);
+    // per-coefficient values are recomputed from `tl`, a copy of tid laundered once per digit, so
+    // the compiler cannot hoist 16 addresses, sources and counters out of the digit loop (that
+    // costs ~80 registers and spills)
+    int tl = tid;
+    u64 eb = ebase;
+    auto src_of = [&](int c) {
+        const u64 e2 = (eb + 2 * (u64)(__brev((unsigned)c) >> 28) * it.elt) & (m2 - 1);
+        return (int)(__brev((unsigned)((e2 - 1) >> 1)) >> (32 - LOGN));
+    };
+    u64 A0[16], A1[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) A0[c] = A1[c] = 0;
+    auto mac = [&](int c, u64 e, int j) {   // e < q
+        const u64 ep = mullo64x(e, r1) + mulhi64x(e, r0);
+        const int n = tl + c * TH;
+        const u64 b = __builtin_nontemporal_load(keyb + (size_t)j * K * N + n);
+        const u64 a = seeded_uniform_x(seeds[j] + seeded_ctr_mix(pt, n), q, qb);
+        const u64 pb = mullo64x(b, e) - mullo64x(mulhi64x(b, ep), q);
+        const u64 pa = mullo64x(a, e) - mullo64x(mulhi64x(a, ep), q);
+        if (lazy) {
+            A0[c] += pb;
+            A1[c] += pa;
+        } else {
+            A0[c] = csub(A0[c] + pb, q2);
+            A1[c] = csub(A1[c] + pa, q2);
+        }
+    };
+#pragma unroll 1
+    for (int j = 0; j < dn; ++j) {
+        tl = tid;
+        eb = ebase;
+        asm volatile("" : "+v"(tl), "+v"(eb));
+        const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
+        if (t >= s0 && t < s1) {   // own limb of digit j: the input limb itself (workgroup-uniform branch)
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                mac(c, own[src_of(c)], j);
+                if ((c & (FHS_FUSED_GROUP - 1)) == FHS_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+            }
+            continue;
+        }
+        const u64* yb = acoef + ((size_t)it.src * l + s0) * N;
+        const u64* hat = T.modup_hat + (((size_t)l * T.dnum + j) * P_) * K + pt;
+        const u64* qv = T.modup_Q + (((size_t)l * T.dnum + j) * K + pt) * 2;
+        const u64 Qm = qv[0], nsQm = qv[1], negQ = Qm ? q - Qm : 0;
+        const unsigned char* vb = vcnt + ((size_t)it.src * dn + j) * N;
+        constexpr int CH = FHS_FUSED_CH;
+#pragma unroll 1
+        for (int ch = 0; ch < 16 / CH; ++ch) {
+            Acc3 a3[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k) a3[k] = Acc3{0, 0, 0};
+#pragma unroll 1
+            for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
+                const Split30 hw = split30(hat[(size_t)w * K]);
+                const u64* yw = yb + (size_t)w * N + tid + ch * CH * TH;
+                u64 y[CH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) y[k] = yw[k * TH];
+#pragma unroll
+                for (int k = 0; k < CH; ++k) acc3_mac(a3[k], split30(y[k]), hw);
+            }
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const int e = tid + (ch * CH + k) * TH;
+                u64 x;
+                if (RU.cpm) {   // - v Q_S folded into L as v (q - Q_S mod q); result in [0, 2q)
+                    const uint32_t v = vb[e];
+                    const u64 vq = mul32w(v, (uint32_t)negQ) + ((u64)(v * (uint32_t)(negQ >> 32)) << 32);
+                    x = acc3_reduce_pm(a3[k].L + vq, a3[k].M, a3[k].H, RU.b, RU.d);
+                } else {
+                    u128 s = {0, 0};
+                    acc3_fold(s, a3[k]);
+                    mac128(s, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
+                    x = submod(reduce128(s.lo, s.hi, RU), nsQm, q);
+                }
+                lds[lds_pad(e)] = x;
+            }
+        }
+        __syncthreads();
+        ntt_fwd_lds<LOGN, FHS_FUSED_RL>(lds, tid, tw, q, RU.lazy);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            mac(c, fwd_canon(lds[lds_pad(src_of(c))], RU), j);
+            if ((c & (FHS_FUSED_GROUP - 1)) == FHS_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        __syncthreads();   // every read of this digit's transform precedes the next digit's writes
+    }
+    u64* o0 = acc + (((size_t)r * 2 + 0) * E + t) * N;
+    u64* o1 = acc + (((size_t)r * 2 + 1) * E + t) * N;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int n = tid + c * TH;
+        u64 a0 = A0[c], a1 = A1[c];
+        if (lazy) {   // < 2 dn q
+            a0 = reduce128(a0, 0, RU);
+            a1 = reduce128(a1, 0, RU);
+        } else {
+            a0 = csub(a0, q);
+            a1 = csub(a1, q);
+        }
+        o0[n] = a0;
+        o1[n] = a1;
+    }
+}
+
+// Giant steps after k_ks_giant_fused, limbs t < l: bpart[c][t][n] = P^-1 sum_r acc[r][c][t][n]
+// + [c == 0] sum_r sigma_r(c0_r)[t][n], written in place into the r = 0 slot (k_ks_ip_sum's output).
+__global__ void __launch_bounds__(256) k_giant_ip_reduce(DevTables T, const KsItem* items, u64* acc, int l, int R) {
+    const int N = T.N, P_ = T.P, E = l + P_;
+    const size_t total = (size_t)2 * l * N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int comp = (int)(idx / ((size_t)l * N));
+        const int t = (int)((idx / N) % l), n = (int)(idx % N);
+        const RedU RD = redu(PK(T, t));
+        const u64 q = RD.q;
+        u64 s = 0, sadd = 0;
+        for (int r = 0; r < R; ++r) {
+            s = addmod(s, acc[(((size_t)r * 2 + comp) * E + t) * N + n], q);
+            if (comp == 0) {
+                const KsItem it = items[r];
+                sadd = addmod(sadd, it.add0[(size_t)t * N + galois_src(n, it.elt, T.logN)], q);
+            }
+        }
+        const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
+        acc[((size_t)comp * E + t) * N + n] = addmod(shoup(s, pinv, pinv_s, q), sadd, q);
+    }
 }
 
 // (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
@@ -1085,8 +1280,8 @@ __device__ __forceinline__ void ld_diag(const u64* p, u64* out) {
         out[0] = __builtin_nontemporal_load(p);
     }
 }
-template <int VEC>
-__global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
+template <int VEC, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
                                                     const u64* const* __restrict__ pts, int G, int g0, int g1, int D,
                                                     int l, u64* __restrict__ inner) {
     extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][W], split-30 packed
@@ -1094,14 +1289,14 @@ __global__ void __launch_bounds__(64 * FHS_INNER_WAVES) k_bsgs_inner(DevTables T
     const int N = T.N;
     const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t S = (size_t)l * N;
-    for (int idx = tid; idx < G * 2 * W; idx += 64 * FHS_INNER_WAVES) {
+    for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
         const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
         sb[idx] = pack30(baby[b][comp * S + (size_t)i * N + n0 + c]);
     }
     __syncthreads();
     const RedU R = redu(PK(T, i));
     const size_t off = (size_t)i * N + n0 + lane * VEC;
-    for (int g = g0 + wave; g < g1; g += FHS_INNER_WAVES) {
+    for (int g = g0 + wave; g < g1; g += WAVES) {
         const int bmax = min(G, D - g * G);
         if (bmax <= 0) continue;
         u128 c0[VEC], c1[VEC];
@@ -1263,16 +1458,79 @@ static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* cons
 // chunk's ModUp overlaps the next chunk's Hadamard and the previous chunk's inner product.  Chunks
 // only reorder independent work: the limbs are identical to the serial schedule.
 size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) { return bsgs_giant_workspace_bytes(T, R, l); }
+
+// Hadamard shape (coefficients per lane, waves per LDS slice): FHESPEAR_INNER="vec,waves" (A/B knob;
+// default FHS_INNER_VEC, FHS_INNER_WAVES).  Fewer waves leave registers for a co-scheduled ModUp.
+struct InnerShape {
+    int vec, waves;
+};
+static InnerShape inner_shape() {
+    static const InnerShape s = [] {
+        InnerShape r{FHS_INNER_VEC, FHS_INNER_WAVES};
+        if (const char* e = getenv("FHESPEAR_INNER")) {
+            int v = 0, w = 0;
+            if (sscanf(e, "%d,%d", &v, &w) == 2 && (v == 1 || v == 2) && (w == 4 || w == 8 || w == 16)) r = {v, w};
+        }
+        return r;
+    }();
+    return s;
+}
+template <int VEC, int WAVES>
+static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, const u64* const* pts, int G, int g0,
+                                 int g1, int D, int l, u64* inner, hipStream_t st) {
+    constexpr int W = 64 * VEC;
+    static bool attr = false;
+    if (!attr) {   // dynamic LDS above 64 KiB must be opted into
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)std::max<size_t>(64 * 2 * W * 8, FHS_INNER_LDS_MIN));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const size_t sh = std::max<size_t>((size_t)G * 2 * W * 8, FHS_INNER_LDS_MIN);
+    hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES>), dim3(T.N / W, l), dim3(64 * WAVES), sh, st, T, baby, pts, G, g0,
+                       g1, D, l, inner);
+    return hipGetLastError();
+}
+static hipError_t launch_inner(const DevTables& T, const u64* const* baby, const u64* const* pts, int G, int g0, int g1,
+                               int D, int l, u64* inner, hipStream_t st) {
+    const InnerShape s = inner_shape();
+#define FHS_INNER_CASE(V, Wv) \
+    if (s.vec == V && s.waves == Wv) return launch_inner_t<V, Wv>(T, baby, pts, G, g0, g1, D, l, inner, st);
+    FHS_INNER_CASE(2, 16) FHS_INNER_CASE(2, 8) FHS_INNER_CASE(2, 4) FHS_INNER_CASE(1, 16) FHS_INNER_CASE(1, 8)
+    FHS_INNER_CASE(1, 4)
+#undef FHS_INNER_CASE
+    return hipErrorInvalidValue;
+}
+
+// Pipelined BSGS (Hadamard + giant steps) on two streams.  The giant rotations are cut into
+// `chunks` groups.  Main stream: INTT + centred ModUp + NTT of chunk c (VALU-bound) as soon as its
+// inner products exist.  Aux stream: Hadamard of chunk c + 1, then the key inner products and the
+// running giant sum of chunk c (memory-bound), so a chunk's ModUp can share the CUs with the next
+// chunk's Hadamard and the previous chunk's key reads.  Chunks only reorder independent work: the
+// limbs are identical to the serial schedule.
+// Giant steps through k_ks_giant_fused (N = 256 .. 16384) when FHESPEAR_GIANT_FUSED=1 (A/B knob).
+// Off by default: limb-identical, but at cfg2 the fused kernel takes 5.05-5.14 ms against 4.0 ms
+// for k_modup_h + k_ks_ip/k_ks_ip_sum of the giant steps (profiles/r02/ab_giant_fused.jsonl): one
+// 1024-thread workgroup per CU with the 32 accumulators per thread left ~60 registers for the NTT
+// (spills), every barrier stalls all 16 waves, and the Shoup products with the on-the-fly companion
+// add ~70 VALU instructions per digit and coefficient to a kernel that is already VALU-bound.
+static bool giant_fused(const DevTables& T) {
+    static const bool on = [] {
+        const char* e = getenv("FHESPEAR_GIANT_FUSED");
+        return e && atoi(e) != 0;
+    }();
+    return on && T.logN >= 8 && T.logN <= 14;
+}
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, const u64* giant_elts, u64* inner, u64* out, u64* ws,
                        size_t ws_bytes,
                        void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm) {
-    constexpr int VEC = FHS_INNER_VEC, W = 64 * VEC;
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
-    if (T.N % W || G > 64 || R > 512) return hipErrorInvalidValue;
+    if (T.N % 128 || G > 64 || R > 512) return hipErrorInvalidValue;
     if (R > 0 && bsgs_giant_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
-    const int C = R > 0 ? std::max(1, std::min(ss.chunks, std::min(R, (ss.nev - 2) / 2))) : 1;
+    const int C = (R > 0 && !giant_fused(T)) ? std::max(1, std::min(ss.chunks, std::min(R, (ss.nev - 2) / 2))) : 1;
     hipStream_t sm = ss.main, sa = ss.aux;
     hipEvent_t ev_start = ss.ev[0], ev_end = ss.ev[1];
     const hipEvent_t* evH = ss.ev + 2;
@@ -1298,34 +1556,27 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
         if (e != hipSuccess) return e;
     }
-    // FHS_INNER_LDS_MIN pads the dynamic LDS so fewer Hadamard workgroups fit a CU and the
-    // VALU-bound ModUp of the previous chunk (other stream) can be co-resident (experiment knob)
-    const size_t sh = std::max<size_t>((size_t)G * 2 * W * 8, FHS_INNER_LDS_MIN);
-    static bool attr = false;
-    if (!attr) {   // dynamic LDS above 64 KiB must be opted into
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)std::max<size_t>(64 * 2 * W * 8, FHS_INNER_LDS_MIN));
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    // Hadamard: either one launch on the main stream, or (split_hadamard) one launch per chunk on
-    // the aux stream (chunk 0 also produces g = 0, which needs no rotation)
-    hipStream_t sh_st = ss.split_hadamard ? sa : sm;
-    if (ss.split_hadamard) {
+    // Hadamard chunk c: giant groups [g0(c), g1(c)) (chunk 0 also produces g = 0, which needs no rotation)
+    const bool split = ss.split_hadamard && R > 0 && C > 1;
+    auto hg0 = [&](int c) { return c == 0 ? 0 : rb(c) + 1; };
+    auto hg1 = [&](int c) { return split ? rb(c + 1) + 1 : B; };
+    auto hadamard = [&](int c, hipStream_t st) -> hipError_t {
+        FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
+        hipError_t e = launch_inner(T, baby_dev, pts_dev, G, hg0(c), hg1(c), D, l, inner, st);
+        FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
+        hipEventRecord(evH[c], st);
+        return e;
+    };
+    hipError_t he = hipSuccess;
+    if (split) {
         hipEventRecord(ev_start, sm);
         hipStreamWaitEvent(sa, ev_start, 0);
-    }
-    for (int c = 0; c < (ss.split_hadamard ? C : 1); ++c) {
-        const int g0 = c == 0 ? 0 : rb(c) + 1, g1 = (R > 0 && ss.split_hadamard) ? rb(c + 1) + 1 : B;
-        FHS_TMARK(tm, KID_BSGS_INNER, 1, sh_st);
-        hipLaunchKernelGGL(k_bsgs_inner<VEC>, dim3(T.N / W, l), dim3(64 * FHS_INNER_WAVES), sh, sh_st, T, baby_dev,
-                           pts_dev, G, g0, g1, D, l, inner);
-        FHS_TMARK(tm, KID_BSGS_INNER, 0, sh_st);
-        hipEventRecord(evH[c], sh_st);
-    }
-    if (!ss.split_hadamard)
+        he = hadamard(0, sa);
+    } else {
+        he = hadamard(0, sm);
         for (int c = 1; c < C; ++c) hipEventRecord(evH[c], sm);
+    }
+    if (he != hipSuccess) return he;
     hipEventRecord(ev_start, sm);
     hipStreamWaitEvent(sa, ev_start, 0);
     if (R <= 0) {
@@ -1335,6 +1586,43 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
     }
     u64* base = ws + keyswitch_workspace_bytes(T, R, R, l) / 8;
     u64* convsum = base + 2 * S;
+    if (giant_fused(T)) {   // serial: INTT + counts, fused ModUp x key, reduce, ModDown sum
+        FHS_DISPATCH_LOGN(T.logN, {
+            if constexpr (LOGN >= 8 && LOGN <= 14) {
+                const KsBufs b = ks_carve(T, ws, R, R, l);
+                const int E = l + T.P, dn = (l + T.P - 1) / T.P;
+                FHS_TMARK(tm, KID_KS_INTT, 1, sm);
+                if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
+                    hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * R), dim3((1 << LOGN) / 32), 0, sm, T, uq, b.acoef, l,
+                                       R);
+                else
+                    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * R), dim3((1 << LOGN) / 16), 0, sm, T, uq, b.acoef, l, R);
+                hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)R * dn * N)), dim3(256), 0, sm, T, b.acoef, b.vcnt,
+                                   l, R);
+                FHS_TMARK(tm, KID_KS_INTT, 0, sm);
+                FHS_TMARK(tm, KID_KS_FUSED, 1, sm);
+                hipLaunchKernelGGL((k_ks_giant_fused<LOGN>), dim3(xcd_grid(E, R)), dim3((1 << LOGN) / 16), 0, sm, T, it, uq,
+                                   b.acoef, b.vcnt, b.acc, l, R);
+                FHS_TMARK(tm, KID_KS_FUSED, 0, sm);
+                FHS_TMARK(tm, KID_KS_IP, 1, sm);
+                hipLaunchKernelGGL(k_giant_ip_reduce, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, it, b.acc, l, R);
+                FHS_TMARK(tm, KID_KS_IP, 0, sm);
+                FHS_TMARK(tm, KID_SPECIAL_INTT, 1, sm);
+                hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, sm, T, b.acc,
+                                   b.ycoef, l, R);
+                FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sm);
+                FHS_TMARK(tm, KID_GIANT_SUM, 1, sm);
+                hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, b.acc, b.ycoef, inner, base,
+                                   convsum, l, R, 1);
+                FHS_TMARK(tm, KID_GIANT_SUM, 0, sm);
+                FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
+                hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum,
+                                   out, l);
+                FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
+            }
+        });
+        return hipGetLastError();
+    }
     FHS_DISPATCH_LOGN(T.logN, {
         const KsBufs all = ks_carve(T, ws, R, R, l);
         // main: INTT + centred ModUp + NTT per chunk, as soon as its inner products exist
@@ -1343,8 +1631,13 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             ks_modup_stage<LOGN>(T, uq + rb(c), rb(c + 1) - rb(c), l, ks_at(T, all, rb(c), rb(c), l), sm, tm);
             hipEventRecord(evF[c], sm);
         }
-        // aux: key inner product, special-limb INTT and the running giant sum per chunk
+        // aux: Hadamard of chunk c + 1, then key inner product, special-limb INTT and the running
+        // giant sum of chunk c
         for (int c = 0; c < C; ++c) {
+            if (split && c + 1 < C) {
+                he = hadamard(c + 1, sa);
+                if (he != hipSuccess) return he;
+            }
             const int Rc = rb(c + 1) - rb(c);
             const KsBufs bc = ks_at(T, all, rb(c), rb(c), l);
             hipStreamWaitEvent(sa, evF[c], 0);

@@ -817,7 +817,8 @@ class Event:
 
 
 KERNEL_IDS = {"k_bsgs_inner": 0, "k_modup": 1, "k_ks_ip": 2, "k_moddown": 3, "k_ks_intt": 4,
-              "k_ks_special_intt": 5, "k_giant_sum": 6, "k_giant_final": 7, "rescale": 8}
+              "k_ks_special_intt": 5, "k_giant_sum": 6, "k_giant_final": 7, "rescale": 8,
+              "k_ks_giant_fused": 9}
 
 
 def kernel_timer_arm(ctx, names=None):

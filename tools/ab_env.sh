@@ -1,9 +1,24 @@
 #!/bin/bash
-# A/B one environment variable on the cfg2 bench (GPU box): tools/ab_env.sh VAR v1 v2 ...
-mkdir -p gpurun_out
-var=$1; shift
-for v in "$@"; do
-  env $var=$v timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/abenv_$v.log 2>&1 || exit 1
-  python -c "
-import json; d=json.loads(open('gpurun_out/abenv_$v.log').read().strip().splitlines()[-1]); print('$var=$v', d['value'], d['ms_per_step'], {k:v['ms_per_step'] for k,v in d['kernels'].items()})"
+# A/B of runtime knobs on the cfg2 bench: tools/ab_env.sh OUT "name VAR=v VAR=v" "name2 ..." ...
+# Each variant is one bench.py run (no CPU baseline) under its own time limit; one JSON summary line
+# per variant is appended to OUT.  Stops at the first failing run.
+out=$1
+shift
+cfg=${AB_CONFIG:-cfg2}
+steps=${AB_STEPS:-10}
+for spec in "$@"; do
+    name=${spec%% *}
+    envs=${spec#"$name"}
+    line=$(env $envs timeout -k 10 300 python3 bench.py --config "$cfg" --steps "$steps" --warmup 3 --no-cpu-baseline) || {
+        echo "variant $name failed (rc $?)" >> "$out"
+        exit 1
+    }
+    python3 - "$name" "$envs" "$line" >> "$out" <<'EOF'
+import json, sys
+name, envs, line = sys.argv[1], sys.argv[2].strip(), sys.argv[3]
+d = json.loads(line.strip().splitlines()[-1])
+k = {n: v["ms_per_step"] for n, v in d.get("kernels", {}).items()}
+print(json.dumps({"variant": name, "env": envs, "value": d["value"], "ms_per_step": d["ms_per_step"], "kernels_ms": k}))
+EOF
+    tail -1 "$out"
 done
