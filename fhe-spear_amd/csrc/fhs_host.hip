@@ -229,6 +229,9 @@ struct PendingRot {
 struct fhs_context {
     int device = 0;
     hipStream_t st = nullptr;
+    // the context's own stream-ordered pool (release threshold infinite: freed blocks stay mapped
+    // for reuse); trimmed on out-of-memory, at destruction (then destroyed) and at process exit
+    hipMemPool_t pool = nullptr;
     hipStream_t st_aux = nullptr;          // second stream of the pipelined BSGS (memory-bound kernels)
     std::vector<hipEvent_t> bsgs_ev;       // cross-stream ordering events of launch_bsgs
     int bsgs_chunks = 1;                   // FHESPEAR_BSGS_CHUNKS (overlap measured slower)
@@ -320,6 +323,25 @@ struct fhs_galois_keys {
 };
 
 static void ctx_retain(fhs_context* c) { c->refs.fetch_add(1); }
+
+// Live contexts, for the out-of-memory path (every pool's unused blocks are released before the
+// retry) and for the process-exit release.  A multi-GB pool still mapped when the HIP runtime's own
+// exit handler ran crashed inside libamdhip64 (round 1, a 13-block d=2048 FFN chain with 135 GB
+// cached): release_at_exit is registered with atexit() right after the first context's stream is
+// created, i.e. after HIP registered its handler, so it runs first (LIFO) and leaves every pool
+// trimmed and the caches empty.
+static std::mutex g_live_mu;
+static std::set<fhs_context*> g_live;
+static void release_pool_blocks(fhs_context* c);
+static void release_at_exit() {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    for (fhs_context* c : g_live) release_pool_blocks(c);
+}
+static void trim_all_pools(fhs_context* self) {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    for (fhs_context* c : g_live)
+        if (c != self && c->pool && c->device == self->device) (void)hipMemPoolTrimTo(c->pool, 0);
+}
 static void ctx_release(fhs_context* c);
 
 // switching key in HBM: b_j [dnum][K][N] then the dnum seeds of the uniform a_j, which the key
@@ -339,6 +361,23 @@ static void trim_cache(fhs_context* c) {
     hipStreamSynchronize(c->st);
     c->free_blocks.clear();
     c->cached_bytes = 0;
+    if (c->pool) (void)hipMemPoolTrimTo(c->pool, 0);
+}
+// exit path: cached blocks back to the pool, the pool's unused memory back to the device
+static void release_pool_blocks(fhs_context* c) {
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    hipStreamSynchronize(c->st);
+    if (c->st_aux) hipStreamSynchronize(c->st_aux);
+    for (auto& kv : c->free_blocks)
+        for (void* p : kv.second) (void)hipFreeAsync(p, c->st);
+    hipStreamSynchronize(c->st);
+    c->free_blocks.clear();
+    c->cached_bytes = 0;
+    if (c->pool) {
+        uint64_t zero = 0;
+        (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &zero);
+        (void)hipMemPoolTrimTo(c->pool, 0);
+    }
 }
 static void evict_cold(fhs_context* c, size_t keep) {
     while (c->cached_bytes > c->cache_cap) {
@@ -371,11 +410,12 @@ static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
         return hipSuccess;
     }
     void* v = nullptr;
-    hipError_t e = hipMallocAsync(&v, bytes, c->st);
-    if (e == hipErrorOutOfMemory && c->cached_bytes) {   // give the cache back and retry once
+    hipError_t e = hipMallocFromPoolAsync(&v, bytes, c->pool, c->st);
+    if (e == hipErrorOutOfMemory) {   // give the caches and every pool's unused blocks back, retry once
         (void)hipGetLastError();
         trim_cache(c);
-        e = hipMallocAsync(&v, bytes, c->st);
+        trim_all_pools(c);
+        e = hipMallocFromPoolAsync(&v, bytes, c->pool, c->st);
     }
     if (e == hipSuccess) {
         *p = (uint64_t*)v;
@@ -554,11 +594,16 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     c->q.assign(primes, primes + nprimes);
     HIPCHK(hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking), "hipStreamCreate");
     {
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-            uint64_t thr = ~0ull;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-        }
+        static std::once_flag exit_once;
+        std::call_once(exit_once, [] { atexit(release_at_exit); });
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = device;
+        HIPCHK(hipMemPoolCreate(&c->pool, &props), "memory pool");
+        uint64_t thr = ~0ull;
+        (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &thr);
         size_t free_b = 0, total_b = 0;
         (void)hipMemGetInfo(&free_b, &total_b);
         c->cache_cap = total_b / 4;
@@ -766,6 +811,10 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
         c->slot_index[j] = (e5 - 1) / 2;
         e5 = (e5 * 5) & (2 * N - 1);
     }
+    {
+        std::lock_guard<std::mutex> lk(g_live_mu);
+        g_live.insert(c.get());
+    }
     *out = c.release();
     return FHS_OK;
 }
@@ -785,14 +834,20 @@ static void ctx_free(fhs_context* c) {
         for (void* p : c->tables) hipFree(p);
         for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
             if (c->scr[k]) hipFree(c->scr[k]);
+        {
+            std::lock_guard<std::mutex> lk(g_live_mu);
+            g_live.erase(c);
+        }
         for (auto& kv : c->free_blocks)
             for (void* p : kv.second) hipFreeAsync(p, c->st);
         hipStreamSynchronize(c->st);
-        // hand the stream-ordered pool's freed blocks back while the stream that freed them still
-        // exists: blocks left in the default pool tied to a destroyed stream crashed the HIP
-        // runtime's own exit handler after multi-GB chains (tools/debug/exit_crash.py)
-        hipMemPool_t pool = nullptr;
-        if (hipDeviceGetDefaultMemPool(&pool, c->device) == hipSuccess && pool) hipMemPoolTrimTo(pool, 0);
+        // every block of the pool is free now (the context outlives all its objects): hand the
+        // memory back and destroy the pool while the stream that freed the blocks still exists
+        if (c->pool) {
+            hipMemPoolTrimTo(c->pool, 0);
+            hipMemPoolDestroy(c->pool);
+            c->pool = nullptr;
+        }
         if (c->ring) hipHostFree(c->ring);
         for (auto& v : c->timer_pairs)
             for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
@@ -1079,6 +1134,29 @@ extern "C" fhs_status fhs_plaintext_destroy(fhs_plaintext* pt) {
     ctx_release(c);
     return FHS_OK;
 }
+// Output array of a batch creator: cleared on entry; if the call fails part-way (e.g. device OOM,
+// which bg:1164-1170 catches to fall back to on-the-fly encoding) the plaintexts already created
+// are destroyed and their slots reset to null, so a failed batch leaves no HBM behind.
+struct BatchOut {
+    fhs_plaintext** outs;
+    size_t n;
+    bool kept = false;
+    BatchOut(fhs_plaintext** o, size_t count) : outs(o), n(o ? count : 0) {
+        for (size_t i = 0; i < n; ++i) outs[i] = nullptr;
+    }
+    fhs_status keep(fhs_status st) {
+        kept = st == FHS_OK;
+        return st;
+    }
+    ~BatchOut() {
+        if (kept) return;
+        for (size_t i = 0; i < n; ++i)
+            if (outs[i]) {
+                fhs_plaintext_destroy(outs[i]);
+                outs[i] = nullptr;
+            }
+    }
+};
 extern "C" fhs_status fhs_ciphertext_info(const fhs_ciphertext* ct, int* ncomp, int* ci, int* l, double* scale) {
     if (!ct) return fail(FHS_ERR_INVALID, "null ciphertext");
     if (ncomp) *ncomp = ct->ncomp;
@@ -1216,6 +1294,7 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
     fhs_status st = encode_checks(c, n, scale, ci);
     if (st != FHS_OK) return st;
     if (count == 0) return FHS_OK;
+    BatchOut bo(outs, count);
     const size_t stride = is_real ? n : 2 * n;
     // values -> HBM (the copy completes before returning: the caller's buffer may be reused), then
     // FFT + exact reduction + NTT on the GPU (k_encode, k_ntt_fwd_ptrs), stream-ordered
@@ -1238,7 +1317,7 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
         if (ht.on) { hipStreamSynchronize(c->st); ht.mark("encode: gpu"); }
         if (s != FHS_OK) return s;
     }
-    return FHS_OK;
+    return bo.keep(FHS_OK);
 }
 
 // Extension (no reference symbol): the whole caller-side diagonal pipeline of bg:198-203 +
@@ -1256,6 +1335,7 @@ extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, 
     fhs_status st = encode_checks(c, n, scale, ci);
     if (st != FHS_OK) return st;
     const bool is_real = M2 == nullptr;
+    BatchOut bo(out, (size_t)D);
     const size_t mb = 8ull * D * D, stride = is_real ? n : 2 * n;
     uint64_t *dm = nullptr, *dvals = nullptr;
     HIPCHK(dalloc(c, &dm, mb * (is_real ? 1 : 2)), "encode_diagonals matrix");
@@ -1279,7 +1359,7 @@ extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, 
     }
     dfree(c, dm, mb * (is_real ? 1 : 2));
     if (e != hipSuccess) return hip_fail(e, "encode_diagonals");
-    return st;
+    return bo.keep(st);
 }
 extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, const double* M2, int D, int G,
                                            double scale, int ci, fhs_plaintext** out) {
@@ -1341,6 +1421,7 @@ extern "C" fhs_status fhs_encode_precise(fhs_context* c, const double* re_im, si
     const int l = c->L0 + 1 - ci;
     if (ci < 1 || l < 1) return fail(FHS_ERR_LEVEL, "encode: chain index out of range");
     if (count == 0) return FHS_OK;
+    BatchOut bo(outs, count);
     const size_t N = c->N;
     std::vector<int64_t> hi(count * N);
     std::vector<uint64_t> lo(count * N);
@@ -1373,7 +1454,7 @@ extern "C" fhs_status fhs_encode_precise(fhs_context* c, const double* re_im, si
                                       reinterpret_cast<fhs::u64* const*>(dptrs), l, c->st);
     dfree(c, dbuf, 16 * count * N);
     if (e != hipSuccess) return hip_fail(e, "encode_precise");
-    return FHS_OK;
+    return bo.keep(FHS_OK);
 }
 
 extern "C" fhs_status fhs_encode(fhs_context* c, const double* re_im, size_t n, double scale, int ci,
@@ -1496,10 +1577,13 @@ static void crt_compose(const fhs_context* c, const std::vector<uint64_t>& limbs
     for (auto& t : th) t.join();
 }
 
-// Coefficients of a decrypted plaintext are |x| = |m| scale + noise, far below Q/2: the centred
-// CRT over the first k limbs (prod q_i >= scale 2^72) is the same integer as over all l, hence the
-// same double.  k+1 limbs are composed as a check; a disagreement (|x| beyond the first k limbs'
-// range) falls back to all l limbs, so the result equals the full composition in every case.
+// Coefficients of a decrypted plaintext are |x| = |m| scale + noise: the centred CRT over the first
+// k limbs (prod q_i >= scale 2^72) is the same integer as over all l, hence the same double, whenever
+// |x| < Q_{k+1} / 2 -- i.e. for every plaintext whose coefficients are below 2^71 scale, the range
+// CKKS decoding is meant for.  k+1 limbs are composed and |x| >= Q_k / 4 falls back to all l limbs,
+// which catches coefficients between Q_k / 4 and Q_{k+1} / 2; a coefficient of |x| >= Q_{k+1} / 2
+// whose residue mod Q_{k+1} happens to be small is NOT detected (it decodes to the aliased value).
+// FHESPEAR_DECODE_FULL=1 always composes all l limbs.
 static int decode_limbs(const fhs_context* c, double scale, int l) {
     double bits = 0, need = std::log2(std::max(scale, 1.0)) + 72.0;
     for (int i = 0; i < l; ++i) {
@@ -2226,15 +2310,16 @@ extern "C" fhs_status fhs_upload_plaintexts(fhs_context* c, const uint64_t* host
                                             fhs_plaintext** outs) {
     ENTER(c);
     if (!host || !outs || count < 1) return fail(FHS_ERR_INVALID, "upload: bad args");
+    BatchOut bo(outs, (size_t)count);
     for (int k = 0; k < count; ++k) {
         fhs_plaintext* pt;
         fhs_status s = new_pt(c, ci, scale, &pt);
         if (s != FHS_OK) return s;
-        HIPCHK(hipMemcpyAsync(pt->d, host + (size_t)k * pt->l * c->N, pt_bytes(pt), hipMemcpyHostToDevice, c->st), "upload");
         outs[k] = pt;
+        HIPCHK(hipMemcpyAsync(pt->d, host + (size_t)k * pt->l * c->N, pt_bytes(pt), hipMemcpyHostToDevice, c->st), "upload");
     }
     HIPCHK(hipStreamSynchronize(c->st), "upload");
-    return FHS_OK;
+    return bo.keep(FHS_OK);
 }
 extern "C" fhs_status fhs_bsgs_from_cpu(fhs_context* c, const fhs_ciphertext* const* baby, int G, const uint64_t* host,
                                         int D, int B, int ci, double scale, const fhs_galois_keys* gk,
@@ -2259,15 +2344,16 @@ extern "C" fhs_status fhs_random_plaintexts(fhs_context* c, uint64_t seed, int c
                                             fhs_plaintext** outs) {
     ENTER(c);
     if (!outs || count < 1) return fail(FHS_ERR_INVALID, "random_plaintexts: bad args");
+    BatchOut bo(outs, (size_t)count);
     for (int k = 0; k < count; ++k) {
         fhs_plaintext* pt;
         fhs_status s = new_pt(c, ci, scale, &pt);
         if (s != FHS_OK) return s;
+        outs[k] = pt;
         HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(seed, (7ull << 56) | (uint64_t)k), pt->d, pt->l, 0,
                                   c->st), "random_plaintexts");
-        outs[k] = pt;
     }
-    return FHS_OK;
+    return bo.keep(FHS_OK);
 }
 extern "C" fhs_status fhs_event_record(fhs_context* c, void** ev) {
     ENTER(c);
@@ -2339,23 +2425,49 @@ extern "C" fhs_status fhs_kernel_timer_arm(fhs_context* c, uint32_t mask) {
     return FHS_OK;
 }
 // device-to-device copy of a ciphertext's limbs into caller memory (RCCL interop); synchronises
-extern "C" fhs_status fhs_ciphertext_copy_to_device(fhs_context* c, const fhs_ciphertext* ct, void* dst) {
-    ENTER(c);
+static fhs_status copy_to_device(fhs_context* c, const fhs_ciphertext* ct, void* dst, bool sync) {
     if (!ct || !dst) return fail(FHS_ERR_INVALID, "null argument");
     HIPCHK(hipMemcpyAsync(dst, ct->d, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st), "copy_to_device");
-    HIPCHK(hipStreamSynchronize(c->st), "copy_to_device");
+    if (sync) HIPCHK(hipStreamSynchronize(c->st), "copy_to_device");
     return FHS_OK;
 }
-extern "C" fhs_status fhs_ciphertext_from_device(fhs_context* c, const void* src, int ncomp, int ci, double scale,
-                                                 fhs_ciphertext** out) {
-    ENTER(c);
+static fhs_status from_device(fhs_context* c, const void* src, int ncomp, int ci, double scale, fhs_ciphertext** out,
+                              bool sync) {
     if (!src || !out) return fail(FHS_ERR_INVALID, "null argument");
     fhs_ciphertext* ct;
     fhs_status s = new_ct(c, ncomp, ci, scale, &ct);
     if (s != FHS_OK) return s;
-    HIPCHK(hipMemcpyAsync(ct->d, src, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st), "from_device");
-    HIPCHK(hipStreamSynchronize(c->st), "from_device");
+    hipError_t e = hipMemcpyAsync(ct->d, src, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st);
+    if (e == hipSuccess && sync) e = hipStreamSynchronize(c->st);
+    if (e != hipSuccess) {
+        fhs_ciphertext_destroy(ct);
+        return hip_fail(e, "from_device");
+    }
     *out = ct;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_ciphertext_copy_to_device(fhs_context* c, const fhs_ciphertext* ct, void* dst) {
+    ENTER(c);
+    return copy_to_device(c, ct, dst, true);
+}
+extern "C" fhs_status fhs_ciphertext_from_device(fhs_context* c, const void* src, int ncomp, int ci, double scale,
+                                                 fhs_ciphertext** out) {
+    ENTER(c);
+    return from_device(c, src, ncomp, ci, scale, out, true);
+}
+extern "C" fhs_status fhs_ciphertext_copy_to_device_async(fhs_context* c, const fhs_ciphertext* ct, void* dst) {
+    ENTER(c);
+    return copy_to_device(c, ct, dst, false);
+}
+extern "C" fhs_status fhs_ciphertext_from_device_async(fhs_context* c, const void* src, int ncomp, int ci, double scale,
+                                                       fhs_ciphertext** out) {
+    ENTER(c);
+    return from_device(c, src, ncomp, ci, scale, out, false);
+}
+extern "C" fhs_status fhs_context_stream(fhs_context* c, void** stream) {
+    ENTER(c);
+    if (!stream) return fail(FHS_ERR_INVALID, "null argument");
+    *stream = (void*)c->st;
     return FHS_OK;
 }
 

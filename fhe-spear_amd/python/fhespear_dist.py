@@ -4,9 +4,10 @@ One process per GPU (torchrun); backend "nccl" = RCCL over xGMI on MI355X, "gloo
 The data path has exactly two exchange steps, both on flat int64 views of ciphertext limbs:
 
   * gather_to_root   -- every rank's output ciphertext(s) to rank 0 (the "client" decrypts there);
-  * broadcast_from   -- one rank's ciphertext limbs to all (baby steps shared by projections with
-                        the same input, e.g. the FFN key pair, bg:563, north_star "computed once and
-                        broadcast").
+  * broadcast_from   -- one rank's ciphertext limbs to all: the stage inputs from the client, and
+                        (BlockRunner baby_mode="broadcast") the G baby steps of an input that several
+                        ranks need, e.g. the FFN key pair, bg:563, north_star "computed once and
+                        broadcast".
 
 Projections are assigned round-robin (projection p -> rank p % world).  The reference runs the
 block's 8 BSGS calls serially in one process (bg:784-892); which of them are independent:
@@ -24,6 +25,8 @@ from __future__ import annotations
 # block stage structure of bg.client_aided_block (bg:784-892): projections per stage
 RWKV_BLOCK_STAGES = (("r", "k", "v"), ("o",), ("ffn_key_0", "ffn_key_1"), ("ffn_val_0", "ffn_val_1"))
 RWKV_BLOCK_PROJECTIONS = tuple(p for st in RWKV_BLOCK_STAGES for p in st)
+# projections of one stage that take the same input ciphertext, hence the same baby steps (bg:563)
+RWKV_SHARED_INPUTS = (("ffn_key_0", "ffn_key_1"),)
 
 
 def owner(p: int, world: int) -> int:
@@ -55,20 +58,82 @@ def broadcast_from(dist, tensor, src: int):
     return tensor
 
 
+def int64_sum_is_exact(world: int, moduli) -> bool:
+    """A plain int64 sum of `world` residues r_i < q stays exact iff world (max q - 1) < 2^63."""
+    return world * (max(int(q) for q in moduli) - 1) < 2 ** 63
+
+
 def modular_reduce_sum(dist, tensor, moduli_per_row, root: int = 0, group=None):
     """Sum of residues across the ranks of `group` (default: all), reduced mod q_i per limb row on
-    the global rank `root` (giant-step sharding, §8e(2)).  RCCL's integer sum is not modular; with
-    <= 15 ranks and 59-bit residues the plain int64 sum stays < 2^63, so one final reduction on the
-    root is exact."""
+    the global rank `root` (giant-step sharding, §8e(2)).  RCCL's integer sum is not modular: when
+    world (max q - 1) < 2^63 (e.g. <= 15 ranks at 59-bit, <= 7 at 60-bit) one int64 reduce and one
+    reduction on the root are exact; otherwise the partials are gathered to the root and added mod q
+    one at a time (every intermediate < 2 q < 2^63)."""
     import torch
-    if dist.get_world_size(group) > 15:
-        raise ValueError("modular_reduce_sum: > 15 ranks could overflow int64 with 59-bit residues")
-    dist.reduce(tensor, dst=root, group=group)
-    if dist.get_rank() == root:
-        q = torch.as_tensor(moduli_per_row, dtype=torch.int64, device=tensor.device).view(-1, 1)
-        t = tensor.view(q.shape[0], -1)
-        t.remainder_(q)
+    world = dist.get_world_size(group)
+    q = torch.as_tensor([int(m) for m in moduli_per_row], dtype=torch.int64, device=tensor.device).view(-1, 1)
+    me = dist.get_rank()
+    if int64_sum_is_exact(world, moduli_per_row):
+        dist.reduce(tensor, dst=root, group=group)
+        if me == root:
+            tensor.view(q.shape[0], -1).remainder_(q)
+        return tensor
+    parts = [torch.empty_like(tensor) for _ in range(world)] if me == root else None
+    dist.gather(tensor, parts, dst=root, group=group)
+    if me == root:
+        acc = tensor.view(q.shape[0], -1)
+        acc.zero_()
+        for p in parts:
+            acc.add_(p.view(q.shape[0], -1))
+            acc.sub_(q * (acc >= q))
     return tensor
+
+
+# ------------------------------------------------------------------ library stream <-> torch stream
+_LIB_STREAMS = {}
+
+
+def lib_stream(ph, ctx):
+    """torch view of the context's HIP stream (every library call is ordered on it)."""
+    import torch
+    key = id(ctx)
+    st = _LIB_STREAMS.get(key)
+    if st is None or st[0] is not ctx:
+        dev = torch.device("cuda", getattr(ctx, "device", torch.cuda.current_device()))
+        st = (ctx, torch.cuda.ExternalStream(ph.context_stream(ctx), device=dev))
+        _LIB_STREAMS[key] = st
+    return st[1]
+
+
+def _order(first, then):
+    """`then` waits (on the device) for the work enqueued so far on `first`."""
+    import torch
+    ev = torch.cuda.Event()
+    ev.record(first)
+    then.wait_event(ev)
+
+
+def to_buffer(ph, ctx, ct, buf):
+    """Ciphertext limbs -> torch buffer (int64 view), ordered by events instead of device-wide
+    synchronisation: the library stream waits for torch's pending work on `buf` (the allocation's
+    previous use), the copy runs on the library stream, torch's current stream waits for the copy
+    before any RCCL / torch op reads `buf`."""
+    import torch
+    cur, lib = torch.cuda.current_stream(buf.device), lib_stream(ph, ctx)
+    _order(cur, lib)
+    ph.ciphertext_copy_to_device(ctx, ct, buf.data_ptr(), sync=False)
+    _order(lib, cur)
+
+
+def from_buffer(ph, ctx, buf, ncomp, chain_index, scale):
+    """torch buffer -> new ciphertext; the library stream waits for the buffer's producer (e.g. an
+    RCCL receive on torch's stream), torch waits for the copy before it may reuse `buf`."""
+    import torch
+    cur, lib = torch.cuda.current_stream(buf.device), lib_stream(ph, ctx)
+    _order(cur, lib)
+    ct = ph.ciphertext_from_device(ctx, buf.data_ptr(), ncomp, chain_index, scale, sync=False)
+    _order(lib, cur)
+    return ct
 
 
 def stage_groups(n_proj: int, world: int):
@@ -129,8 +194,7 @@ def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts,
     part = bsgs_giant_partial(ph, ctx, baby, pts, G, D, share, gk, zero_pts)
     ci, scale, l = part.chain_index(), part.scale(), part.coeff_modulus_size()
     buf = torch.empty(2 * l * ctx.N, dtype=torch.int64, device=device)
-    torch.cuda.synchronize()                      # torch's earlier use of the allocation is done
-    ph.ciphertext_copy_to_device(ctx, part, buf.data_ptr())
+    to_buffer(ph, ctx, part, buf)
     rows = [int(q) for q in ctx.primes[:l]] * 2   # [comp][limb] rows, limb t mod q_t
     if dist.get_backend(group) == "gloo":
         h = buf.cpu()
@@ -140,6 +204,5 @@ def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts,
         modular_reduce_sum(dist, buf, rows, root=ranks[0], group=group)
     if me != ranks[0]:
         return None
-    torch.cuda.synchronize()
-    total = ph.ciphertext_from_device(ctx, buf.data_ptr(), 2, ci, scale)
+    total = from_buffer(ph, ctx, buf, 2, ci, scale)
     return ph.rescale_to_next(ctx, total)

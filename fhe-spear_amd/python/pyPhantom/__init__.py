@@ -137,9 +137,34 @@ _SIGS = {
     "fhs_kernel_timer_arm": (C.c_int, [_vp, C.c_uint32]),
     "fhs_ciphertext_copy_to_device": (C.c_int, [_vp, _vp, _vp]),
     "fhs_ciphertext_from_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
+    "fhs_ciphertext_copy_to_device_async": (C.c_int, [_vp, _vp, _vp]),
+    "fhs_ciphertext_from_device_async": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
+    "fhs_context_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
 }
+# Fork-only symbols the reference probes with try/except AttributeError (bg:449-461, 382-391): if
+# the library lacks one (an older build, or FHESPEAR_DISABLE_SYMBOLS for tests), the Python names
+# below are removed at the end of this module, so the reference takes its documented fallback (the
+# upload + fused path, or the pure-Python BSGS loop / per-row encode) instead of failing on import.
+_OPTIONAL = {
+    "fhs_bsgs_multiply_accumulate": ("bsgs_multiply_accumulate",),
+    "fhs_bsgs_from_cpu": ("bsgs_from_cpu", "bsgs_complete_from_cpu"),
+    "fhs_upload_plaintexts": ("upload_plaintexts",),
+    "fhs_offload_plaintexts": ("offload_plaintexts",),
+    "fhs_encode_real_batch": ("ckks_encoder.encode_double_vector_batch",),
+    "fhs_encode_batch": ("ckks_encoder.encode_complex_vector_batch",),
+}
+_DISABLED = {x.strip() for x in os.environ.get("FHESPEAR_DISABLE_SYMBOLS", "").split(",") if x.strip()}
+_MISSING = []
 for _name, (_res, _args) in _SIGS.items():
-    _f = getattr(_lib, _name)
+    try:
+        if _name in _DISABLED:
+            raise AttributeError(_name)
+        _f = getattr(_lib, _name)
+    except AttributeError:
+        if _name in _OPTIONAL:
+            _MISSING.append(_name)
+            continue
+        raise ImportError(f"pyPhantom: {LIB_PATH} lacks the required symbol {_name}") from None
     _f.restype = _res
     _f.argtypes = _args
 
@@ -266,8 +291,9 @@ class context:
         else:
             elts, ep, ne = None, None, 0
         h = _vp()
+        self.device = _default_device() if device is None else int(device)
         _check(_lib.fhs_context_create(p.poly_modulus_degree, pp, len(p.coeff_modulus), p.special_modulus_size, ep, ne,
-                                       _default_device() if device is None else int(device), C.byref(h)), "context")
+                                       self.device, C.byref(h)), "context")
         self._h = h
         self.params = p
         self.N = p.poly_modulus_degree
@@ -761,11 +787,32 @@ def _ctx_of(data):
     return ctx
 
 
+def _host_diagonals(ctx, data, chain_index, coeff_modulus_size, poly_modulus_degree, count, what):
+    """Validate a host array of plaintext limbs (count, limbs, N) against the context before the
+    device DMA reads count * limbs * N words from it (bg:348 tuple: chain_index, coeff_modulus_size,
+    poly_modulus_degree)."""
+    a = np.ascontiguousarray(data, dtype=np.uint64)
+    l = ctx.L0 + 1 - int(chain_index)
+    if a.ndim != 3:
+        raise ValueError(f"{what}: expected a (count, limbs, N) array, got shape {a.shape}")
+    if int(coeff_modulus_size) != l or a.shape[1] != l:
+        raise ValueError(f"{what}: chain_index {chain_index} has {l} limbs, but coeff_modulus_size is "
+                         f"{coeff_modulus_size} and the array has {a.shape[1]}")
+    if int(poly_modulus_degree) != ctx.N or a.shape[2] != ctx.N:
+        raise ValueError(f"{what}: poly_modulus_degree {poly_modulus_degree} / array width {a.shape[2]} "
+                         f"differ from the context's N = {ctx.N}")
+    if count is not None and a.shape[0] < count:
+        raise ValueError(f"{what}: {a.shape[0]} plaintexts given, {count} needed")
+    return a
+
+
 def upload_plaintexts(data, chain_index, scale, coeff_modulus_size, poly_modulus_degree):
     """bg:349: host -> device; returns a list of plaintexts."""
     ctx = _ctx_of(data)
-    a = np.ascontiguousarray(data, dtype=np.uint64)
+    a = _host_diagonals(ctx, data, chain_index, coeff_modulus_size, poly_modulus_degree, None, "upload_plaintexts")
     n = a.shape[0]
+    if n < 1:
+        raise ValueError("upload_plaintexts: empty array")
     hs = (_vp * n)()
     _check(_lib.fhs_upload_plaintexts(ctx._h, a.ctypes.data_as(_u64p), n, int(chain_index), float(scale), hs),
            "upload_plaintexts")
@@ -774,8 +821,8 @@ def upload_plaintexts(data, chain_index, scale, coeff_modulus_size, poly_modulus
 
 def bsgs_from_cpu(ctx, ct_baby, data, chain_index, scale, coeff_modulus_size, poly_modulus_degree, G, B, D, gk):
     """bg:449: BSGS with the diagonals streamed from host memory."""
-    a = np.ascontiguousarray(data, dtype=np.uint64)
     G, B, D = int(G), int(B), int(D)
+    a = _host_diagonals(ctx, data, chain_index, coeff_modulus_size, poly_modulus_degree, D, "bsgs_from_cpu")
     bb = (_vp * G)(*[c._h for c in ct_baby[:G]])
     return _ct(ctx, _lib.fhs_bsgs_from_cpu, bb, G, a.ctypes.data_as(_u64p), D, B, int(chain_index), float(scale),
                gk._h, what="bsgs_from_cpu")
@@ -842,15 +889,25 @@ def kernel_timer_read(ctx, reset=False):
     return out
 
 
-def ciphertext_copy_to_device(ctx, ct, dst_ptr):
-    _check(_lib.fhs_ciphertext_copy_to_device(ctx._h, ct._h, _vp(int(dst_ptr))), "copy_to_device")
+def ciphertext_copy_to_device(ctx, ct, dst_ptr, sync=True):
+    """Ciphertext limbs -> caller-owned HBM.  sync=False only enqueues the copy on the context stream
+    (context_stream); the caller orders its streams with events (fhespear_dist.to_buffer)."""
+    fn = _lib.fhs_ciphertext_copy_to_device if sync else _lib.fhs_ciphertext_copy_to_device_async
+    _check(fn(ctx._h, ct._h, _vp(int(dst_ptr))), "copy_to_device")
 
 
-def ciphertext_from_device(ctx, src_ptr, ncomp, chain_index, scale):
+def ciphertext_from_device(ctx, src_ptr, ncomp, chain_index, scale, sync=True):
+    fn = _lib.fhs_ciphertext_from_device if sync else _lib.fhs_ciphertext_from_device_async
     h = _vp()
-    _check(_lib.fhs_ciphertext_from_device(ctx._h, _vp(int(src_ptr)), int(ncomp), int(chain_index), float(scale),
-                                           C.byref(h)), "from_device")
+    _check(fn(ctx._h, _vp(int(src_ptr)), int(ncomp), int(chain_index), float(scale), C.byref(h)), "from_device")
     return ciphertext(ctx, h)
+
+
+def context_stream(ctx):
+    """The context's HIP stream handle (int), e.g. for torch.cuda.ExternalStream."""
+    h = _vp()
+    _check(_lib.fhs_context_stream(ctx._h, C.byref(h)), "context_stream")
+    return int(h.value or 0)
 
 
 from . import bootstrap as _bootstrap  # noqa: E402
@@ -868,3 +925,11 @@ def device_count():
 
 
 _lock = threading.Lock()
+
+for _name in _MISSING:   # absent optional symbols -> AttributeError for the reference's fallbacks
+    for _py in _OPTIONAL[_name]:
+        _owner, _, _attr = _py.rpartition(".")
+        if _owner:
+            delattr(globals()[_owner], _attr)
+        else:
+            del globals()[_attr]

@@ -225,6 +225,15 @@ fhs_status fhs_kernel_timer(fhs_context* ctx, int kernel_id, float* ms, int* lau
 fhs_status fhs_ciphertext_copy_to_device(fhs_context* ctx, const fhs_ciphertext* ct, void* dst);
 fhs_status fhs_ciphertext_from_device(fhs_context* ctx, const void* src, int ncomp, int chain_index, double scale,
                                       fhs_ciphertext** out);
+/* Stream-ordered variants for callers that order their own streams against the context stream
+ * (fhespear_dist: torch / RCCL buffers): the copy is enqueued on the context stream and the call
+ * returns without waiting; the caller makes the context stream wait for the buffer's producer and
+ * its own stream wait for the copy (HIP events; torch.cuda.ExternalStream on fhs_context_stream). */
+fhs_status fhs_ciphertext_copy_to_device_async(fhs_context* ctx, const fhs_ciphertext* ct, void* dst);
+fhs_status fhs_ciphertext_from_device_async(fhs_context* ctx, const void* src, int ncomp, int chain_index,
+                                            double scale, fhs_ciphertext** out);
+/* the context's HIP stream (hipStream_t), on which every library call is ordered */
+fhs_status fhs_context_stream(fhs_context* ctx, void** stream);
 /* Host-side diagnostic of the device reduction arithmetic (no GPU needed): reduces hi:lo mod q with
  * the pseudo-Mersenne folds the kernels use when q qualifies (*pm_used = 1), else *pm_used = 0 and
  * *out = (hi:lo) mod q.  Exists so the CPU test suite can check the fold bounds against big ints. */

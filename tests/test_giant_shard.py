@@ -52,3 +52,30 @@ def test_giant_sharded_bsgs_bit_exact_two_ranks(require_gpu, D):
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert re.search(r"bit-exact vs one-GPU fused BSGS: True", out.stdout), out.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_giant_sharded_bsgs_over_rccl_world1(require_gpu):
+    """bsgs_giant_sharded through RCCL (backend nccl) at world 1: the int64 reduce, the event-ordered
+    copies between the library stream and torch's stream, and the root's rescale, bit-exact vs the
+    fused BSGS."""
+    env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29561", str(REPO / "tools" / "giant_shard.py"),
+           "--backend", "nccl", "--N", "4096", "--L0", "6", "--P", "3", "--D", "256", "--reps", "1"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert re.search(r"bit-exact vs one-GPU fused BSGS: True", out.stdout), out.stdout[-2000:]
+
+
+def test_modular_reduce_sum_exact_beyond_int64_bound():
+    """60-bit moduli at world 9: a plain int64 sum of residues could pass 2^63, so the helper must
+    switch to the gathered modular sum; world-9 gloo run on CPU, result vs Python ints."""
+    assert fd.int64_sum_is_exact(15, [(1 << 59) - 55])
+    assert not fd.int64_sum_is_exact(9, [(1 << 60) - 93])
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "9",
+           "--master-addr", "127.0.0.1", "--master-port", "29581", str(Path(__file__).parent / "_reduce_worker.py")]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert "reduce exact: True" in out.stdout, out.stdout[-2000:]

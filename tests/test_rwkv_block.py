@@ -88,29 +88,60 @@ def test_projection_matrices_shape_and_stages():
         rb.BlockRunner(ExactServer(D, 32), rb.BlockWeights(np.random.default_rng(1), 0, D, 3 * D, 2), False)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("world,split", [(2, False), (2, True), (4, True)])
-def test_block_over_ranks(require_gpu, world, split):
-    """cfg4's exchange (stage inputs broadcast from the client rank, output ciphertexts to it) on one
-    GPU: gloo stages the limbs through host memory, every rank's context shares cuda:0.  split=True
-    is latency mode (giant steps of a projection sharded over a rank group: at world 4 the stages
-    split 2+1+1 / 4 / 2+2 / 2+2; at world 2 stage 1 is dealt).  The decrypted block must match the
-    plaintext block as in the one-rank case."""
+def _run_block_tool(world, backend="gloo", extra=(), port=29541):
+    """tools/rwkv_block.py under torch.distributed.run on cuda:0; returns (final max_err, x digest)."""
     import os
     import re
     import subprocess
     env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(29541 + world + 10 * split),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
            str(REPO / "tools" / "rwkv_block.py"),
-           "--backend", "gloo", "--N", "2048", "--L0", "4", "--P", "2", "--D", "64", "--F", "256",
-           "--head-size", "16", "--blocks", "2", "--reps", "1", "--preencoded"] + (["--split"] if split else [])
+           "--backend", backend, "--N", "2048", "--L0", "4", "--P", "2", "--D", "64", "--F", "256",
+           "--head-size", "16", "--blocks", "2", "--reps", "1", "--preencoded"] + list(extra)
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
-    m = re.search(rf"world {world}.*: .* final max_err ([0-9.e+-]+)", out.stdout)
+    m = re.search(rf"world {world}.*: .* final max_err ([0-9.e+-]+) x_sha256 ([0-9a-f]+)", out.stdout)
     assert m, out.stdout[-2000:]
-    assert float(m.group(1)) < 1e-4
     assert all(float(c) > 0.999999 for c in re.findall(r"corr=([0-9.]+)", out.stdout))
+    return float(m.group(1)), m.group(2)
+
+
+_ONE_RANK = {}
+
+
+def _one_rank_digest():
+    if "d" not in _ONE_RANK:
+        _ONE_RANK["d"] = _run_block_tool(1, port=29540)[1]
+    return _ONE_RANK["d"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,split,babies", [(2, False, "recompute"), (2, False, "broadcast"),
+                                                 (2, True, "recompute"), (4, True, "recompute"),
+                                                 (4, True, "broadcast")])
+def test_block_over_ranks(require_gpu, world, split, babies):
+    """cfg4's exchange (stage inputs broadcast from the client rank, output ciphertexts to it) on one
+    GPU: gloo stages the limbs through host memory, every rank's context shares cuda:0.  split=True
+    is latency mode (giant steps of a projection sharded over a rank group: at world 4 the stages
+    split 2+1+1 / 4 / 2+2 / 2+2; at world 2 stage 1 is dealt).  babies="broadcast": the baby steps
+    of an input several ranks need are computed on one rank and broadcast (north_star).  Every
+    variant must give the one-rank block's output bit for bit (same digest of the decrypted x)."""
+    extra = (["--split"] if split else []) + ["--baby-mode", babies]
+    err, digest = _run_block_tool(world, extra=extra, port=29541 + world + 10 * split + 20 * (babies == "broadcast"))
+    assert err < 1e-4
+    assert digest == _one_rank_digest()
+
+
+@pytest.mark.gpu
+def test_block_exchange_over_rccl_world1(require_gpu):
+    """The real transport: backend nccl (RCCL) at world 1 with the process group forced on, so the
+    input broadcast, the output gather and the event ordering between the library stream and torch's
+    stream (fhespear_dist.to_buffer / from_buffer) run on hardware; the output must equal the
+    no-process-group run bit for bit."""
+    err, digest = _run_block_tool(1, backend="nccl", extra=["--dist"], port=29571)
+    assert err < 1e-4
+    assert digest == _one_rank_digest()
 
 
 @pytest.mark.gpu

@@ -23,6 +23,7 @@ decrypt what the others computed; no rank but 0 encrypts or decrypts.
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/rwkv_block.py --preencoded
 """
 import argparse
+import hashlib
 import os
 import sys
 import time
@@ -236,8 +237,14 @@ class BlockRunner:
     steps (fhespear_dist.stage_groups / bsgs_giant_sharded); a stage with more projections than
     ranks is dealt."""
 
-    def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1, split=False):
+    def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1, split=False, baby_mode="recompute"):
         self.srv, self.block, self.pre, self.dist, self.rank, self.world = srv, block, preencoded, dist, rank, world
+        if baby_mode not in ("recompute", "broadcast"):
+            raise ValueError(f"baby_mode {baby_mode!r}: 'recompute' or 'broadcast'")
+        # baby steps of an input several ranks need: every rank computes them ("recompute"), or the
+        # first of those ranks computes them and broadcasts the G ciphertexts (north_star: "computed
+        # once and broadcast"; 434 MB at cfg2) -- limb-identical either way
+        self.baby_mode = baby_mode if dist is not None else "recompute"
         self.mats = {n: (k, m) for n, k, m in projection_matrices(block)}
         if set(self.mats) != set(fhespear_dist.RWKV_BLOCK_PROJECTIONS):
             raise ValueError("rwkv_block: this runner expects F = 4 D (8 projections, RWKV-7)")
@@ -261,6 +268,18 @@ class BlockRunner:
                 self.assign[i] = [n for n, ranks, _ in lay if rank in ranks]
             self.zero = srv.encoder.encode_double_vector_batch(srv.ctx, np.zeros((srv.G, srv.slots)), srv.diag_scale,
                                                                chain_index=srv.level)
+        # dealt stages: ranks owning projections that share an input -> (ranks, process group)
+        self.share_groups = {}
+        if self.baby_mode == "broadcast":
+            for i, names in enumerate(fhespear_dist.RWKV_BLOCK_STAGES):
+                if self.layout[i] is not None:
+                    continue
+                for shared in fhespear_dist.RWKV_SHARED_INPUTS:
+                    if not set(shared) <= set(names):
+                        continue
+                    owners = sorted({names.index(n) % world for n in shared})
+                    if len(owners) > 1:
+                        self.share_groups[(i, shared)] = (owners, dist.new_group(owners))
         mine = {n for st in self.assign for n in st}
         self.pts = {}
         if preencoded:                       # bg:1124-1174 --preencoded, resident in HBM
@@ -286,24 +305,47 @@ class BlockRunner:
         return self.pts[name] if self.pre else self._encode(name)
 
     def _pack(self, ct, buf):
-        """ciphertext limbs + its scale (float64 bits in the last word) into an int64 device buffer.
-        The library copies on its own non-blocking stream: torch's pending work on `buf` (the
-        allocation's previous use) must be done first."""
-        import torch
-        torch.cuda.synchronize()
-        self.srv.ph.ciphertext_copy_to_device(self.srv.ctx, ct, buf.data_ptr())
+        """ciphertext limbs + its scale (float64 bits in the last word) into an int64 device buffer,
+        ordered against torch's stream with events (fhespear_dist.to_buffer)."""
+        fhespear_dist.to_buffer(self.srv.ph, self.srv.ctx, ct, buf)
         buf[-1:].copy_(_scale_word(ct.scale(), buf))
 
     def _unpack(self, buf, ci):
         import torch
-        torch.cuda.synchronize()
         scale = float(buf[-1:].cpu().view(torch.float64).item())
-        return self.srv.ph.ciphertext_from_device(self.srv.ctx, buf.data_ptr(), 2, ci, scale)
+        return fhespear_dist.from_buffer(self.srv.ph, self.srv.ctx, buf, 2, ci, scale)
 
     def _buf(self, ci):
         import torch
         l = self.srv.L0 + 1 - ci
         return torch.empty(2 * l * self.srv.N + 1, dtype=torch.int64, device=f"cuda:{self.srv.device}")
+
+    def _shared_babies(self, ct, ranks, pg):
+        """Baby steps of `ct` (bg:215-220) computed on ranks[0] and broadcast over `pg` to the other
+        ranks of `ranks`, as one buffer of G ciphertexts (rotations keep ct's level and scale)."""
+        import torch
+        srv = self.srv
+        G, ci = srv.G, ct.chain_index()
+        words = 2 * (srv.L0 + 1 - ci) * srv.N
+        buf = torch.empty(G * words + 1, dtype=torch.int64, device=f"cuda:{srv.device}")
+        src = ranks[0]
+        if self.rank == src:
+            babies = srv.baby(ct)
+            for b, c in enumerate(babies):
+                fhespear_dist.to_buffer(srv.ph, srv.ctx, c, buf[b * words:(b + 1) * words])
+            buf[-1:].copy_(_scale_word(ct.scale(), buf))
+        if self.host_coll:
+            h = buf.cpu()
+            self.dist.broadcast(h, src=src, group=pg)
+            if self.rank != src:
+                buf.copy_(h)
+        else:
+            self.dist.broadcast(buf, src=src, group=pg)
+        if self.rank == src:
+            return babies
+        scale = float(buf[-1:].cpu().view(torch.float64).item())
+        return [fhespear_dist.from_buffer(srv.ph, srv.ctx, buf[b * words:(b + 1) * words], 2, ci, scale)
+                for b in range(G)]
 
     def _bcast_ct(self, ct):
         """rank 0's ciphertext -> every rank (RCCL broadcast over xGMI)."""
@@ -311,7 +353,6 @@ class BlockRunner:
         buf = self._buf(srv.level)
         if self.rank == 0:
             self._pack(ct, buf)
-            srv.ctx.synchronize()
         if self.host_coll:                   # gloo (shared-GPU rehearsal): stage through host
             h = buf.cpu()
             fhespear_dist.broadcast_from(self.dist, h, 0)
@@ -334,6 +375,10 @@ class BlockRunner:
             return self._stage_split(idx, inputs, cts)
         mine = names if self.dist is None else self.assign[idx]
         babies = {}
+        for (i, shared), (ranks, pg) in self.share_groups.items():
+            if i == idx and self.rank in ranks:   # computed on ranks[0], broadcast to the others
+                key = inputs[shared[0]][1]
+                babies[key] = self._shared_babies(cts[key], ranks, pg)
         outs = {}
         for n in mine:
             key = inputs[n][1]
@@ -354,7 +399,10 @@ class BlockRunner:
         for n, ranks, pg in self.layout[idx]:
             if self.rank not in ranks:
                 continue
-            baby = srv.baby(cts[inputs[n][1]])
+            if self.baby_mode == "broadcast" and len(ranks) > 1:
+                baby = self._shared_babies(cts[inputs[n][1]], ranks, pg)
+            else:
+                baby = srv.baby(cts[inputs[n][1]])
             pts = self._pts(n)
             if len(ranks) == 1:
                 out = srv.matmul(baby, [pts[k] for k in range(srv.D)] if isinstance(pts, dict) else pts)
@@ -374,7 +422,6 @@ class BlockRunner:
             if self.rank == src:
                 buf = self._buf(ci)
                 self._pack(res[n], buf)
-                srv.ctx.synchronize()
                 if self.host_coll:
                     self.dist.send(buf.cpu(), dst=0)
                 else:
@@ -400,7 +447,6 @@ class BlockRunner:
             local = [n for i, n in enumerate(names) if i // self.world == r and i % self.world == self.rank]
             if local:
                 self._pack(outs[local[0]], buf)
-            srv.ctx.synchronize()
             if self.host_coll:
                 got = fhespear_dist.gather_to_root(self.dist, buf.cpu(), self.world, self.rank)
                 got = [g.to(buf.device) for g in got] if got is not None else None
@@ -501,8 +547,8 @@ def run_blocks(ph, args, dist=None, rank=0, world=1, device=0, log=print):
     blocks = [BlockWeights(rng, b, args.D, args.F, H) for b in range(args.blocks)]
     t0 = time.perf_counter()
     srv = Server(ph, args.N, args.L0, args.P, args.D, device=device)
-    runs = [BlockRunner(srv, b, args.preencoded, dist, rank, world, split=getattr(args, "split", False))
-            for b in blocks]
+    runs = [BlockRunner(srv, b, args.preencoded, dist, rank, world, split=getattr(args, "split", False),
+                        baby_mode=getattr(args, "baby_mode", "recompute")) for b in blocks]
     srv.ctx.synchronize()
     if rank == 0:
         log(f"setup (keys{', pre-encoded diagonals' if args.preencoded else ''}): {time.perf_counter() - t0:.2f} s")
@@ -521,7 +567,8 @@ def run_blocks(ph, args, dist=None, rank=0, world=1, device=0, log=print):
             corr = float(np.corrcoef(st[0], ref[0])[0, 1])
             sec = sum(tm.values())
             rec = dict(block=b, server_seconds=sec, stages=tm, max_err=err, corr=corr,
-                       mag=float(np.max(np.abs(ref[0]))))
+                       mag=float(np.max(np.abs(ref[0]))),
+                       x_sha256=hashlib.sha256(np.ascontiguousarray(st[0]).tobytes()).hexdigest())
             recs.append(rec)
             log(f"block {b}: server {1e3 * sec:.1f} ms (" + ", ".join(f"{k} {1e3 * v:.1f}" for k, v in tm.items())
                 + f")  max_err={err:.3e} |x|={rec['mag']:.2f} corr={corr:.10f}")
@@ -543,12 +590,16 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--split", action="store_true",
                     help="latency mode: each stage's projections shard their giant steps over rank groups")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group even at world 1 (runs the exchange code on one GPU)")
+    ap.add_argument("--baby-mode", default="recompute", choices=("recompute", "broadcast"),
+                    help="baby steps of an input several ranks need: recomputed by each, or computed once and broadcast")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or a.dist:
         import torch
         import torch.distributed as dist
         if a.backend == "nccl":               # RCCL over xGMI, one GPU per rank
@@ -561,8 +612,9 @@ def main():
     recs = run_blocks(ph, a, dist, rank, world, local)
     if rank == 0:
         s = [r["server_seconds"] for r in recs]
-        print(f"world {world}{' split' if a.split else ''}: mean server time per block {np.mean(s):.4f} s over {len(s)} block(s), "
-              f"final max_err {recs[-1]['max_err']:.3e}")
+        print(f"world {world}{' split' if a.split else ''} babies {a.baby_mode}: mean server time per block "
+              f"{np.mean(s):.4f} s over {len(s)} block(s), final max_err {recs[-1]['max_err']:.3e} "
+              f"x_sha256 {recs[-1]['x_sha256']}")
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
