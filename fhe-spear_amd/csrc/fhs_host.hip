@@ -2,8 +2,8 @@
 // generation, CKKS encode/decode, and every extern "C" entry point of include/fhespear.h.
 //
 // Runtime model (MI355X-first):
-//  - one context = one device + one HIP stream; all device memory comes from the stream-ordered
-//    pool (hipMallocAsync) behind a per-size caching free list, so a free never synchronises the host;
+//  - one context = one device + one HIP stream; device blocks come from hipMalloc behind a bounded
+//    per-size caching free list reused in stream order, so a free never synchronises the host;
 //  - calls on a context are serialised by a mutex (ctypes drops the GIL; bg:223-249 may call
 //    from a thread pool);
 //  - rotations are DEFERRED and batched: fhs_rotate allocates the output and queues the
@@ -229,9 +229,6 @@ struct PendingRot {
 struct fhs_context {
     int device = 0;
     hipStream_t st = nullptr;
-    // the context's own stream-ordered pool (release threshold infinite: freed blocks stay mapped
-    // for reuse); trimmed on out-of-memory, at destruction (then destroyed) and at process exit
-    hipMemPool_t pool = nullptr;
     hipStream_t st_aux = nullptr;          // second stream of the pipelined BSGS (memory-bound kernels)
     std::vector<hipEvent_t> bsgs_ev;       // cross-stream ordering events of launch_bsgs
     int bsgs_chunks = 1;                   // FHESPEAR_BSGS_CHUNKS (overlap measured slower)
@@ -258,9 +255,9 @@ struct fhs_context {
     std::atomic<int> refs{1};
     // caching allocator: freed device blocks are kept per exact size and reused in stream order
     // (every use of a block is ordered on `st`, aux-stream work is joined back into `st`).  A large
-    // hipMallocAsync costs ~0.35 ms/GB of host time and each hipFreeAsync ~8 us (tools/microbench/
+    // device allocation costs host time per GB and a free synchronises (tools/microbench/
     // alloc.hip); ciphertexts and plaintexts come in a handful of sizes, so almost every allocation
-    // after warm-up is a free-list pop.  Trimmed on out-of-memory and at context destruction.
+    // after warm-up is a free-list pop.  Trimmed on out-of-memory, at context destruction and exit.
     std::unordered_map<size_t, std::vector<void*>> free_blocks;
     size_t cached_bytes = 0;
     // bounded: a chain walks down the levels, so every level brings new sizes and the sizes of the
@@ -281,7 +278,7 @@ struct fhs_context {
     static constexpr size_t kRingBytes = 16u << 20;
     fhs::Stager stager{};
     // grow-only scratch buffers reused across calls (stream order makes reuse safe): a large
-    // hipMallocAsync costs ~0.7 ms/GB of host time and can wait on earlier frees
+    // allocation costs host time per GB
     enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_ENC_PTRS, SCR_COUNT };
     uint64_t* scr[SCR_COUNT] = {};
     size_t scr_bytes[SCR_COUNT] = {};
@@ -304,13 +301,13 @@ struct fhs_plaintext {
 struct fhs_secret_key {
     fhs_context* ctx;
     uint64_t* s;   // K limbs, NTT
-    uint64_t seed;
-    uint64_t ctr;
+    PrfKey key;    // 256-bit PRF key all secret randomness is drawn from
+    uint64_t ctr;  // symmetric-encryption counter
 };
 struct fhs_public_key {
     fhs_context* ctx;
     uint64_t* pk;  // 2 x L0
-    uint64_t seed;
+    PrfKey rng;    // encryption-mask key: a PRF output of the secret key (reveals nothing about it)
     uint64_t ctr;
 };
 struct fhs_relin_key {
@@ -324,23 +321,20 @@ struct fhs_galois_keys {
 
 static void ctx_retain(fhs_context* c) { c->refs.fetch_add(1); }
 
-// Live contexts, for the out-of-memory path (every pool's unused blocks are released before the
-// retry) and for the process-exit release.  A multi-GB pool still mapped when the HIP runtime's own
-// exit handler ran crashed inside libamdhip64 (round 1, a 13-block d=2048 FFN chain with 135 GB
-// cached): release_at_exit is registered with atexit() right after the first context's stream is
-// created, i.e. after HIP registered its handler, so it runs first (LIFO) and leaves every pool
-// trimmed and the caches empty.
+// Live contexts, for the out-of-memory path (every context's cached blocks on the device are
+// released before the retry) and for the process-exit release.  Device blocks come from plain
+// hipMalloc behind the per-size cache: round 1 used stream-ordered pools with an infinite release
+// threshold, and a process exiting with a multi-GB pool still mapped crashed inside libamdhip64's
+// exit handler (a 13-block d=2048 FFN chain with 135 GB cached), and a pool that had been driven to
+// out-of-memory left the next process exit crashing too.  release_at_exit is registered with atexit()
+// after the first context's stream exists (i.e. after HIP registered its own handlers), so it runs
+// first and returns every cached block.
 static std::mutex g_live_mu;
 static std::set<fhs_context*> g_live;
-static void release_pool_blocks(fhs_context* c);
+static void release_cached_blocks(fhs_context* c);
 static void release_at_exit() {
     std::lock_guard<std::mutex> lk(g_live_mu);
-    for (fhs_context* c : g_live) release_pool_blocks(c);
-}
-static void trim_all_pools(fhs_context* self) {
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    for (fhs_context* c : g_live)
-        if (c != self && c->pool && c->device == self->device) (void)hipMemPoolTrimTo(c->pool, 0);
+    for (fhs_context* c : g_live) release_cached_blocks(c);
 }
 static void ctx_release(fhs_context* c);
 
@@ -350,36 +344,38 @@ static size_t key_words(const fhs_context* c) { return (size_t)c->dnum * c->K * 
 // exported / oracle layout: [dnum][2][K][N]
 static size_t key_words_full(const fhs_context* c) { return (size_t)c->dnum * 2 * c->K * c->N; }
 
+static void ctx_sync(fhs_context* c) {
+    hipStreamSynchronize(c->st);
+    if (c->st_aux) hipStreamSynchronize(c->st_aux);
+}
+// every cached block back to the device (the caller holds c->mu)
 static void trim_cache(fhs_context* c) {
     if (c->free_blocks.empty()) return;
     if (getenv("FHESPEAR_TRACE_LIFETIME"))
         fprintf(stderr, "[fhespear] trim: %zu cached bytes in %zu sizes, %llu live\n", c->cached_bytes,
                 c->free_blocks.size(), (unsigned long long)c->bytes_live.load());
-    if (c->st_aux) hipStreamSynchronize(c->st_aux);
+    ctx_sync(c);   // a cached block may still be read by queued work
     for (auto& kv : c->free_blocks)
-        for (void* p : kv.second) (void)hipFreeAsync(p, c->st);
-    hipStreamSynchronize(c->st);
+        for (void* p : kv.second) (void)hipFree(p);
     c->free_blocks.clear();
     c->cached_bytes = 0;
-    if (c->pool) (void)hipMemPoolTrimTo(c->pool, 0);
 }
-// exit path: cached blocks back to the pool, the pool's unused memory back to the device
-static void release_pool_blocks(fhs_context* c) {
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    hipStreamSynchronize(c->st);
-    if (c->st_aux) hipStreamSynchronize(c->st_aux);
-    for (auto& kv : c->free_blocks)
-        for (void* p : kv.second) (void)hipFreeAsync(p, c->st);
-    hipStreamSynchronize(c->st);
-    c->free_blocks.clear();
-    c->cached_bytes = 0;
-    if (c->pool) {
-        uint64_t zero = 0;
-        (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &zero);
-        (void)hipMemPoolTrimTo(c->pool, 0);
+// out-of-memory retry: the other contexts on the device give their caches back too (try_lock: a
+// context busy on another thread keeps its cache rather than risk a lock-order inversion)
+static void trim_other_caches(fhs_context* self) {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    for (fhs_context* c : g_live) {
+        if (c == self || c->device != self->device) continue;
+        std::unique_lock<std::recursive_mutex> cl(c->mu, std::try_to_lock);
+        if (cl.owns_lock()) trim_cache(c);
     }
 }
+static void release_cached_blocks(fhs_context* c) {
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    trim_cache(c);
+}
 static void evict_cold(fhs_context* c, size_t keep) {
+    std::vector<void*> victims;
     while (c->cached_bytes > c->cache_cap) {
         size_t victim = 0;
         uint64_t oldest = ~0ull;
@@ -391,12 +387,15 @@ static void evict_cold(fhs_context* c, size_t keep) {
         if (!victim) victim = keep;   // only the size in hand is cached: shed its blocks
         auto& v = c->free_blocks[victim];
         while (!v.empty() && c->cached_bytes > c->cache_cap) {
-            (void)hipFreeAsync(v.back(), c->st);
+            victims.push_back(v.back());
             v.pop_back();
             c->cached_bytes -= victim;
         }
         if (v.empty()) c->free_blocks.erase(victim);
     }
+    if (victims.empty()) return;
+    ctx_sync(c);
+    for (void* p : victims) (void)hipFree(p);
 }
 static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
     bytes = bytes ? bytes : 8;
@@ -410,16 +409,18 @@ static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
         return hipSuccess;
     }
     void* v = nullptr;
-    hipError_t e = hipMallocFromPoolAsync(&v, bytes, c->pool, c->st);
-    if (e == hipErrorOutOfMemory) {   // give the caches and every pool's unused blocks back, retry once
+    hipError_t e = hipMalloc(&v, bytes);
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {   // give every cache back, retry once
         (void)hipGetLastError();
         trim_cache(c);
-        trim_all_pools(c);
-        e = hipMallocFromPoolAsync(&v, bytes, c->pool, c->st);
+        trim_other_caches(c);
+        e = hipMalloc(&v, bytes);
     }
     if (e == hipSuccess) {
         *p = (uint64_t*)v;
         c->bytes_live += bytes;
+    } else {
+        (void)hipGetLastError();   // not sticky: the next launch's hipGetLastError must not see it
     }
     return e;
 }
@@ -552,6 +553,7 @@ struct Guard {
 #define ENTER(ctx)                                                           \
     if (!(ctx)) return fail(FHS_ERR_INVALID, "null context");               \
     Guard _g(ctx);                                                           \
+    (void)hipGetLastError(); /* a failed HIP call of an earlier entry is not this one's */ \
     do {                                                                     \
         fhs_status _s = flush(ctx);                                          \
         if (_s != FHS_OK) return _s;                                         \
@@ -596,14 +598,6 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     {
         static std::once_flag exit_once;
         std::call_once(exit_once, [] { atexit(release_at_exit); });
-        hipMemPoolProps props{};
-        props.allocType = hipMemAllocationTypePinned;
-        props.handleTypes = hipMemHandleTypeNone;
-        props.location.type = hipMemLocationTypeDevice;
-        props.location.id = device;
-        HIPCHK(hipMemPoolCreate(&c->pool, &props), "memory pool");
-        uint64_t thr = ~0ull;
-        (void)hipMemPoolSetAttribute(c->pool, hipMemPoolAttrReleaseThreshold, &thr);
         size_t free_b = 0, total_b = 0;
         (void)hipMemGetInfo(&free_b, &total_b);
         c->cache_cap = total_b / 4;
@@ -839,15 +833,8 @@ static void ctx_free(fhs_context* c) {
             g_live.erase(c);
         }
         for (auto& kv : c->free_blocks)
-            for (void* p : kv.second) hipFreeAsync(p, c->st);
-        hipStreamSynchronize(c->st);
-        // every block of the pool is free now (the context outlives all its objects): hand the
-        // memory back and destroy the pool while the stream that freed the blocks still exists
-        if (c->pool) {
-            hipMemPoolTrimTo(c->pool, 0);
-            hipMemPoolDestroy(c->pool);
-            c->pool = nullptr;
-        }
+            for (void* p : kv.second) hipFree(p);
+        c->free_blocks.clear();
         if (c->ring) hipHostFree(c->ring);
         for (auto& v : c->timer_pairs)
             for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
@@ -890,25 +877,45 @@ extern "C" fhs_status fhs_memory_in_use(fhs_context* c, uint64_t* bytes) {
 
 // ============================================================================ sampling helpers
 // sm64: fhs_modarith.h (host + device)
-static uint64_t stream_key(uint64_t seed, uint64_t stream) { return sm64(seed ^ sm64(stream)); }
+// 256 bits from the OS entropy pool (a secret key created without a caller-supplied key)
+static bool os_random(void* buf, size_t n) {
+    FILE* f = fopen("/dev/urandom", "rb");
+    if (!f) return false;
+    const size_t got = fread(buf, 1, n, f);
+    fclose(f);
+    return got == n;
+}
+static uint64_t prf_u64(const PrfKey& K, uint64_t sid) {
+    uint64_t w0, w1;
+    prf128(K, sid, 0, w0, w1);
+    return w0;
+}
 static uint64_t stream_id(uint64_t kind, uint64_t a, uint64_t b) { return (kind << 56) | (a << 16) | b; }
-enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6 };
+enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6, ST_PK_RNG = 7 };
 
 // sample a small polynomial (ternary/CBD) over `limbs` primes and NTT it
-static hipError_t sample_small_ntt(fhs_context* c, int mode, uint64_t key, uint64_t* out, int limbs) {
-    hipError_t e = fhs::launch_sample(c->T, mode, key, out, limbs, 0, c->st);
+static hipError_t sample_small_ntt(fhs_context* c, int mode, const PrfKey& K, uint64_t sid, uint64_t* out, int limbs) {
+    hipError_t e = fhs::launch_sample(c->T, mode, K, sid, out, limbs, c->st);
     if (e != hipSuccess) return e;
     return fhs::launch_ntt_fwd(c->T, out, limbs, limbs, 1, 0, c->st);
 }
 
 // ============================================================================ keys
-extern "C" fhs_status fhs_secret_key_create(fhs_context* c, uint64_t seed, fhs_secret_key** out) {
+extern "C" fhs_status fhs_secret_key_create(fhs_context* c, const uint8_t* key32, fhs_secret_key** out) {
     ENTER(c);
     if (!out) return fail(FHS_ERR_INVALID, "null out");
-    auto* sk = new fhs_secret_key{c, nullptr, seed, 0};
+    PrfKey K{};
+    if (key32) {
+        for (int w = 0; w < 8; ++w)
+            K.k[w] = (uint32_t)key32[4 * w] | ((uint32_t)key32[4 * w + 1] << 8) | ((uint32_t)key32[4 * w + 2] << 16) |
+                     ((uint32_t)key32[4 * w + 3] << 24);
+    } else if (!os_random(K.k, sizeof(K.k))) {
+        return fail(FHS_ERR_INVALID, "secret_key: /dev/urandom unavailable");
+    }
+    auto* sk = new fhs_secret_key{c, nullptr, K, 0};
     hipError_t e = dalloc(c, &sk->s, 8ull * c->K * c->N);
     if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key"); }
-    e = sample_small_ntt(c, fhs::SAMPLE_TERNARY, stream_key(seed, stream_id(ST_SECRET, 0, 0)), sk->s, c->K);
+    e = sample_small_ntt(c, fhs::SAMPLE_TERNARY, sk->key, stream_id(ST_SECRET, 0, 0), sk->s, c->K);
     if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key sampling"); }
     ctx_retain(c);
     *out = sk;
@@ -923,7 +930,7 @@ extern "C" fhs_status fhs_secret_key_destroy(fhs_secret_key* sk) {
     return FHS_OK;
 }
 
-static fhs_status gen_switch_key(fhs_context* c, uint64_t seed, uint64_t base, const uint64_t* s, const uint64_t* snew,
+static fhs_status gen_switch_key(fhs_context* c, const PrfKey& K, uint64_t base, const uint64_t* s, const uint64_t* snew,
                                  uint64_t** key_out) {
     uint64_t* key = nullptr;
     hipError_t e = dalloc(c, &key, 8 * key_words(c));
@@ -936,10 +943,9 @@ static fhs_status gen_switch_key(fhs_context* c, uint64_t seed, uint64_t base, c
     uint64_t* abuf = tmp + S;
     std::vector<uint64_t> seeds(c->dnum);
     for (int j = 0; j < c->dnum && e == hipSuccess; ++j) {
-        seeds[j] = stream_key(seed, base | (uint64_t)(2 * j));
-        const uint64_t ke = stream_key(seed, base | (uint64_t)(2 * j + 1));
-        e = fhs::launch_sample(c->T, fhs::SAMPLE_SEEDED, seeds[j], abuf, c->K, 0, c->st);
-        if (e == hipSuccess) e = sample_small_ntt(c, fhs::SAMPLE_CBD, ke, ebuf, c->K);
+        seeds[j] = prf_u64(K, base | (uint64_t)(2 * j));   // public seed of a_j: a PRF output
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_SEEDED, K, seeds[j], abuf, c->K, c->st);
+        if (e == hipSuccess) e = sample_small_ntt(c, fhs::SAMPLE_CBD, K, base | (uint64_t)(2 * j + 1), ebuf, c->K);
         if (e == hipSuccess) e = fhs::launch_switch_key_assemble(c->T, key + (size_t)j * S, abuf, ebuf, s, snew, j, c->st);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(key + (size_t)c->dnum * S, seeds.data(), 8 * seeds.size(),
@@ -962,7 +968,7 @@ static fhs_status export_switch_key(fhs_context* c, const uint64_t* key, uint64_
     hipError_t e = hipSuccess;
     for (int j = 0; j < c->dnum && e == hipSuccess; ++j) {
         e = hipMemcpyAsync(full + (size_t)j * 2 * S, key + (size_t)j * S, 8 * S, hipMemcpyDeviceToDevice, c->st);
-        if (e == hipSuccess) e = fhs::launch_sample(c->T, fhs::SAMPLE_SEEDED, seeds[j], full + ((size_t)j * 2 + 1) * S, c->K, 0, c->st);
+        if (e == hipSuccess) e = fhs::launch_sample(c->T, fhs::SAMPLE_SEEDED, PrfKey{}, seeds[j], full + ((size_t)j * 2 + 1) * S, c->K, c->st);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(host, full, 8 * key_words_full(c), hipMemcpyDeviceToHost, c->st);
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);
@@ -978,7 +984,7 @@ extern "C" fhs_status fhs_gen_relin_key(fhs_context* c, fhs_secret_key* sk, fhs_
     HIPCHK(dalloc(c, &s2, 8ull * c->K * c->N), "relin key");
     HIPCHK(fhs::launch_key_prod(c->T, sk->s, sk->s, s2, c->K, c->st), "relin key");
     auto* rk = new fhs_relin_key{c, nullptr};
-    fhs_status s = gen_switch_key(c, sk->seed, stream_id(ST_RELIN, 0, 0), sk->s, s2, &rk->key);
+    fhs_status s = gen_switch_key(c, sk->key, stream_id(ST_RELIN, 0, 0), sk->s, s2, &rk->key);
     dfree(c, s2, 8ull * c->K * c->N);
     if (s != FHS_OK) { delete rk; return s; }
     ctx_retain(c);
@@ -1009,7 +1015,7 @@ extern "C" fhs_status fhs_create_galois_keys(fhs_context* c, fhs_secret_key* sk,
         e = fhs::launch_galois_perm(c->T, sk->s, sn, c->K, elt, c->st);
         if (e != hipSuccess) break;
         uint64_t* key = nullptr;
-        fhs_status s = gen_switch_key(c, sk->seed, stream_id(ST_GALOIS, elt, 0), sk->s, sn, &key);
+        fhs_status s = gen_switch_key(c, sk->key, stream_id(ST_GALOIS, elt, 0), sk->s, sn, &key);
         if (s != FHS_OK) {
             dfree(c, sn, 8ull * c->K * c->N);
             for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
@@ -1077,17 +1083,22 @@ extern "C" fhs_status fhs_secret_key_export(fhs_context* c, const fhs_secret_key
 extern "C" fhs_status fhs_gen_public_key(fhs_context* c, fhs_secret_key* sk, fhs_public_key** out) {
     ENTER(c);
     if (!sk || !out) return fail(FHS_ERR_INVALID, "null argument");
-    auto* pk = new fhs_public_key{c, nullptr, sk->seed, 1ull << 20};
+    auto* pk = new fhs_public_key{c, nullptr, PrfKey{}, 1ull << 20};
+    for (int w = 0; w < 4; ++w) {   // rng = 256 PRF bits of stream ST_PK_RNG
+        uint64_t w0, w1;
+        prf128(sk->key, stream_id(ST_PK_RNG, 0, 0), (uint32_t)w, w0, w1);
+        pk->rng.k[2 * w] = (uint32_t)w0;
+        pk->rng.k[2 * w + 1] = (uint32_t)(w0 >> 32);
+    }
     const size_t S = (size_t)c->L0 * c->N;
     hipError_t e = dalloc(c, &pk->pk, 16 * S);
     if (e != hipSuccess) { delete pk; return hip_fail(e, "public key"); }
     uint64_t* eb = nullptr;
     e = dalloc(c, &eb, 8 * S);
     if (e == hipSuccess)
-        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(sk->seed, stream_id(ST_PUBKEY, 0, 0)), pk->pk + S,
-                               c->L0, 0, c->st);
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, sk->key, stream_id(ST_PUBKEY, 0, 0), pk->pk + S, c->L0, c->st);
     if (e == hipSuccess)
-        e = sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(sk->seed, stream_id(ST_PUBKEY, 0, 1)), eb, c->L0);
+        e = sample_small_ntt(c, fhs::SAMPLE_CBD, sk->key, stream_id(ST_PUBKEY, 0, 1), eb, c->L0);
     if (e == hipSuccess)
         e = fhs::launch_encrypt_combine(c->T, 0, pk->pk, pk->pk + S, sk->s, nullptr, nullptr, eb, nullptr, nullptr,
                                         c->L0, c->st);
@@ -1662,9 +1673,8 @@ extern "C" fhs_status fhs_encrypt_symmetric(fhs_context* c, fhs_secret_key* sk, 
     const size_t S = (size_t)l * c->N;
     uint64_t* eb = nullptr;
     HIPCHK(dalloc(c, &eb, 8 * S), "encrypt");
-    HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(sk->seed, stream_id(ST_ENC_SYM, ctr, 0)), ct->d + S,
-                              l, 0, c->st), "encrypt");
-    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(sk->seed, stream_id(ST_ENC_SYM, ctr, 1)), eb, l), "encrypt");
+    HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, sk->key, stream_id(ST_ENC_SYM, ctr, 0), ct->d + S, l, c->st), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, sk->key, stream_id(ST_ENC_SYM, ctr, 1), eb, l), "encrypt");
     HIPCHK(fhs::launch_encrypt_combine(c->T, 0, ct->d, ct->d + S, sk->s, nullptr, nullptr, eb, nullptr, pt->d, l, c->st),
            "encrypt");
     dfree(c, eb, 8 * S);
@@ -1684,9 +1694,9 @@ extern "C" fhs_status fhs_encrypt_asymmetric(fhs_context* c, fhs_public_key* pk,
     uint64_t* tmp = nullptr;
     HIPCHK(dalloc(c, &tmp, 24 * S), "encrypt");
     uint64_t *u = tmp, *e0 = tmp + S, *e1 = tmp + 2 * S;
-    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_TERNARY, stream_key(pk->seed, stream_id(ST_ENC_ASYM, ctr, 0)), u, l), "encrypt");
-    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(pk->seed, stream_id(ST_ENC_ASYM, ctr, 1)), e0, l), "encrypt");
-    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, stream_key(pk->seed, stream_id(ST_ENC_ASYM, ctr, 2)), e1, l), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_TERNARY, pk->rng, stream_id(ST_ENC_ASYM, ctr, 0), u, l), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, pk->rng, stream_id(ST_ENC_ASYM, ctr, 1), e0, l), "encrypt");
+    HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, pk->rng, stream_id(ST_ENC_ASYM, ctr, 2), e1, l), "encrypt");
     HIPCHK(fhs::launch_encrypt_combine(c->T, 1, ct->d, ct->d + S, pk->pk, pk->pk + SL, u, e0, e1, pt->d, l, c->st),
            "encrypt");
     dfree(c, tmp, 24 * S);
@@ -2350,8 +2360,7 @@ extern "C" fhs_status fhs_random_plaintexts(fhs_context* c, uint64_t seed, int c
         fhs_status s = new_pt(c, ci, scale, &pt);
         if (s != FHS_OK) return s;
         outs[k] = pt;
-        HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, stream_key(seed, (7ull << 56) | (uint64_t)k), pt->d, pt->l, 0,
-                                  c->st), "random_plaintexts");
+        HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_TESTDATA, PrfKey{}, sm64(seed ^ sm64((7ull << 56) | (uint64_t)k)), pt->d, pt->l, c->st), "random_plaintexts");
     }
     return bo.keep(FHS_OK);
 }

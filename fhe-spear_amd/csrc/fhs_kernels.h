@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+struct PrfKey;   // fhs_modarith.h (ChaCha20 key of the secret-randomness PRF)
+
 namespace fhs {
 
 typedef uint64_t u64;
@@ -95,7 +97,10 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
                          double scale, u64* const* outs_dev, int l, hipStream_t st,
                          double* coef_scratch = nullptr);
-hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int prime_base, hipStream_t st);
+// SAMPLE_UNIFORM / TERNARY / CBD draw from the ChaCha20 PRF stream (K, sid); SAMPLE_SEEDED expands
+// the public seed `sid` (switching-key a_j); SAMPLE_TESTDATA is the non-secret SplitMix64 uniform of
+// random_plaintexts (K unused)
+hipError_t launch_sample(const DevTables& T, int mode, const ::PrfKey& K, u64 sid, u64* out, int l, hipStream_t st);
 // b_j = e - a_j s + [limb in digit j] (P mod q) s_new  (switching-key component 0 of digit j)
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* b_out, const u64* a, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st);
@@ -126,6 +131,6 @@ hipError_t launch_encode_int128(const DevTables& T, const int64_t* hi, const u64
                                 int l, hipStream_t st);
 
 enum EltOp { OP_ADD = 0, OP_SUB = 1, OP_NEG = 2, OP_MULP = 3, OP_ADDP = 4, OP_SUBP = 5, OP_SUBNEG = 6 };
-enum SampleMode { SAMPLE_UNIFORM = 0, SAMPLE_TERNARY = 1, SAMPLE_CBD = 2, SAMPLE_SEEDED = 3 };
+enum SampleMode { SAMPLE_UNIFORM = 0, SAMPLE_TERNARY = 1, SAMPLE_CBD = 2, SAMPLE_SEEDED = 3, SAMPLE_TESTDATA = 4 };
 
 }  // namespace fhs

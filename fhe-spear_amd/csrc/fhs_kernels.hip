@@ -1662,11 +1662,13 @@ size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
 
 
 // ============================================================================ sampling / keys
-__device__ __forceinline__ u64 rnd(u64 key, u64 ctr) { return sm64(key ^ sm64(ctr ^ 0xD1B54A32D192ED03ULL)); }
+__device__ __forceinline__ u64 rnd_testdata(u64 key, u64 ctr) { return sm64(key ^ sm64(ctr ^ 0xD1B54A32D192ED03ULL)); }
 
-// mode 0: uniform mod q_i directly (NTT-domain sample); 1: ternary; 2: CBD(21) -- small values
-// replicated over limbs in coefficient form (caller runs the forward NTT)
-__global__ void k_sample(DevTables T, int mode, u64 key, u64* out, int l) {
+// SAMPLE_UNIFORM: uniform mod q_i in the NTT domain from 128 PRF bits (block i N + n, bias < 2^-67);
+// SAMPLE_TERNARY / SAMPLE_CBD: one small value per coefficient (block n), replicated over the limbs
+// in coefficient form (the caller runs the forward NTT); SAMPLE_SEEDED: public a_j expansion of the
+// seed `sid`; SAMPLE_TESTDATA: SplitMix64 uniform (random_plaintexts, not secret)
+__global__ void k_sample(DevTables T, int mode, PrfKey K, u64 sid, u64* out, int l) {
     const int N = T.N;
     const size_t S = (size_t)l * N;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
@@ -1674,12 +1676,17 @@ __global__ void k_sample(DevTables T, int mode, u64 key, u64* out, int l) {
         const PrimeK& P = PK(T, i);
         u64 v;
         if (mode == SAMPLE_UNIFORM) {
-            const u64 ctr = 2 * ((u64)i * N + n);
-            v = reduce128(rnd(key, ctr + 1), rnd(key, ctr), P);
+            u64 hi, lo;
+            prf128(K, sid, (uint32_t)idx, hi, lo);
+            v = reduce128(lo, hi, P);
         } else if (mode == SAMPLE_SEEDED) {
-            v = seeded_uniform_x(key + seeded_ctr_mix(i, n), P.q, 64 - __clzll(P.q));
+            v = seeded_uniform_x(sid + seeded_ctr_mix(i, n), P.q, 64 - __clzll(P.q));
+        } else if (mode == SAMPLE_TESTDATA) {
+            const u64 ctr = 2 * ((u64)i * N + n);
+            v = reduce128(rnd_testdata(sid, ctr + 1), rnd_testdata(sid, ctr), P);
         } else {
-            const u64 r = rnd(key, (u64)n);
+            u64 r, unused;
+            prf128(K, sid, (uint32_t)n, r, unused);
             long long s;
             if (mode == SAMPLE_TERNARY) {
                 const u64 t = r % 3;
@@ -1692,8 +1699,8 @@ __global__ void k_sample(DevTables T, int mode, u64 key, u64* out, int l) {
         out[idx] = v;
     }
 }
-hipError_t launch_sample(const DevTables& T, int mode, u64 key, u64* out, int l, int, hipStream_t st) {
-    hipLaunchKernelGGL(k_sample, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, mode, key, out, l);
+hipError_t launch_sample(const DevTables& T, int mode, const PrfKey& K, u64 sid, u64* out, int l, hipStream_t st) {
+    hipLaunchKernelGGL(k_sample, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, mode, K, sid, out, l);
     return hipGetLastError();
 }
 

@@ -156,7 +156,52 @@ __device__ __forceinline__ void acc3_fold(u128& c, Acc3& a) {
     a = Acc3{0, 0, 0};
 }
 
-// SplitMix64 (the sampling spec shared with oracle/ckks_oracle.c ock_splitmix64).
+// ---- secret randomness: ChaCha20 (RFC 8439 §2.3) as a PRF keyed by a 256-bit secret (DESIGN.md
+// §Sampling; shared with oracle/ckks_oracle.c ock_chacha20_block).  Stream `sid` (a 64-bit domain
+// label: kind, Galois element, digit, encryption counter) is the 96-bit nonce (lo32, hi32, "FHS1"),
+// the block counter indexes the coefficient.  Everything secret (s, errors, encryption masks) and
+// every public value derived from the secret key (the switching keys' a_j seeds, the public key's
+// a) is a PRF output, so publishing it reveals nothing about the key.
+struct PrfKey {
+    uint32_t k[8];
+};
+#define FHS_ROTL32(v, n) (((v) << (n)) | ((v) >> (32 - (n))))
+#define FHS_QR(a, b, c, d)                  \
+    a += b; d ^= a; d = FHS_ROTL32(d, 16);  \
+    c += d; b ^= c; b = FHS_ROTL32(b, 12);  \
+    a += b; d ^= a; d = FHS_ROTL32(d, 8);   \
+    c += d; b ^= c; b = FHS_ROTL32(b, 7);
+__host__ __device__ __forceinline__ void chacha20_block(const PrfKey& K, uint32_t ctr, uint32_t n0, uint32_t n1,
+                                                         uint32_t n2, uint32_t out[16]) {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, K.k[0], K.k[1], K.k[2], K.k[3],
+                      K.k[4],      K.k[5],      K.k[6],      K.k[7],      ctr,    n0,     n1,     n2};
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = s[i];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        FHS_QR(x[0], x[4], x[8], x[12]) FHS_QR(x[1], x[5], x[9], x[13])
+        FHS_QR(x[2], x[6], x[10], x[14]) FHS_QR(x[3], x[7], x[11], x[15])
+        FHS_QR(x[0], x[5], x[10], x[15]) FHS_QR(x[1], x[6], x[11], x[12])
+        FHS_QR(x[2], x[7], x[8], x[13]) FHS_QR(x[3], x[4], x[9], x[14])
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + s[i];
+}
+#undef FHS_QR
+#undef FHS_ROTL32
+constexpr uint32_t kPrfTag = 0x31534846u;   // "FHS1"
+// first two 64-bit words of block `ctr` of stream `sid`
+__host__ __device__ __forceinline__ void prf128(const PrfKey& K, u64 sid, uint32_t ctr, u64& w0, u64& w1) {
+    uint32_t o[16];
+    chacha20_block(K, ctr, (uint32_t)sid, (uint32_t)(sid >> 32), kPrfTag, o);
+    w0 = (u64)o[0] | ((u64)o[1] << 32);
+    w1 = (u64)o[2] | ((u64)o[3] << 32);
+}
+
+// SplitMix64 (the sampling spec shared with oracle/ckks_oracle.c ock_splitmix64): public
+// expansion of a switching key's a_j from its seed (regenerated inside the key inner product, where
+// a ChaCha block per coefficient would cost more than the key bytes it saves) and test data.
 __host__ __device__ __forceinline__ u64 sm64(u64 x) {
     x += 0x9E3779B97F4A7C15ULL;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;

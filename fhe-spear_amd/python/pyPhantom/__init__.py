@@ -34,6 +34,33 @@ _LIB_CANDIDATES = [
 ]
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7,
+    but libtorch_hip asks for it as `libamdhip64.so`, so the loader never matches it against
+    /opt/rocm's copy).  When this library loads first it binds /opt/rocm's runtime, a later
+    `import torch` loads a second runtime, and torch.cuda then reports "No HIP GPUs are available"
+    -- while the reference callers import torch first (fhe_common.py:5, bg:6) and so share torch's.
+    Loading torch's runtime here (if torch is installed; torch itself is not imported) makes both
+    orders bind the same one.  FHESPEAR_HIP_RUNTIME=system keeps /opt/rocm's."""
+    if os.environ.get("FHESPEAR_HIP_RUNTIME", "torch") != "torch":
+        return None
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    rt = Path(list(spec.submodule_search_locations)[0]) / "lib" / "libamdhip64.so"
+    if not rt.is_file():
+        return None
+    C.CDLL(str(rt), mode=C.RTLD_GLOBAL)
+    return str(rt)
+
+
+HIP_RUNTIME = _share_torch_hip_runtime()
+
+
 def _load():
     for p in _LIB_CANDIDATES:
         if p and Path(p).is_file():
@@ -63,7 +90,7 @@ _SIGS = {
     "fhs_context_galois_elts": (C.c_int, [_vp, _u64p]),
     "fhs_synchronize": (C.c_int, [_vp]),
     "fhs_memory_in_use": (C.c_int, [_vp, _u64p]),
-    "fhs_secret_key_create": (C.c_int, [_vp, _u64, C.POINTER(_vp)]),
+    "fhs_secret_key_create": (C.c_int, [_vp, C.c_char_p, C.POINTER(_vp)]),
     "fhs_secret_key_destroy": (C.c_int, [_vp]),
     "fhs_gen_public_key": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     "fhs_gen_relin_key": (C.c_int, [_vp, _vp, C.POINTER(_vp)]),
@@ -478,18 +505,22 @@ def _fresh_seed():
     s = os.environ.get("FHESPEAR_SEED", "").strip()
     if s:
         return int(s, 0)
-    return int.from_bytes(os.urandom(8), "little")
+    return int.from_bytes(os.urandom(32), "little")
 
 
 class secret_key:
-    """pb:100-110 PhantomSecretKey.  `seed` (extension) makes key generation and encryption
-    deterministic; by default it comes from FHESPEAR_SEED or os.urandom."""
+    """pb:100-110 PhantomSecretKey.  All secret randomness (s, errors, encryption masks) is drawn
+    from ChaCha20 keyed by 256 bits: by default os.urandom(32) (or
+    FHESPEAR_SEED); `seed` (extension, an integer < 2^256, its 32 little-endian bytes are the key)
+    makes key generation and encryption deterministic for tests."""
 
     def __init__(self, ctx, seed=None):
         self._ctx = ctx
         self.seed = _fresh_seed() if seed is None else int(seed)
+        if not 0 <= self.seed < 1 << 256:
+            raise ValueError("secret_key: seed must be an integer in [0, 2^256)")
         h = _vp()
-        _check(_lib.fhs_secret_key_create(ctx._h, self.seed, C.byref(h)), "secret_key")
+        _check(_lib.fhs_secret_key_create(ctx._h, self.seed.to_bytes(32, "little"), C.byref(h)), "secret_key")
         self._h = h
 
     def __del__(self):

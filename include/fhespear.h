@@ -70,8 +70,10 @@ fhs_status fhs_synchronize(fhs_context* ctx);
 fhs_status fhs_memory_in_use(fhs_context* ctx, uint64_t* bytes);
 
 /* ---- keys (pb:100-124) ---- */
-/* pb:100 secret_key(ctx).  Sampling is deterministic in `seed`. */
-fhs_status fhs_secret_key_create(fhs_context* ctx, uint64_t seed, fhs_secret_key** out);
+/* pb:100 secret_key(ctx).  All secret randomness is ChaCha20 keyed by key32:
+ * deterministic for a caller-supplied key (tests: the integer seed, 32 bytes little-endian). */
+fhs_status fhs_secret_key_create(fhs_context* ctx, const uint8_t* key32 /* 32 bytes, NULL: /dev/urandom */,
+                                 fhs_secret_key** out);
 fhs_status fhs_secret_key_destroy(fhs_secret_key* sk);
 fhs_status fhs_gen_public_key(fhs_context* ctx, fhs_secret_key* sk, fhs_public_key** out);      /* pb:102 */
 fhs_status fhs_gen_relin_key(fhs_context* ctx, fhs_secret_key* sk, fhs_relin_key** out);        /* pb:103 */

@@ -38,10 +38,45 @@ uint64_t ock_splitmix64(uint64_t x) {
     x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
     return x ^ (x >> 31);
 }
-uint64_t ock_stream_key(uint64_t seed, uint64_t stream) { return ock_splitmix64(seed ^ ock_splitmix64(stream)); }
 uint64_t ock_rnd(uint64_t key, uint64_t ctr) { return ock_splitmix64(key ^ ock_splitmix64(ctr ^ 0xD1B54A32D192ED03ULL)); }
 
-enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6 };
+/* ChaCha20 block function, RFC 8439 §2.3 (state: constants, 8 key words, counter, 3 nonce words;
+ * 20 rounds as 10 column + diagonal double rounds; output = rounds(state) + state) */
+#define ROTL32(v, n) (((v) << (n)) | ((v) >> (32 - (n))))
+#define QROUND(a, b, c, d) do { \
+    a += b; d ^= a; d = ROTL32(d, 16); c += d; b ^= c; b = ROTL32(b, 12); \
+    a += b; d ^= a; d = ROTL32(d, 8);  c += d; b ^= c; b = ROTL32(b, 7); } while (0)
+void ock_chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]) {
+    uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 8; i++) st[4 + i] = key[i];
+    st[12] = counter; st[13] = nonce[0]; st[14] = nonce[1]; st[15] = nonce[2];
+    uint32_t x[16];
+    memcpy(x, st, sizeof x);
+    for (int r = 0; r < 10; r++) {
+        QROUND(x[0], x[4], x[8], x[12]); QROUND(x[1], x[5], x[9], x[13]);
+        QROUND(x[2], x[6], x[10], x[14]); QROUND(x[3], x[7], x[11], x[15]);
+        QROUND(x[0], x[5], x[10], x[15]); QROUND(x[1], x[6], x[11], x[12]);
+        QROUND(x[2], x[7], x[8], x[13]); QROUND(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; i++) out[i] = x[i] + st[i];
+}
+/* The secret-randomness PRF: block `ctr` of stream `sid` under the 32-byte key
+ * (little-endian words), nonce (lo32 sid, hi32 sid, "FHS1"); w0/w1 = its first two 64-bit words. */
+typedef struct { uint32_t k[8]; } prf_key;
+static prf_key prf_key_from_bytes(const uint8_t* b) {
+    prf_key K;
+    for (int w = 0; w < 8; w++)
+        K.k[w] = (uint32_t)b[4 * w] | ((uint32_t)b[4 * w + 1] << 8) | ((uint32_t)b[4 * w + 2] << 16) | ((uint32_t)b[4 * w + 3] << 24);
+    return K;
+}
+static void prf128(const prf_key* K, uint64_t sid, uint32_t ctr, uint64_t* w0, uint64_t* w1) {
+    uint32_t nonce[3] = {(uint32_t)sid, (uint32_t)(sid >> 32), 0x31534846u}, o[16];
+    ock_chacha20_block(K->k, ctr, nonce, o);
+    *w0 = (uint64_t)o[0] | ((uint64_t)o[1] << 32);
+    *w1 = (uint64_t)o[2] | ((uint64_t)o[3] << 32);
+}
+
+enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6, ST_PK_RNG = 7 };
 static uint64_t stream_id(uint64_t kind, uint64_t a, uint64_t b) { return (kind << 56) | (a << 16) | b; }
 
 /* ------------------------------------------------------------------ modular helpers */
@@ -615,11 +650,13 @@ void ock_bsgs_loop(const ock_ctx* c, const uint64_t* const* baby, const uint64_t
 /* ------------------------------------------------------------------ sampling */
 static uint64_t reduce128(uint64_t hi, uint64_t lo, uint64_t q) { return (uint64_t)((((u128)hi << 64) | lo) % q); }
 
-static void sample_uniform_ntt(const ock_ctx* c, uint64_t key, int pi, uint64_t* dst) {
+/* uniform mod q_i in the NTT domain: (w0 2^64 + w1) mod q from block pi N + n (bias < 2^-67) */
+static void sample_uniform_ntt(const ock_ctx* c, const prf_key* K, uint64_t sid, int pi, uint64_t* dst) {
     uint64_t N = c->N, q = c->q[pi];
     for (uint64_t n = 0; n < N; n++) {
-        uint64_t ctr = 2 * ((uint64_t)pi * N + n);
-        dst[n] = reduce128(ock_rnd(key, ctr), ock_rnd(key, ctr + 1), q);
+        uint64_t w0, w1;
+        prf128(K, sid, (uint32_t)((uint64_t)pi * N + n), &w0, &w1);
+        dst[n] = reduce128(w0, w1, q);
     }
 }
 /* switching-key `a` components: exactly uniform by rejection from the top bits of one SplitMix64
@@ -637,12 +674,18 @@ uint64_t ock_seeded_uniform(uint64_t key, int pi, uint64_t n, uint64_t q) {
 static void sample_uniform_seeded(const ock_ctx* c, uint64_t key, int pi, uint64_t* dst) {
     for (uint64_t n = 0; n < c->N; n++) dst[n] = ock_seeded_uniform(key, pi, n, c->q[pi]);
 }
-static void sample_ternary(const ock_ctx* c, uint64_t key, int64_t* dst) {
-    for (uint64_t n = 0; n < c->N; n++) { uint64_t t = ock_rnd(key, n) % 3; dst[n] = t == 2 ? -1 : (int64_t)t; }
+/* small samplers: 64 PRF bits (w0 of block n) per coefficient */
+static uint64_t prf_small(const prf_key* K, uint64_t sid, uint64_t n) {
+    uint64_t w0, w1;
+    prf128(K, sid, (uint32_t)n, &w0, &w1);
+    return w0;
 }
-static void sample_cbd(const ock_ctx* c, uint64_t key, int64_t* dst) {
+static void sample_ternary(const ock_ctx* c, const prf_key* K, uint64_t sid, int64_t* dst) {
+    for (uint64_t n = 0; n < c->N; n++) { uint64_t t = prf_small(K, sid, n) % 3; dst[n] = t == 2 ? -1 : (int64_t)t; }
+}
+static void sample_cbd(const ock_ctx* c, const prf_key* K, uint64_t sid, int64_t* dst) {
     for (uint64_t n = 0; n < c->N; n++) {
-        uint64_t v = ock_rnd(key, n);
+        uint64_t v = prf_small(K, sid, n);
         dst[n] = (int64_t)__builtin_popcountll(v & 0x1FFFFFULL) - (int64_t)__builtin_popcountll((v >> 21) & 0x1FFFFFULL);
     }
 }
@@ -652,23 +695,24 @@ static void small_to_ntt(const ock_ctx* c, const int64_t* s, int pi, uint64_t* d
     ock_ntt_fwd(c, dst, pi);
 }
 
-void ock_gen_secret(const ock_ctx* c, uint64_t seed, uint64_t* s_ntt) {
+void ock_gen_secret(const ock_ctx* c, const uint8_t* key32, uint64_t* s_ntt) {
+    prf_key K = prf_key_from_bytes(key32);
     int64_t* s = (int64_t*)malloc(8 * c->N);
-    sample_ternary(c, ock_stream_key(seed, stream_id(ST_SECRET, 0, 0)), s);
+    sample_ternary(c, &K, stream_id(ST_SECRET, 0, 0), s);
     for (int i = 0; i < c->K; i++) small_to_ntt(c, s, i, s_ntt + (size_t)i * c->N);
     free(s);
 }
 
 /* key_j = (-a_j s + e_j + [i in digit j] (P mod q_i) s_new,  a_j) over all L0+P limbs */
-void ock_gen_switch_key(const ock_ctx* c, uint64_t seed, uint64_t stream_base,
+void ock_gen_switch_key(const ock_ctx* c, const uint8_t* key32, uint64_t stream_base,
                         const uint64_t* s_ntt, const uint64_t* snew, uint64_t* key) {
+    prf_key PK = prf_key_from_bytes(key32);
     uint64_t N = c->N; int K = c->K, P = c->P, L0 = c->L0;
     int dnum = (L0 + P - 1) / P;
     int64_t* e = (int64_t*)malloc(8 * N); uint64_t* et = (uint64_t*)malloc(8 * N);
     for (int j = 0; j < dnum; j++) {
-        uint64_t ka = ock_stream_key(seed, stream_base | (uint64_t)(2 * j));
-        uint64_t ke = ock_stream_key(seed, stream_base | (uint64_t)(2 * j + 1));
-        sample_cbd(c, ke, e);
+        uint64_t ka = prf_small(&PK, stream_base | (uint64_t)(2 * j), 0);   /* public seed of a_j */
+        sample_cbd(c, &PK, stream_base | (uint64_t)(2 * j + 1), e);
         for (int i = 0; i < K; i++) {
             uint64_t q = c->q[i];
             uint64_t* k0 = key + (((size_t)j * 2 + 0) * K + i) * N;
@@ -689,57 +733,65 @@ void ock_gen_switch_key(const ock_ctx* c, uint64_t seed, uint64_t stream_base,
     free(e); free(et);
 }
 
-void ock_gen_galois_key(const ock_ctx* c, uint64_t seed, const uint64_t* s_ntt, uint64_t elt, uint64_t* key) {
+void ock_gen_galois_key(const ock_ctx* c, const uint8_t* key32, const uint64_t* s_ntt, uint64_t elt, uint64_t* key) {
     uint64_t N = c->N;
     uint64_t* sn = (uint64_t*)malloc(8 * N * c->K);
     for (int i = 0; i < c->K; i++) ock_apply_galois_ntt(c, s_ntt + (size_t)i * N, sn + (size_t)i * N, elt);
-    ock_gen_switch_key(c, seed, stream_id(ST_GALOIS, elt, 0), s_ntt, sn, key);
+    ock_gen_switch_key(c, key32, stream_id(ST_GALOIS, elt, 0), s_ntt, sn, key);
     free(sn);
 }
-void ock_gen_relin_key(const ock_ctx* c, uint64_t seed, const uint64_t* s_ntt, uint64_t* key) {
+void ock_gen_relin_key(const ock_ctx* c, const uint8_t* key32, const uint64_t* s_ntt, uint64_t* key) {
     uint64_t N = c->N;
     uint64_t* s2 = (uint64_t*)malloc(8 * N * c->K);
     for (int i = 0; i < c->K; i++)
         for (uint64_t n = 0; n < N; n++) s2[(size_t)i * N + n] = mulmod(s_ntt[(size_t)i * N + n], s_ntt[(size_t)i * N + n], c->q[i]);
-    ock_gen_switch_key(c, seed, stream_id(ST_RELIN, 0, 0), s_ntt, s2, key);
+    ock_gen_switch_key(c, key32, stream_id(ST_RELIN, 0, 0), s_ntt, s2, key);
     free(s2);
 }
-void ock_gen_public_key(const ock_ctx* c, uint64_t seed, const uint64_t* s_ntt, uint64_t* pk) {
+void ock_gen_public_key(const ock_ctx* c, const uint8_t* key32, const uint64_t* s_ntt, uint64_t* pk) {
     uint64_t N = c->N; int L0 = c->L0;
-    uint64_t ka = ock_stream_key(seed, stream_id(ST_PUBKEY, 0, 0)), ke = ock_stream_key(seed, stream_id(ST_PUBKEY, 0, 1));
+    prf_key K = prf_key_from_bytes(key32);
     int64_t* e = (int64_t*)malloc(8 * N); uint64_t* et = (uint64_t*)malloc(8 * N);
-    sample_cbd(c, ke, e);
+    sample_cbd(c, &K, stream_id(ST_PUBKEY, 0, 1), e);
     for (int i = 0; i < L0; i++) {
         uint64_t q = c->q[i]; uint64_t* p0 = pk + (size_t)i * N; uint64_t* p1 = pk + ((size_t)L0 + i) * N;
-        sample_uniform_ntt(c, ka, i, p1);
+        sample_uniform_ntt(c, &K, stream_id(ST_PUBKEY, 0, 0), i, p1);
         small_to_ntt(c, e, i, et);
         for (uint64_t n = 0; n < N; n++) p0[n] = submod(et[n], mulmod(p1[n], s_ntt[(size_t)i * N + n], q), q);
     }
     free(e); free(et);
 }
-void ock_encrypt_symmetric(const ock_ctx* c, uint64_t seed, uint64_t counter, const uint64_t* s_ntt,
+void ock_encrypt_symmetric(const ock_ctx* c, const uint8_t* key32, uint64_t counter, const uint64_t* s_ntt,
                            const uint64_t* pt, int l, uint64_t* ct) {
     uint64_t N = c->N; size_t S = (size_t)l * N;
-    uint64_t ka = ock_stream_key(seed, stream_id(ST_ENC_SYM, counter, 0));
-    uint64_t ke = ock_stream_key(seed, stream_id(ST_ENC_SYM, counter, 1));
+    prf_key K = prf_key_from_bytes(key32);
     int64_t* e = (int64_t*)malloc(8 * N); uint64_t* et = (uint64_t*)malloc(8 * N);
-    sample_cbd(c, ke, e);
+    sample_cbd(c, &K, stream_id(ST_ENC_SYM, counter, 1), e);
     for (int i = 0; i < l; i++) {
         uint64_t q = c->q[i]; uint64_t* c0 = ct + (size_t)i * N; uint64_t* c1 = ct + S + (size_t)i * N;
-        sample_uniform_ntt(c, ka, i, c1);
+        sample_uniform_ntt(c, &K, stream_id(ST_ENC_SYM, counter, 0), i, c1);
         small_to_ntt(c, e, i, et);
         for (uint64_t n = 0; n < N; n++)
             c0[n] = addmod(submod(et[n], mulmod(c1[n], s_ntt[(size_t)i * N + n], q), q), pt[(size_t)i * N + n], q);
     }
     free(e); free(et);
 }
-void ock_encrypt_asymmetric(const ock_ctx* c, uint64_t seed, uint64_t counter, const uint64_t* pk,
+/* the public key's encryption-mask key: 256 PRF bits (w0 of blocks 0..3) of stream ST_PK_RNG */
+void ock_pk_rng_key(const uint8_t* key32, uint8_t* rng32) {
+    prf_key K = prf_key_from_bytes(key32);
+    for (int w = 0; w < 4; w++) {
+        uint64_t v = prf_small(&K, stream_id(ST_PK_RNG, 0, 0), (uint64_t)w);
+        for (int b = 0; b < 8; b++) rng32[8 * w + b] = (uint8_t)(v >> (8 * b));
+    }
+}
+void ock_encrypt_asymmetric(const ock_ctx* c, const uint8_t* rng32, uint64_t counter, const uint64_t* pk,
                             const uint64_t* pt, int l, uint64_t* ct) {
     uint64_t N = c->N; size_t S = (size_t)l * N; int L0 = c->L0;
+    prf_key R = prf_key_from_bytes(rng32);
     int64_t* u = (int64_t*)malloc(8 * N); int64_t* e0 = (int64_t*)malloc(8 * N); int64_t* e1 = (int64_t*)malloc(8 * N);
-    sample_ternary(c, ock_stream_key(seed, stream_id(ST_ENC_ASYM, counter, 0)), u);
-    sample_cbd(c, ock_stream_key(seed, stream_id(ST_ENC_ASYM, counter, 1)), e0);
-    sample_cbd(c, ock_stream_key(seed, stream_id(ST_ENC_ASYM, counter, 2)), e1);
+    sample_ternary(c, &R, stream_id(ST_ENC_ASYM, counter, 0), u);
+    sample_cbd(c, &R, stream_id(ST_ENC_ASYM, counter, 1), e0);
+    sample_cbd(c, &R, stream_id(ST_ENC_ASYM, counter, 2), e1);
     uint64_t* ut = (uint64_t*)malloc(8 * N); uint64_t* t0 = (uint64_t*)malloc(8 * N); uint64_t* t1 = (uint64_t*)malloc(8 * N);
     for (int i = 0; i < l; i++) {
         uint64_t q = c->q[i];

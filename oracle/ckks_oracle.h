@@ -32,8 +32,11 @@ typedef struct ock_ctx ock_ctx;
 
 /* --- deterministic sampling spec (shared with libfhespear_hip) --- */
 uint64_t ock_splitmix64(uint64_t x);
-uint64_t ock_stream_key(uint64_t seed, uint64_t stream);
-uint64_t ock_rnd(uint64_t key, uint64_t ctr);
+uint64_t ock_rnd(uint64_t key, uint64_t ctr);   /* test data only (random plaintexts) */
+/* ChaCha20 block (RFC 8439 §2.3): the PRF all secret randomness is drawn from */
+void ock_chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]);
+/* the public key's encryption-mask key, derived from the secret key's 32 bytes */
+void ock_pk_rng_key(const uint8_t* key32, uint8_t* rng32);
 /* uniform residue mod q from (key, prime index, coefficient) by rejection (switching-key a_j) */
 uint64_t ock_seeded_uniform(uint64_t key, int pi, uint64_t n, uint64_t q);
 
@@ -86,16 +89,17 @@ void ock_relinearize(const ock_ctx* c, const uint64_t* ct3, const uint64_t* rlk,
 void ock_bsgs_loop(const ock_ctx* c, const uint64_t* const* baby, const uint64_t* const* pts,
                    const uint64_t* const* gkeys_by_giant, int G, int B, int D, int l, uint64_t* out);
 
-/* ---- keys & encryption (deterministic sampling) ---- */
-void ock_gen_secret(const ock_ctx* c, uint64_t seed, uint64_t* s_ntt /* L0+P limbs */);
-void ock_gen_switch_key(const ock_ctx* c, uint64_t seed, uint64_t stream_base,
+/* ---- keys & encryption (ChaCha20 PRF keyed by the secret key's 32 bytes; deterministic) ---- */
+void ock_gen_secret(const ock_ctx* c, const uint8_t* key32, uint64_t* s_ntt /* L0+P limbs */);
+void ock_gen_switch_key(const ock_ctx* c, const uint8_t* key32, uint64_t stream_base,
                         const uint64_t* s_ntt, const uint64_t* snew_ntt, uint64_t* key);
-void ock_gen_galois_key(const ock_ctx* c, uint64_t seed, const uint64_t* s_ntt, uint64_t elt, uint64_t* key);
-void ock_gen_relin_key(const ock_ctx* c, uint64_t seed, const uint64_t* s_ntt, uint64_t* key);
-void ock_gen_public_key(const ock_ctx* c, uint64_t seed, const uint64_t* s_ntt, uint64_t* pk /* 2 x L0 */);
-void ock_encrypt_symmetric(const ock_ctx* c, uint64_t seed, uint64_t counter, const uint64_t* s_ntt,
+void ock_gen_galois_key(const ock_ctx* c, const uint8_t* key32, const uint64_t* s_ntt, uint64_t elt, uint64_t* key);
+void ock_gen_relin_key(const ock_ctx* c, const uint8_t* key32, const uint64_t* s_ntt, uint64_t* key);
+void ock_gen_public_key(const ock_ctx* c, const uint8_t* key32, const uint64_t* s_ntt, uint64_t* pk /* 2 x L0 */);
+void ock_encrypt_symmetric(const ock_ctx* c, const uint8_t* key32, uint64_t counter, const uint64_t* s_ntt,
                            const uint64_t* pt, int l, uint64_t* ct);
-void ock_encrypt_asymmetric(const ock_ctx* c, uint64_t seed, uint64_t counter, const uint64_t* pk,
+/* rng32: ock_pk_rng_key of the secret key (the public key's own mask key) */
+void ock_encrypt_asymmetric(const ock_ctx* c, const uint8_t* rng32, uint64_t counter, const uint64_t* pk,
                             const uint64_t* pt, int l, uint64_t* ct);
 void ock_decrypt(const ock_ctx* c, const uint64_t* s_ntt, const uint64_t* ct, int ncomp, int l, uint64_t* pt);
 

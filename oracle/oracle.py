@@ -46,8 +46,8 @@ def lib():
         for name in ("ock_splitmix64",):
             getattr(L, name).restype = C.c_uint64
             getattr(L, name).argtypes = [C.c_uint64]
-        L.ock_stream_key.restype = C.c_uint64
-        L.ock_stream_key.argtypes = [C.c_uint64, C.c_uint64]
+        L.ock_chacha20_block.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.ock_pk_rng_key.argtypes = [C.c_char_p, C.c_char_p]
         L.ock_rnd.restype = C.c_uint64
         L.ock_rnd.argtypes = [C.c_uint64, C.c_uint64]
         vp = C.c_void_p
@@ -71,13 +71,13 @@ def lib():
         L.ock_seeded_uniform.restype = C.c_uint64
         L.ock_bsgs_loop.argtypes = [vp, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p),
                                     C.c_int, C.c_int, C.c_int, C.c_int, _u64p]
-        L.ock_gen_secret.argtypes = [vp, C.c_uint64, _u64p]
-        L.ock_gen_switch_key.argtypes = [vp, C.c_uint64, C.c_uint64, _u64p, _u64p, _u64p]
-        L.ock_gen_galois_key.argtypes = [vp, C.c_uint64, _u64p, C.c_uint64, _u64p]
-        L.ock_gen_relin_key.argtypes = [vp, C.c_uint64, _u64p, _u64p]
-        L.ock_gen_public_key.argtypes = [vp, C.c_uint64, _u64p, _u64p]
-        L.ock_encrypt_symmetric.argtypes = [vp, C.c_uint64, C.c_uint64, _u64p, _u64p, C.c_int, _u64p]
-        L.ock_encrypt_asymmetric.argtypes = [vp, C.c_uint64, C.c_uint64, _u64p, _u64p, C.c_int, _u64p]
+        L.ock_gen_secret.argtypes = [vp, C.c_char_p, _u64p]
+        L.ock_gen_switch_key.argtypes = [vp, C.c_char_p, C.c_uint64, _u64p, _u64p, _u64p]
+        L.ock_gen_galois_key.argtypes = [vp, C.c_char_p, _u64p, C.c_uint64, _u64p]
+        L.ock_gen_relin_key.argtypes = [vp, C.c_char_p, _u64p, _u64p]
+        L.ock_gen_public_key.argtypes = [vp, C.c_char_p, _u64p, _u64p]
+        L.ock_encrypt_symmetric.argtypes = [vp, C.c_char_p, C.c_uint64, _u64p, _u64p, C.c_int, _u64p]
+        L.ock_encrypt_asymmetric.argtypes = [vp, C.c_char_p, C.c_uint64, _u64p, _u64p, C.c_int, _u64p]
         L.ock_decrypt.argtypes = [vp, _u64p, _u64p, C.c_int, C.c_int, _u64p]
         L.ock_encode_complex.argtypes = [vp, _dblp, C.c_size_t, C.c_double, C.c_int, _u64p]
         L.ock_decode_complex.argtypes = [vp, _u64p, C.c_int, C.c_double, _dblp]
@@ -104,6 +104,30 @@ def centered_count(y, qs) -> int:
     y = np.ascontiguousarray(np.asarray(y, dtype=np.uint64))
     q = np.ascontiguousarray(np.asarray(qs, dtype=np.uint64))
     return int(lib().ock_centered_count_test(_p(y), _p(q), len(y)))
+
+
+def key_bytes(seed: int) -> bytes:
+    """Secret-key PRF key: the integer seed as 32 little-endian bytes (pyPhantom.secret_key)."""
+    return int(seed).to_bytes(32, "little")
+
+
+def chacha20_block(key: bytes, counter: int, nonce: bytes) -> bytes:
+    """ock_chacha20_block (RFC 8439 §2.3) on byte strings: 64 output bytes."""
+    k = (C.c_uint32 * 8)(*np.frombuffer(key, dtype="<u4").tolist())
+    n = (C.c_uint32 * 3)(*np.frombuffer(nonce, dtype="<u4").tolist())
+    out = (C.c_uint32 * 16)()
+    lib().ock_chacha20_block(k, counter, n, out)
+    return np.array(out[:], dtype="<u4").tobytes()
+
+
+def _sm64_for_tests(x: int) -> int:
+    return int(lib().ock_splitmix64(x))
+
+
+def pk_rng_key(key32: bytes) -> bytes:
+    out = C.create_string_buffer(32)
+    lib().ock_pk_rng_key(key32, out)
+    return out.raw
 
 
 def seeded_uniform(key: int, prime_idx: int, n: int, q: int) -> int:
@@ -268,40 +292,54 @@ class Oracle:
         lib().ock_bsgs_loop(self._h, BA, PA, KA, G, B, D, l, _p(out))
         return out
 
-    # --- keys / encryption
+    # --- keys / encryption.  `seed` is the secret key's PRF key as an integer (< 2^256), the same
+    # 32 little-endian bytes pyPhantom.secret_key(ctx, seed) hands to fhs_secret_key_create.
     def gen_secret(self, seed: int):
         s = np.empty((self.K, self.N), dtype=np.uint64)
-        lib().ock_gen_secret(self._h, seed, _p(s))
+        lib().ock_gen_secret(self._h, key_bytes(seed), _p(s))
         return s
 
     def key_shape(self):
         return (self.dnum, 2, self.K, self.N)
 
+    def switch_key_seeds(self, seed: int, stream_base: int):
+        """The public a_j seeds a switching key stores (one per digit): w0 of block 0 of stream
+        stream_base | 2j (fhs_host.hip gen_switch_key)."""
+        out = []
+        for j in range(self.dnum):
+            sid = stream_base | (2 * j)
+            blk = chacha20_block(key_bytes(seed), 0, (sid & 0xFFFFFFFF).to_bytes(4, "little") +
+                                 (sid >> 32).to_bytes(4, "little") + (0x31534846).to_bytes(4, "little"))
+            out.append(int.from_bytes(blk[:8], "little"))
+        return out
+
     def gen_galois_key(self, seed: int, s, elt: int):
         k = np.empty(self.key_shape(), dtype=np.uint64)
-        lib().ock_gen_galois_key(self._h, seed, _p(s), elt, _p(k))
+        lib().ock_gen_galois_key(self._h, key_bytes(seed), _p(s), elt, _p(k))
         return k
 
     def gen_relin_key(self, seed: int, s):
         k = np.empty(self.key_shape(), dtype=np.uint64)
-        lib().ock_gen_relin_key(self._h, seed, _p(s), _p(k))
+        lib().ock_gen_relin_key(self._h, key_bytes(seed), _p(s), _p(k))
         return k
 
     def gen_public_key(self, seed: int, s):
         pk = np.empty((2, self.L0, self.N), dtype=np.uint64)
-        lib().ock_gen_public_key(self._h, seed, _p(s), _p(pk))
+        lib().ock_gen_public_key(self._h, key_bytes(seed), _p(s), _p(pk))
         return pk
 
     def encrypt_symmetric(self, seed: int, counter: int, s, pt):
         l = pt.shape[0]
         ct = np.empty((2, l, self.N), dtype=np.uint64)
-        lib().ock_encrypt_symmetric(self._h, seed, counter, _p(s), _p(np.ascontiguousarray(pt)), l, _p(ct))
+        lib().ock_encrypt_symmetric(self._h, key_bytes(seed), counter, _p(s), _p(np.ascontiguousarray(pt)), l, _p(ct))
         return ct
 
     def encrypt_asymmetric(self, seed: int, counter: int, pk, pt):
+        """`seed`: the SECRET key's seed; the masks come from the public key's own PRF key
+        (pk_rng_key), as in fhs_gen_public_key."""
         l = pt.shape[0]
         ct = np.empty((2, l, self.N), dtype=np.uint64)
-        lib().ock_encrypt_asymmetric(self._h, seed, counter, _p(np.ascontiguousarray(pk)),
+        lib().ock_encrypt_asymmetric(self._h, pk_rng_key(key_bytes(seed)), counter, _p(np.ascontiguousarray(pk)),
                                      _p(np.ascontiguousarray(pt)), l, _p(ct))
         return ct
 

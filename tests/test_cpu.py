@@ -342,3 +342,49 @@ def test_seeded_key_sampler_spec(orc):
         for key in (0, 1, 0xDEADBEEFCAFEF00D):
             for pi, n in ((0, 0), (3, 1), (38, 16383), (5, 777)):
                 assert seeded_uniform(key, pi, n, q) == spec(key, pi, n, q)
+
+
+def test_chacha20_rfc8439_block_vector(orc):
+    """The secret-randomness PRF is ChaCha20: RFC 8439 §2.3.2 test vector
+    (key 00..1f, nonce 00:00:00:09:00:00:00:4a:00:00:00:00, block counter 1)."""
+    out = orc.chacha20_block(bytes(range(32)), 1, bytes.fromhex("000000090000004a00000000"))
+    assert out.hex() == ("10f1e7e4d13b5915500fdd1fa32071c4c7d1f4c733c068030422aa9ac3d46c4e"
+                         "d2826446079faa0914c2d705d98b02a2b5129cd1de164eb9cbd083e8a2503c4e")
+
+
+def _sm64_inverse(z):
+    """Inverse of SplitMix64's finaliser (the round-1 sampler), used to run the ADVICE r1 attack."""
+    M = (1 << 64) - 1
+
+    def unxorshift(x, k):
+        y = x
+        for _ in range(64 // k + 1):
+            y = x ^ (y >> k)
+        return y & M
+    z = unxorshift(z, 31)
+    z = (z * pow(0x94D049BB133111EB, -1, 1 << 64)) & M
+    z = unxorshift(z, 27)
+    z = (z * pow(0xBF58476D1CE4E5B9, -1, 1 << 64)) & M
+    z = unxorshift(z, 30)
+    return (z - 0x9E3779B97F4A7C15) & M
+
+
+def test_switching_key_seeds_do_not_reveal_the_secret_key(orc):
+    """round 1 stored each a_j seed as sm64(sk_seed ^ sm64(stream)), so inverting
+    SplitMix64 on a published key gave sk.  The seeds are now ChaCha20 outputs under the 256-bit
+    secret key: the same inversion yields nothing that regenerates s, and the key has 256 bits
+    (two keys sharing their low 64 bits differ)."""
+    from oracle.oracle import Oracle, _sm64_for_tests
+    N, primes, P = 1024, [int(q) for q in orc.create_coeff_modulus(1024, [40] * 4)], 1
+    o = Oracle(N, primes, P)
+    seed = 0x1234_5678_9ABC_DEF0_0FED_CBA9_8765_4321_1122_3344_5566_7788_99AA_BBCC_DDEE_FF00
+    s = o.gen_secret(seed)
+    elt = orc.galois_elt(1, N)
+    stream = (4 << 56) | (elt << 16)
+    assert _sm64_inverse(_sm64_for_tests(0x0123456789ABCDEF)) == 0x0123456789ABCDEF   # the inverse is right
+    seeds = o.switch_key_seeds(seed, stream)
+    for j, sj in enumerate(seeds):
+        guess = _sm64_inverse(sj) ^ _sm64_for_tests(stream | (2 * j))   # round-1 recovery
+        assert not np.array_equal(o.gen_secret(guess), s)
+    s_low = o.gen_secret(seed & ((1 << 64) - 1))
+    assert not np.array_equal(s_low, s)
