@@ -7,9 +7,9 @@ import numpy as np
 from oracle.oracle import Oracle, galois_elt
 
 
-def worker(N, primes, P, G, nr, nd, seed, barrier, out):
-    """Set up a context, a Galois key and random operands, wait for all workers, then time `nr`
-    rotations (oracle/ckks_oracle.c ock_rotate) and `nd` multiply_plain+add pairs."""
+def worker(N, primes, P, G, nr, nd, seed, barrier, out, reps=1):
+    """Set up a context, a Galois key and random operands, wait for all workers, then `reps` times
+    time `nr` rotations (oracle/ckks_oracle.c ock_rotate) and `nd` multiply_plain+add pairs."""
     L0 = len(primes) - P
     o = Oracle(N, primes, P)
     s = o.gen_secret(5 + seed)
@@ -18,12 +18,16 @@ def worker(N, primes, P, G, nr, nd, seed, barrier, out):
     ct = np.stack([np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)]) for _ in range(2)])
     pt = np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)])
     barrier.wait()
-    t0 = time.perf_counter()
-    for _ in range(nr):
-        o.rotate(ct, key, G)
-    t1 = time.perf_counter()
-    acc = o.multiply_plain(ct, pt)
-    for _ in range(nd - 1):
-        acc = o.add(acc, o.multiply_plain(ct, pt))
-    t2 = time.perf_counter()
-    out.put((t1 - t0, t2 - t1))
+    tr, td = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for _ in range(nr):
+            o.rotate(ct, key, G)
+        t1 = time.perf_counter()
+        acc = o.multiply_plain(ct, pt)
+        for _ in range(nd - 1):
+            acc = o.add(acc, o.multiply_plain(ct, pt))
+        t2 = time.perf_counter()
+        tr.append(t1 - t0)
+        td.append(t2 - t1)
+    out.put((tr, td))

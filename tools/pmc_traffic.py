@@ -10,6 +10,7 @@ import csv
 import collections
 import json
 import sys
+from pathlib import Path
 
 
 def load(path, counter):
@@ -36,7 +37,10 @@ def main():
                   "traffic_bytes_per_step": int(rd + wr), "launches_per_step": fn.get(k, 0) / steps}
     meta = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes)",
             "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes", "steps_executed": steps}
-    json.dump({"meta": meta, "kernels": res}, open(out, "w"), indent=1)
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench import kernel_source_hash
+    json.dump({"meta": meta, "kernel_source_sha256_16": kernel_source_hash(), "kernels": res}, open(out, "w"),
+              indent=1)
     for k, v in res.items():
         print(f"{k:22s} read {v['read_bytes_per_step'] / 1e9:7.3f} GB  write {v['write_bytes_per_step'] / 1e9:7.3f} GB per step")
 
