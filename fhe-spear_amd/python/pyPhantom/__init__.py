@@ -347,6 +347,15 @@ class context:
     def limbs(self, chain_index):
         return self.L0 + 1 - chain_index
 
+    def galois_elts(self):
+        """The Galois elements keys are made for (the params' set, or the SEAL/Phantom default
+        +-2^k steps and conjugation when none was set)."""
+        n, L0, P, ne = _u64(), C.c_int(), C.c_int(), C.c_int()
+        _check(_lib.fhs_context_info(self._h, C.byref(n), C.byref(L0), C.byref(P), C.byref(ne)), "context_info")
+        out = np.empty(ne.value, dtype=np.uint64)
+        _check(_lib.fhs_context_galois_elts(self._h, out.ctypes.data_as(_u64p)), "context_galois_elts")
+        return [int(e) for e in out]
+
 
 _default_ctx = None
 

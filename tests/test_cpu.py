@@ -388,3 +388,27 @@ def test_switching_key_seeds_do_not_reveal_the_secret_key(orc):
         assert not np.array_equal(o.gen_secret(guess), s)
     s_low = o.gen_secret(seed & ((1 << 64) - 1))
     assert not np.array_equal(s_low, s)
+
+
+@pytest.mark.parametrize("case", ["client_aided_n256", "ffn_replay_n256"])
+def test_recorded_reference_calls_replay_on_the_oracle(orc, case):
+    """The fixtures the GPU replay tests use (tests/test_golden_replay.py) are self-consistent on
+    the CPU: the oracle re-encodes every recorded plaintext to the recorded SHA-256, and re-running
+    each recorded BSGS call (baby steps bg:215-220 + loop bg:464-485) on its recorded input gives
+    the recorded output limbs."""
+    man = json.loads((GOLDEN / "manifest.json").read_text())["cases"][case]
+    z = np.load(GOLDEN / man["file"])
+    N, P, D = man["N"], man["P"], man["D"]
+    o = orc.Oracle(N, [int(q) for q in z["primes"]], P)
+    s = o.gen_secret(man["sk_seed"])
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    baby_keys = {b: o.gen_galois_key(man["sk_seed"], s, orc.galois_elt(b, N)) for b in range(1, G)}
+    giant_keys = [None] + [o.gen_galois_key(man["sk_seed"], s, orc.galois_elt(g * G, N)) for g in range(1, B)]
+    for i, c in enumerate(man["calls"]):
+        l = o.L0 + 1 - c["pt_level"]
+        pts = [o.encode(r, c["pt_scale"], l) for r in z[f"c{i}_rows"]]
+        assert hashlib.sha256(np.ascontiguousarray(np.stack(pts)).tobytes()).hexdigest() == c["pt_sha256"]
+        ct = z[f"c{i}_ct_in"]
+        baby = [ct] + [o.rotate(ct, baby_keys[b], b) for b in range(1, G)]
+        assert np.array_equal(o.bsgs_loop(baby, pts, giant_keys, G, B, D), z[f"c{i}_out"]), f"call {i}"
