@@ -259,6 +259,8 @@ struct fhs_context {
     // alloc.hip); ciphertexts and plaintexts come in a handful of sizes, so almost every allocation
     // after warm-up is a free-list pop.  Trimmed on out-of-memory, at context destruction and exit.
     std::unordered_map<size_t, std::vector<void*>> free_blocks;
+    // imported switching keys (fhs_*_keys_import): key -> its explicit a_j [dnum][K][N]
+    std::unordered_map<const void*, uint64_t*> key_a;
     size_t cached_bytes = 0;
     // bounded: a chain walks down the levels, so every level brings new sizes and the sizes of the
     // levels behind it go cold.  Over the cap, whole sizes are evicted least-recently-used first
@@ -343,6 +345,20 @@ static void ctx_release(fhs_context* c);
 static size_t key_words(const fhs_context* c) { return (size_t)c->dnum * c->K * c->N + (size_t)c->dnum; }
 // exported / oracle layout: [dnum][2][K][N]
 static size_t key_words_full(const fhs_context* c) { return (size_t)c->dnum * 2 * c->K * c->N; }
+static void dfree(fhs_context* c, void* p, size_t bytes);
+// an imported key's explicit a_j (null for generated keys, whose a_j are regenerated from seeds)
+static const uint64_t* key_akey(const fhs_context* c, const uint64_t* key) {
+    auto it = c->key_a.find(key);
+    return it == c->key_a.end() ? nullptr : it->second;
+}
+static void free_key(fhs_context* c, uint64_t* key) {
+    auto it = c->key_a.find(key);
+    if (it != c->key_a.end()) {
+        dfree(c, it->second, 8ull * c->dnum * c->K * c->N);
+        c->key_a.erase(it);
+    }
+    dfree(c, key, 8 * key_words(c));
+}
 
 static void ctx_sync(fhs_context* c) {
     hipStreamSynchronize(c->st);
@@ -688,7 +704,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
         }
     }
     // ---- ModDown tables
-    std::vector<uint64_t> md_intt((size_t)P * 4), md_hat((size_t)P * L0), md_pinv((size_t)3 * L0);
+    std::vector<uint64_t> md_intt((size_t)P * 4), md_hat((size_t)P * L0), md_pinv((size_t)4 * L0);
     for (int k = 0; k < P; ++k) {
         const int pi = L0 + k;
         const uint64_t p = primes[pi];
@@ -715,6 +731,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
         md_pinv[2 * i] = pinv;
         md_pinv[2 * i + 1] = h_shoup(pinv, q);
         md_pinv[2 * L0 + i] = pm;
+        md_pinv[3 * L0 + i] = P == 1 ? (primes[L0] >> 1) % q : 0;   // SEAL ModDown rounding (P = 1)
     }
     // ---- rescale tables: level l (limbs) drops q_{l-1}
     std::vector<uint64_t> rs((size_t)(L0 + 1) * L0 * 4, 0);
@@ -959,6 +976,16 @@ static fhs_status gen_switch_key(fhs_context* c, const PrfKey& K, uint64_t base,
 // [dnum][2][K][N] with the a_j regenerated from their seeds (the oracle's layout)
 static fhs_status export_switch_key(fhs_context* c, const uint64_t* key, uint64_t* host) {
     const size_t S = (size_t)c->K * c->N;
+    if (const uint64_t* akey = key_akey(c, key)) {   // imported: (b_j, a_j) as given
+        for (int j = 0; j < c->dnum; ++j) {
+            HIPCHK(hipMemcpyAsync(host + (size_t)j * 2 * S, key + (size_t)j * S, 8 * S, hipMemcpyDeviceToHost, c->st),
+                   "key export");
+            HIPCHK(hipMemcpyAsync(host + ((size_t)j * 2 + 1) * S, akey + (size_t)j * S, 8 * S, hipMemcpyDeviceToHost,
+                                  c->st), "key export");
+        }
+        HIPCHK(hipStreamSynchronize(c->st), "key export");
+        return FHS_OK;
+    }
     std::vector<uint64_t> seeds(c->dnum);
     HIPCHK(hipMemcpyAsync(seeds.data(), key + (size_t)c->dnum * S, 8 * seeds.size(), hipMemcpyDeviceToHost, c->st),
            "key export");
@@ -994,7 +1021,7 @@ extern "C" fhs_status fhs_gen_relin_key(fhs_context* c, fhs_secret_key* sk, fhs_
 extern "C" fhs_status fhs_relin_key_destroy(fhs_relin_key* rk) {
     if (!rk) return FHS_OK;
     fhs_context* c = rk->ctx;
-    { Guard g(c); flush(c); dfree(c, rk->key, 8 * key_words(c)); }
+    { Guard g(c); flush(c); free_key(c, rk->key); }
     delete rk;
     ctx_release(c);
     return FHS_OK;
@@ -1018,7 +1045,7 @@ extern "C" fhs_status fhs_create_galois_keys(fhs_context* c, fhs_secret_key* sk,
         fhs_status s = gen_switch_key(c, sk->key, stream_id(ST_GALOIS, elt, 0), sk->s, sn, &key);
         if (s != FHS_OK) {
             dfree(c, sn, 8ull * c->K * c->N);
-            for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
+            for (auto& kv : gk->keys) free_key(c, kv.second);
             delete gk;
             return s;
         }
@@ -1026,7 +1053,7 @@ extern "C" fhs_status fhs_create_galois_keys(fhs_context* c, fhs_secret_key* sk,
     }
     dfree(c, sn, 8ull * c->K * c->N);
     if (e != hipSuccess) {
-        for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
+        for (auto& kv : gk->keys) free_key(c, kv.second);
         delete gk;
         return hip_fail(e, "galois key generation");
     }
@@ -1040,7 +1067,7 @@ extern "C" fhs_status fhs_galois_keys_destroy(fhs_galois_keys* gk) {
     {
         Guard g(c);
         flush(c);
-        for (auto& kv : gk->keys) dfree(c, kv.second, 8 * key_words(c));
+        for (auto& kv : gk->keys) free_key(c, kv.second);
     }
     delete gk;
     ctx_release(c);
@@ -1073,6 +1100,109 @@ extern "C" fhs_status fhs_relin_key_export(fhs_context* c, const fhs_relin_key* 
     ENTER(c);
     if (!rk || !host) return fail(FHS_ERR_INVALID, "null argument");
     return export_switch_key(c, rk->key, host);
+}
+// ---- key import ("identical keys": a key set produced elsewhere, e.g. by SEAL, in the export layout)
+static bool canonical_limbs(const fhs_context* c, const uint64_t* host, int nlimbs, int limb0) {
+    for (int i = 0; i < nlimbs; ++i) {
+        const uint64_t q = c->q[(limb0 + i) % c->K];
+        const uint64_t* v = host + (size_t)i * c->N;
+        for (uint64_t n = 0; n < c->N; ++n)
+            if (v[n] >= q) return false;
+    }
+    return true;
+}
+// host [dnum][2][K][N] -> b_j in the key, a_j in a companion allocation (key_a)
+static fhs_status import_switch_key(fhs_context* c, const uint64_t* host, uint64_t** key_out) {
+    const size_t S = (size_t)c->K * c->N;
+    for (int j = 0; j < 2 * c->dnum; ++j)
+        if (!canonical_limbs(c, host + (size_t)j * S, c->K, 0))
+            return fail(FHS_ERR_INVALID, "key import: residues must be canonical (< q_i) in [dnum][2][K][N] order");
+    uint64_t *key = nullptr, *a = nullptr;
+    HIPCHK(dalloc(c, &key, 8 * key_words(c)), "key import");
+    hipError_t e = dalloc(c, &a, 8ull * c->dnum * S);
+    if (e != hipSuccess) { dfree(c, key, 8 * key_words(c)); return hip_fail(e, "key import"); }
+    for (int j = 0; j < c->dnum && e == hipSuccess; ++j) {
+        e = hipMemcpyAsync(key + (size_t)j * S, host + (size_t)j * 2 * S, 8 * S, hipMemcpyHostToDevice, c->st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(a + (size_t)j * S, host + ((size_t)j * 2 + 1) * S, 8 * S, hipMemcpyHostToDevice, c->st);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(key + (size_t)c->dnum * S, 0, 8 * c->dnum, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // pageable host source
+    if (e != hipSuccess) {
+        dfree(c, a, 8ull * c->dnum * S);
+        dfree(c, key, 8 * key_words(c));
+        return hip_fail(e, "key import");
+    }
+    c->key_a[key] = a;
+    *key_out = key;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_galois_keys_import(fhs_context* c, const uint64_t* elts, int n, const uint64_t* host,
+                                             fhs_galois_keys** out) {
+    ENTER(c);
+    if (!elts || n < 1 || !host || !out) return fail(FHS_ERR_INVALID, "galois_keys_import: bad args");
+    auto* gk = new fhs_galois_keys{c, {}};
+    for (int k = 0; k < n; ++k) {
+        if ((elts[k] & 1) == 0 || elts[k] >= 2 * c->N || gk->keys.count(elts[k])) {
+            for (auto& kv : gk->keys) free_key(c, kv.second);
+            delete gk;
+            return fail(FHS_ERR_INVALID, "galois_keys_import: invalid or repeated galois element");
+        }
+        uint64_t* key = nullptr;
+        fhs_status s = import_switch_key(c, host + (size_t)k * key_words_full(c), &key);
+        if (s != FHS_OK) {
+            for (auto& kv : gk->keys) free_key(c, kv.second);
+            delete gk;
+            return s;
+        }
+        gk->keys[elts[k]] = key;
+    }
+    ctx_retain(c);
+    *out = gk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_relin_key_import(fhs_context* c, const uint64_t* host, fhs_relin_key** out) {
+    ENTER(c);
+    if (!host || !out) return fail(FHS_ERR_INVALID, "null argument");
+    auto* rk = new fhs_relin_key{c, nullptr};
+    fhs_status s = import_switch_key(c, host, &rk->key);
+    if (s != FHS_OK) { delete rk; return s; }
+    ctx_retain(c);
+    *out = rk;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_secret_key_import(fhs_context* c, const uint64_t* host, fhs_secret_key** out) {
+    ENTER(c);
+    if (!host || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (!canonical_limbs(c, host, c->K, 0)) return fail(FHS_ERR_INVALID, "secret_key_import: residues must be < q_i");
+    PrfKey K{};
+    if (!os_random(K.k, sizeof(K.k))) return fail(FHS_ERR_INVALID, "secret_key_import: /dev/urandom unavailable");
+    auto* sk = new fhs_secret_key{c, nullptr, K, 0};   // fresh encryption randomness
+    hipError_t e = dalloc(c, &sk->s, 8ull * c->K * c->N);
+    if (e == hipSuccess) e = hipMemcpyAsync(sk->s, host, 8ull * c->K * c->N, hipMemcpyHostToDevice, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    if (e != hipSuccess) {
+        if (sk->s) dfree(c, sk->s, 8ull * c->K * c->N);
+        delete sk;
+        return hip_fail(e, "secret_key_import");
+    }
+    ctx_retain(c);
+    *out = sk;
+    return FHS_OK;
+}
+// key-switch convention of the context (fhs_kernels.h DevTables::ks_seal)
+extern "C" fhs_status fhs_context_set_key_switch_mode(fhs_context* c, int mode) {
+    ENTER(c);
+    if (mode != FHS_KS_EXACT && mode != FHS_KS_SEAL) return fail(FHS_ERR_INVALID, "key switch mode: 0 exact, 1 seal");
+    if (mode == FHS_KS_SEAL && c->P != 1)
+        return fail(FHS_ERR_INVALID, "key switch mode seal: SEAL's switch_key_inplace has one special prime (P = 1)");
+    c->T.ks_seal = mode == FHS_KS_SEAL;
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_context_key_switch_mode(const fhs_context* c, int* mode) {
+    if (!c || !mode) return fail(FHS_ERR_INVALID, "null argument");
+    *mode = c->T.ks_seal ? FHS_KS_SEAL : FHS_KS_EXACT;
+    return FHS_OK;
 }
 extern "C" fhs_status fhs_secret_key_export(fhs_context* c, const fhs_secret_key* sk, uint64_t* host) {
     ENTER(c);
@@ -1820,7 +1950,7 @@ extern "C" fhs_status fhs_relinearize(fhs_context* c, const fhs_ciphertext* a, c
     fhs_status s = new_ct(c, 2, a->ci, a->scale, &r);
     if (s != FHS_OK) return s;
     const size_t S = (size_t)a->l * c->N;
-    std::vector<KsItem> it{KsItem{a->d + 2 * S, a->d, a->d + S, rk->key, r->d, r->d + S, 1, 0}};
+    std::vector<KsItem> it{KsItem{a->d + 2 * S, a->d, a->d + S, rk->key, r->d, r->d + S, 1, 0, key_akey(c, rk->key)}};
     s = run_keyswitch(c, it, a->l);
     if (s != FHS_OK) return s;
     *out = r;
@@ -1899,7 +2029,8 @@ static fhs_status queue_rotation(fhs_context* c, const fhs_ciphertext* a, uint64
     fhs_status s = new_ct(c, 2, a->ci, a->scale, &r);
     if (s != FHS_OK) return s;
     const size_t S = (size_t)a->l * c->N;
-    c->pending.push_back(PendingRot{KsItem{a->d + S, a->d, nullptr, it->second, r->d, r->d + S, elt, 0}, r, a});
+    c->pending.push_back(PendingRot{KsItem{a->d + S, a->d, nullptr, it->second, r->d, r->d + S, elt, 0,
+                                           key_akey(c, it->second)}, r, a});
     c->pending_l = a->l;
     c->pending_refs.insert(r);
     c->pending_refs.insert(a);
@@ -1952,12 +2083,13 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     if (rescale && l < 2) return fail(FHS_ERR_LEVEL, "bsgs: no level left for the final rescale");
     if (giant_elts && giant_elts[0] != 1) return fail(FHS_ERR_INVALID, "linear_transform: giant group 0 must be the identity");
     HostTrace ht;
-    std::vector<const uint64_t*> keys(Beff, nullptr);
+    std::vector<const uint64_t*> keys(Beff, nullptr), akeys(Beff, nullptr);
     for (int g = 1; g < Beff; ++g) {
         const uint64_t elt = giant_elts ? giant_elts[g] : fhs_galois_elt_from_step(g * G, c->N);
         auto it = gk->keys.find(elt);
         if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "bsgs: galois key for a giant step is missing");
         keys[g] = it->second;
+        akeys[g] = key_akey(c, it->second);
     }
     const size_t S = (size_t)l * c->N;
     // pointer arrays -> device
@@ -1980,7 +2112,8 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     ht.mark("workspaces");
     const fhs::BsgsStreams ss{c->st, c->st_aux, c->bsgs_ev.data(), (int)c->bsgs_ev.size(), c->bsgs_chunks,
                               c->bsgs_split_h};
-    HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), giant_elts, inner, sum, ws, wsb, c->items_dev,
+    HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), akeys.data(), giant_elts, inner, sum, ws, wsb,
+                            c->items_dev,
                             c->stager, ss, tm),
            "bsgs");
     ht.mark("launch bsgs");

@@ -20,13 +20,17 @@ struct DevTables {
     const u64* modup_Q;       // [L0+1][dnum][K][2]  Q_S mod prime(t), ns*Q_S mod prime(t)
     const u64* md_intt;       // [P][4]  INTT constants with inv(P/p_k) folded in
     const u64* md_hat;        // [P][L0]  (P / p_k) mod q_i
-    const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup
+    const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup; then [L0] P mod q_i; then [L0] floor(p/2) mod q_i (P = 1)
     const u64* rescale;       // [L0+1][L0][4]  inv(q_{l-1}) mod q_i (+Shoup), half mod q_i, half
     const u64* pow2;          // [K][1088] 2^e mod q_i (exact double reduction)
     const double* enc_w;      // [N/2][2]  omega^-k, omega = exp(2 pi i / (N/2))   (GPU encoder FFT)
     const double* enc_twist;  // [N/2][2]  (2/N) zeta^-k, zeta = exp(i pi / N)
     const unsigned* enc_pos;  // [N/2]     rev_{log N - 1}((5^j mod 2N - 1) / 4): LDS slot of z_j
     int N, logN, L0, P, K, dnum;
+    // key-switch convention: 0 = exact centred ModUp, ModDown without rounding (hoistable; the
+    // default); 1 = SEAL's switch_key_inplace (P = 1): per-limb lift without centring, automorphism
+    // before the decomposition, ModDown rounded by adding floor(p/2)
+    int ks_seal;
 };
 
 // One key-switch of a batch: out = KS_key( galois_elt(a) ) + (galois_elt(add0), add1).
@@ -42,6 +46,7 @@ struct KsItem {
     u64* out1;           // l limbs
     u64 elt;             // galois element (1 = identity)
     u64 src;             // index of `a` in the distinct-input list
+    const u64* akey;     // imported key: its a_j [dnum][K][N] (null: a_j regenerated from the seeds)
 };
 
 // Optional per-kernel event timer (bench.py): rec(ctx, id, begin, stream) is called around launches.
@@ -90,8 +95,8 @@ size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
 // giant_elts (host, B entries, may be null): Galois element of giant group g (g >= 1); null means
 // 5^(g G) mod 2N (the BSGS matvec of bg:464-485).  Group 0 is never rotated.
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
-                       int l, const u64* const* keys_host, const u64* giant_elts, u64* inner, u64* out, u64* workspace,
-                       size_t ws_bytes, void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
+                       int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
+                       u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
 // CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
 // apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,

@@ -554,8 +554,8 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
         const int s0 = j * P_, ns = min(s0 + P_, l) - s0;
         const u64* yb = acoef + ((size_t)u * l + s0) * N + n;
         int v;
-        if (ns == 1) {
-            v = yb[0] > (PK(T, s0).q >> 1) ? 1 : 0;
+        if (ns == 1) {   // SEAL: the limb's residue in [0, q) is lifted as is
+            v = T.ks_seal ? 0 : (yb[0] > (PK(T, s0).q >> 1) ? 1 : 0);
         } else {
             const u64* R = T.modup_R + (((size_t)l * T.dnum + j) * P_) * 2;
             u64 lo = 0, ys[8], qs[8];
@@ -821,7 +821,8 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     for (int j = 0; j < dn; ++j) {
         const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
         acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * K * N)));
-        acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
+        acc3_mac(a1, v, split30(it.akey ? __builtin_nontemporal_load(it.akey + (size_t)j * K * N + (size_t)pt * N + n)
+                                        : seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
         if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
             acc3_fold(c0, a0);
             acc3_fold(c1, a1);
@@ -863,7 +864,8 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
         for (int j = 0; j < dn; ++j) {
             const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
             acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * K * N)));
-            acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, q, qb)));
+            acc3_mac(a1, v, split30(it.akey ? __builtin_nontemporal_load(it.akey + (size_t)j * K * N + (size_t)t * N + n)
+                                            : seeded_uniform_x(seeds[j] + cx, q, qb)));
             if ((j & 7) == 7) {
                 acc3_fold(c0, a0);
                 acc3_fold(c1, a1);
@@ -931,7 +933,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_giant_fused(DevTables T
         const u64 ep = mullo64x(e, r1) + mulhi64x(e, r0);
         const int n = tl + c * TH;
         const u64 b = __builtin_nontemporal_load(keyb + (size_t)j * K * N + n);
-        const u64 a = seeded_uniform_x(seeds[j] + seeded_ctr_mix(pt, n), q, qb);
+        const u64 a = it.akey ? __builtin_nontemporal_load(it.akey + (size_t)j * K * N + (size_t)pt * N + n)
+                              : seeded_uniform_x(seeds[j] + seeded_ctr_mix(pt, n), q, qb);
         const u64 pb = mullo64x(b, e) - mullo64x(mulhi64x(b, ep), q);
         const u64 pa = mullo64x(a, e) - mullo64x(mulhi64x(a, ep), q);
         if (lazy) {
@@ -1057,8 +1060,9 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ks_special_intt(DevTabl
     const u64* src = acc + (((size_t)r * 2 + comp) * E + l + k) * N;
     u64* dst = ycoef + (((size_t)r * 2 + comp) * P_ + k) * N;
     const u64* cst = T.md_intt + (size_t)k * 4;
+    const u64 p = P.q, half = T.ks_seal ? p >> 1 : 0;   // SEAL: + floor(p/2) turns the floor into rounding
     inv_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3],
-                               [&](int e) { return src[e]; }, [&](int e, u64 v) { dst[e] = v; });
+                               [&](int e) { return src[e]; }, [&](int e, u64 v) { dst[e] = csub(csub(v, p) + half, p); });
 }
 
 // (d) ModDown: out_c[i] = (acc_c[i] - NTT(conv_P->q_i(y_c))) * P^-1 (+ add_c)
@@ -1081,12 +1085,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
     const u64 q = P.q;
     const KsItem it = items[r];
     const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N;
+    const u64 halfq = T.ks_seal ? T.md_pinv[3 * T.L0 + i] : 0;   // SEAL rounding: - floor(p/2) mod q_i
 #pragma unroll 4
     for (int kk = 0; kk < 16; ++kk) {
         const int e = tid + kk * TH;
         u128 s = {0, 0};
         for (int k = 0; k < P_; ++k) mac128(s, y[(size_t)k * N + e], T.md_hat[(size_t)k * T.L0 + i]);
-        lds[lds_pad(e)] = reduce128(s.lo, s.hi, P);
+        lds[lds_pad(e)] = submod(reduce128(s.lo, s.hi, P), halfq, q);
     }
     __syncthreads();
     const RedU RU = redu(P);
@@ -1126,6 +1131,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     const KsItem it = items[r];
     const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N;
     const u64* tw = T.tw_fwd + (size_t)i * N * 2;
+    const u64 halfq = T.ks_seal ? T.md_pinv[3 * T.L0 + i] : 0;
     u64 w0, w0p;
     ld_tw(tw, 1, w0, w0p);
     u64 hi[16];
@@ -1156,6 +1162,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
                 acc3_fold(s, a3[z]);
                 x[z] = reduce128(s.lo, s.hi, RU);
             }
+            if (T.ks_seal) x[z] = submod(csub(x[z], q), halfq, q);   // SEAL rounding: - floor(p/2) mod q_i
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {   // global stage 0: (e, e + N/2)
@@ -1190,11 +1197,47 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     }
 }
 
-size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l) {
+static size_t ks_core_bytes(const DevTables& T, int R, int U, int l) {
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     // acoef | ext | acc | ycoef | centred counts (bytes, rounded up to words)
     return 8 * N * ((size_t)U * l + (size_t)U * dn * E + (size_t)R * 2 * E + (size_t)R * 2 * T.P) +
            ((size_t)U * dn * N + 7) / 8 * 8;
+}
+// SEAL convention: every item's input gets its own decomposition (U = R) and the permuted
+// ciphertexts [R][2][l][N] follow the core workspace
+size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l) {
+    if (!T.ks_seal) return ks_core_bytes(T, R, U, l);
+    return ks_core_bytes(T, R, R, l) + 8 * (size_t)R * 2 * l * T.N;
+}
+// SEAL's switch_key_inplace decomposes the automorphed ciphertext (the lift without centring does
+// not commute with the automorphism, so nothing is hoisted): items with elt != 1 are rewritten to
+// read galois_elt(c0), galois_elt(c1) materialised in `perm`, with elt = 1 and an input each.
+// seal_rewrite changes the host items; seal_permute (enqueued once the inputs exist) fills `perm`.
+static void seal_rewrite(const DevTables& T, KsItem* items, int R, const u64** uniq, int l, u64* perm) {
+    const size_t S = (size_t)l * T.N;
+    for (int r = 0; r < R; ++r) {
+        KsItem& it = items[r];
+        if (it.elt != 1) {
+            u64* pc = perm + (size_t)r * 2 * S;
+            it.a = pc + S;
+            if (it.add0) it.add0 = pc;
+            it.elt = 1;
+        }
+        uniq[r] = it.a;
+        it.src = (u64)r;
+    }
+}
+static hipError_t seal_permute(const DevTables& T, const KsItem* orig, int R, int l, u64* perm, hipStream_t st) {
+    const size_t S = (size_t)l * T.N;
+    for (int r = 0; r < R; ++r) {
+        const KsItem& it = orig[r];
+        if (it.elt == 1) continue;
+        u64* pc = perm + (size_t)r * 2 * S;
+        hipError_t e = launch_galois_perm(T, it.a, pc + S, l, it.elt, st);
+        if (e == hipSuccess && it.add0) e = launch_galois_perm(T, it.add0, pc, l, it.elt, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // INTT + centred ModUp per distinct input, then key inner product and special-limb INTT per item;
@@ -1249,6 +1292,19 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
     if (keyswitch_workspace_bytes(T, R, U, l) > ws_bytes) return hipErrorInvalidValue;
     const KsItem* it;
     const u64* const* uq;
+    std::vector<KsItem> sitems;
+    std::vector<const u64*> suniq;
+    if (T.ks_seal) {
+        sitems.assign(items_host, items_host + R);
+        suniq.resize(R);
+        u64* perm = ws + ks_core_bytes(T, R, R, l) / 8;
+        seal_rewrite(T, sitems.data(), R, suniq.data(), l, perm);
+        hipError_t pe = seal_permute(T, items_host, R, l, perm, st);
+        if (pe != hipSuccess) return pe;
+        items_host = sitems.data();
+        uniq_host = suniq.data();
+        U = R;
+    }
     hipError_t e = upload_items(items_host, R, uniq_host, U, items_dev, sg, &it, &uq);
     if (e != hipSuccess) return e;
     FHS_DISPATCH_LOGN(T.logN, {
@@ -1375,6 +1431,14 @@ __global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, con
             }
         }
         // chunks of rotations accumulate mod q: both sums are linear in the rotations
+        if (T.ks_seal) {   // SEAL rounding: each of the R conversions carries - floor(p/2) mod q_i
+            u128 h = {0, 0};
+            mac128(h, (u64)R, T.md_pinv[3 * T.L0 + i]);
+            const u64 rh = reduce128(h.lo, h.hi, P);
+            cs.lo = reduce128(cs.lo, cs.hi, P);
+            cs.hi = 0;
+            cs.lo = submod(cs.lo, rh, q);
+        }
         u64 cv = reduce128(cs.lo, cs.hi, P);
         u64 bv = bpart[((size_t)comp * E + i) * N + n];
         if (first) {
@@ -1520,17 +1584,18 @@ static bool giant_fused(const DevTables& T) {
         const char* e = getenv("FHESPEAR_GIANT_FUSED");
         return e && atoi(e) != 0;
     }();
-    return on && T.logN >= 8 && T.logN <= 14;
+    return on && T.logN >= 8 && T.logN <= 14 && !T.ks_seal;
 }
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
-                       int l, const u64* const* keys_host, const u64* giant_elts, u64* inner, u64* out, u64* ws,
-                       size_t ws_bytes,
+                       int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
+                       u64* out, u64* ws, size_t ws_bytes,
                        void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm) {
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
     if (T.N % 128 || G > 64 || R > 512) return hipErrorInvalidValue;
     if (R > 0 && bsgs_giant_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
-    const int C = (R > 0 && !giant_fused(T)) ? std::max(1, std::min(ss.chunks, std::min(R, (ss.nev - 2) / 2))) : 1;
+    const int C = (R > 0 && !giant_fused(T) && !T.ks_seal)
+                      ? std::max(1, std::min(ss.chunks, std::min(R, (ss.nev - 2) / 2))) : 1;
     hipStream_t sm = ss.main, sa = ss.aux;
     hipEvent_t ev_start = ss.ev[0], ev_end = ss.ev[1];
     const hipEvent_t* evH = ss.ev + 2;
@@ -1547,9 +1612,18 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             if (giant_elts) elt = giant_elts[g];
             else
                 for (int s2 = 0; s2 < g * G; ++s2) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
-            items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)(r - rb(c))};
+            items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)(r - rb(c)),
+                              akeys_host ? akeys_host[g] : nullptr};
             uniq[r] = ct + S;
         }
+    // SEAL convention: each giant input is automorphed before its decomposition (serial schedule,
+    // C = 1; the permutations are enqueued after the Hadamard that produces the inputs)
+    std::vector<KsItem> seal_orig;
+    u64* seal_perm = ws + ks_core_bytes(T, R, R, l) / 8;
+    if (T.ks_seal && R > 0) {
+        seal_orig.assign(items, items + R);
+        seal_rewrite(T, items, R, uniq, l, seal_perm);
+    }
     const KsItem* it = nullptr;
     const u64* const* uq = nullptr;
     if (R > 0) {
@@ -1577,6 +1651,10 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         for (int c = 1; c < C; ++c) hipEventRecord(evH[c], sm);
     }
     if (he != hipSuccess) return he;
+    if (!seal_orig.empty()) {
+        he = seal_permute(T, seal_orig.data(), R, l, seal_perm, sm);
+        if (he != hipSuccess) return he;
+    }
     hipEventRecord(ev_start, sm);
     hipStreamWaitEvent(sa, ev_start, 0);
     if (R <= 0) {

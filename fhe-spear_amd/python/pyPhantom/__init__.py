@@ -102,6 +102,11 @@ _SIGS = {
     "fhs_galois_key_export": (C.c_int, [_vp, _vp, _u64, _u64p]),
     "fhs_relin_key_export": (C.c_int, [_vp, _vp, _u64p]),
     "fhs_secret_key_export": (C.c_int, [_vp, _vp, _u64p]),
+    "fhs_galois_keys_import": (C.c_int, [_vp, _u64p, C.c_int, _u64p, C.POINTER(_vp)]),
+    "fhs_relin_key_import": (C.c_int, [_vp, _u64p, C.POINTER(_vp)]),
+    "fhs_secret_key_import": (C.c_int, [_vp, _u64p, C.POINTER(_vp)]),
+    "fhs_context_set_key_switch_mode": (C.c_int, [_vp, C.c_int]),
+    "fhs_context_key_switch_mode": (C.c_int, [_vp, _ip]),
     "fhs_public_key_export": (C.c_int, [_vp, _vp, _u64p]),
     "fhs_galois_keys_bytes": (C.c_int, [_vp, _u64p]),
     "fhs_ciphertext_destroy": (C.c_int, [_vp]),
@@ -346,6 +351,21 @@ class context:
 
     def limbs(self, chain_index):
         return self.L0 + 1 - chain_index
+
+    def set_key_switch_mode(self, mode):
+        """Key-switch convention (extension): 'exact' (default: exact centred ModUp,
+        ModDown without rounding -- rotations of one input share a ModUp) or 'seal' (special_modulus_size
+        1 only: SEAL's switch_key_inplace -- per-limb lift without centring, automorphism before the
+        decomposition, ModDown rounded -- no hoisting)."""
+        modes = {"exact": 0, "seal": 1}
+        if mode not in modes:
+            raise ValueError("key switch mode: 'exact' or 'seal'")
+        _check(_lib.fhs_context_set_key_switch_mode(self._h, modes[mode]), "set_key_switch_mode")
+
+    def key_switch_mode(self):
+        v = C.c_int()
+        _check(_lib.fhs_context_key_switch_mode(self._h, C.byref(v)), "key_switch_mode")
+        return ("exact", "seal")[v.value]
 
     def galois_elts(self):
         """The Galois elements keys are made for (the params' set, or the SEAL/Phantom default
@@ -884,6 +904,37 @@ def random_plaintexts(ctx, seed, count, chain_index, scale):
     _check(_lib.fhs_random_plaintexts(ctx._h, int(seed), int(count), int(chain_index), float(scale), hs),
            "random_plaintexts")
     return [plaintext(ctx, _vp(hs[i])) for i in range(count)]
+
+
+def galois_keys_from_numpy(ctx, keys):
+    """{galois element: [dnum][2][L0+P][N] uint64} -> galois_key (import of keys made elsewhere, e.g.
+    SEAL's KSwitchKeys: component 0 = b_j = -a_j s + e_j + P g_j s', component 1 = a_j; the layout
+    galois_key.export returns)."""
+    elts = sorted(int(e) for e in keys)
+    arr = np.ascontiguousarray(np.stack([np.asarray(keys[e], dtype=np.uint64) for e in elts]))
+    e_arr = np.array(elts, dtype=np.uint64)
+    h = _vp()
+    _check(_lib.fhs_galois_keys_import(ctx._h, e_arr.ctypes.data_as(_u64p), len(elts), arr.ctypes.data_as(_u64p),
+                                       C.byref(h)), "galois_keys_from_numpy")
+    return galois_key(ctx, h)
+
+
+def relin_key_from_numpy(ctx, key):
+    a = np.ascontiguousarray(key, dtype=np.uint64)
+    h = _vp()
+    _check(_lib.fhs_relin_key_import(ctx._h, a.ctypes.data_as(_u64p), C.byref(h)), "relin_key_from_numpy")
+    return relin_key(ctx, h)
+
+
+def secret_key_from_numpy(ctx, s_ntt):
+    """[L0+P][N] NTT-form secret -> secret_key (its encryption randomness: a fresh 256-bit key)."""
+    a = np.ascontiguousarray(s_ntt, dtype=np.uint64)
+    sk = secret_key.__new__(secret_key)
+    sk._ctx, sk.seed = ctx, None
+    h = _vp()
+    _check(_lib.fhs_secret_key_import(ctx._h, a.ctypes.data_as(_u64p), C.byref(h)), "secret_key_from_numpy")
+    sk._h = h
+    return sk
 
 
 class Event:

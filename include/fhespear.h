@@ -88,6 +88,22 @@ fhs_status fhs_galois_keys_has(const fhs_galois_keys* gk, uint64_t elt, int* has
 fhs_status fhs_galois_key_export(fhs_context* ctx, const fhs_galois_keys* gk, uint64_t elt, uint64_t* host);
 fhs_status fhs_relin_key_export(fhs_context* ctx, const fhs_relin_key* rk, uint64_t* host);
 fhs_status fhs_secret_key_export(fhs_context* ctx, const fhs_secret_key* sk, uint64_t* host /* [L0+P][N] */);
+/* Key import in the export layout ("identical Galois keys": a key set made elsewhere, e.g. SEAL's
+ * KSwitchKeys with key_vector[j].data(0|1), P = 1).  Residues must be canonical.  Imported keys keep
+ * their a_j explicitly (generated keys regenerate them from seeds).  Replaces no pb symbol: the
+ * binding had no import; TenSEAL's key loading is the analogue. */
+fhs_status fhs_galois_keys_import(fhs_context* ctx, const uint64_t* elts, int n,
+                                  const uint64_t* host /* [n][dnum][2][L0+P][N] */, fhs_galois_keys** out);
+fhs_status fhs_relin_key_import(fhs_context* ctx, const uint64_t* host /* [dnum][2][L0+P][N] */, fhs_relin_key** out);
+fhs_status fhs_secret_key_import(fhs_context* ctx, const uint64_t* host /* [L0+P][N], NTT form */,
+                                 fhs_secret_key** out);
+/* Key-switch convention: FHS_KS_EXACT (default; exact centred ModUp, ModDown without
+ * rounding, hoistable) or FHS_KS_SEAL (P = 1 only: SEAL's switch_key_inplace -- per-limb lift without
+ * centring, automorphism before the decomposition, ModDown rounded by adding floor(p/2)). */
+#define FHS_KS_EXACT 0
+#define FHS_KS_SEAL 1
+fhs_status fhs_context_set_key_switch_mode(fhs_context* ctx, int mode);
+fhs_status fhs_context_key_switch_mode(const fhs_context* ctx, int* mode);
 fhs_status fhs_public_key_export(fhs_context* ctx, const fhs_public_key* pk, uint64_t* host /* [2][L0][N] */);
 fhs_status fhs_galois_keys_bytes(const fhs_galois_keys* gk, uint64_t* bytes);
 

@@ -29,7 +29,20 @@ struct ock_ctx {
     uint64_t* ipsi_rev;     /* K x N  psi^{-rev(k)} */
     uint64_t* ipsi_rev_s;
     uint64_t* n_inv;        /* K */
+    int ks_seal;            /* key-switch convention: 0 exact centred (default), 1 SEAL (P = 1) */
 };
+
+/* SEAL's switch_key_inplace (P = 1; SEAL evaluator.cpp, published): each data limb of the
+ * (already automorphed) target is lifted to the other primes as its residue in [0, q) -- no
+ * centring -- and the ModDown adds floor(p/2) to the special limb before converting it and
+ * subtracts floor(p/2) mod q_i after, i.e. rounds instead of flooring.  The non-centred lift does not
+ * commute with automorphisms, so there is no hoisting in this mode: ock_rotate_hoisted refuses it. */
+int ock_ctx_set_ks_mode(ock_ctx* c, int mode) {
+    if (mode != 0 && mode != 1) return -1;
+    if (mode == 1 && c->P != 1) return -1;
+    c->ks_seal = mode;
+    return 0;
+}
 
 /* ------------------------------------------------------------------ sampling spec */
 uint64_t ock_splitmix64(uint64_t x) {
@@ -443,7 +456,7 @@ void ock_keyswitch(const ock_ctx* c, const uint64_t* a, const uint64_t* key, int
                 for (uint64_t n = 0; n < N; n++) {
                     uint64_t yy[8];
                     for (int u = 0; u < ns; u++) yy[u] = y[(size_t)u * N + n];
-                    int v = ock_centered_count(yy, c->q + s0, ns);
+                    int v = c->ks_seal ? 0 : ock_centered_count(yy, c->q + s0, ns);
                     u128 s = 0;
                     for (int u = 0; u < ns; u++) s += (u128)yy[u] * hm[u];
                     uint64_t r = (uint64_t)(s % m);
@@ -470,6 +483,7 @@ void ock_keyswitch(const ock_ctx* c, const uint64_t* a, const uint64_t* key, int
             memcpy(dst, acc + ((size_t)comp * E + l + k) * N, 8 * N);
             ock_ntt_inv(c, dst, pi);
             for (uint64_t n = 0; n < N; n++) dst[n] = mulmod(dst[n], ih, p);
+            if (c->ks_seal) for (uint64_t n = 0; n < N; n++) dst[n] = addmod(dst[n], p >> 1, p);
         }
         for (int i = 0; i < l; i++) {
             uint64_t q = c->q[i], hm[8], Pm = 1;
@@ -479,10 +493,11 @@ void ock_keyswitch(const ock_ctx* c, const uint64_t* a, const uint64_t* key, int
                 hm[k] = h; Pm = mulmod(Pm, c->q[L0 + k] % q, q);
             }
             uint64_t Pinv = invmod(Pm, q);
+            uint64_t halfq = c->ks_seal ? (c->q[L0] >> 1) % q : 0;
             for (uint64_t n = 0; n < N; n++) {
                 u128 s = 0;
                 for (int k = 0; k < P; k++) s += (u128)yp[(size_t)k * N + n] * hm[k];
-                ext[n] = (uint64_t)(s % q);
+                ext[n] = submod((uint64_t)(s % q), halfq, q);
             }
             ock_ntt_fwd(c, ext, i);
             const uint64_t* ap = acc + ((size_t)comp * E + i) * N;
@@ -514,6 +529,10 @@ void ock_rotate(const ock_ctx* c, const uint64_t* ct, const uint64_t* gkey, uint
  * extension this equals ock_rotate per element, limb for limb (tests/test_cpu.py). */
 void ock_rotate_hoisted(const ock_ctx* c, const uint64_t* ct, const uint64_t* const* gkeys, const uint64_t* elts,
                         int nrot, int l, uint64_t* const* outs) {
+    if (c->ks_seal) {   /* no hoisting under SEAL's convention: one rotation at a time */
+        for (int r = 0; r < nrot; r++) ock_rotate(c, ct, gkeys[r], elts[r], l, outs[r]);
+        return;
+    }
     uint64_t N = c->N; int P = c->P, L0 = c->L0, K = c->K, E = l + P;
     int dnum = (l + P - 1) / P;
     size_t S = (size_t)l * N;

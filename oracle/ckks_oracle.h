@@ -45,6 +45,8 @@ int ock_create_coeff_modulus(uint64_t N, const int* bits, int n, uint64_t* out);
 uint64_t ock_galois_elt_from_step(int step, uint64_t N);       /* pb:124-126 */
 
 ock_ctx* ock_ctx_create(uint64_t N, const uint64_t* primes, int nprimes, int special);
+/* key-switch convention: 0 exact centred (default), 1 SEAL switch_key_inplace (P = 1); 0 on success */
+int ock_ctx_set_ks_mode(ock_ctx* c, int mode);
 void ock_ctx_destroy(ock_ctx* c);
 int ock_ctx_L0(const ock_ctx* c);
 int ock_ctx_P(const ock_ctx* c);

@@ -39,6 +39,8 @@ def lib():
         L = C.CDLL(str(LIB_PATH))
         L.ock_ctx_create.restype = C.c_void_p
         L.ock_ctx_create.argtypes = [C.c_uint64, _u64p, C.c_int, C.c_int]
+        L.ock_ctx_set_ks_mode.argtypes = [C.c_void_p, C.c_int]
+        L.ock_ctx_set_ks_mode.restype = C.c_int
         L.ock_ctx_destroy.argtypes = [C.c_void_p]
         L.ock_create_coeff_modulus.argtypes = [C.c_uint64, C.POINTER(C.c_int), C.c_int, _u64p]
         L.ock_galois_elt_from_step.restype = C.c_uint64
@@ -173,6 +175,12 @@ class Oracle:
         a = np.ascontiguousarray(limb, dtype=np.uint64).copy()
         lib().ock_ntt_inv(self._h, _p(a), prime_idx)
         return a
+
+    def set_key_switch_mode(self, mode: str):
+        """'exact' (default: exact centred ModUp, ModDown without rounding) or 'seal' (P = 1:
+        SEAL's switch_key_inplace, ock_ctx_set_ks_mode)."""
+        if lib().ock_ctx_set_ks_mode(self._h, {"exact": 0, "seal": 1}[mode]) != 0:
+            raise ValueError("seal key switching needs special_modulus_size 1")
 
     def galois_ntt(self, limb: np.ndarray, elt: int) -> np.ndarray:
         a = np.ascontiguousarray(limb, dtype=np.uint64)

@@ -25,3 +25,11 @@ def gpu_available():
 def require_gpu():
     if not gpu_available():
         pytest.fail("GPU test selected but no HIP device / libfhespear_hip.so is available")
+
+
+@pytest.fixture(scope="module")
+def orc():
+    """The CPU parity oracle (oracle/ckks_oracle.c via oracle/oracle.py), built in-tree."""
+    from oracle import oracle
+    oracle.build()
+    return oracle
