@@ -796,6 +796,32 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
 __device__ __forceinline__ const u64* ks_src(const u64* ext_tj, const u64* own_t, int t, int j, int P_, int l) {
     return (t >= j * P_ && t < min(j * P_ + P_, l)) ? own_t : ext_tj;
 }
+// sum_j ext_j[t][sigma(n)] (b_j, a_j)[t][n] as two lazy 128-bit sums; a_j regenerated from the key's
+// seeds, or read from an imported key's explicit a (akey, a separate instantiation: the choice is
+// per item, so the digit loop carries no branch)
+template <bool EXPLICIT_A>
+__device__ __forceinline__ void ks_digits(const DevTables& T, const u64* ex, const u64* own, const u64* key,
+                                          const u64* akey, const u64* seeds, u64 cx, const RedU& RD, unsigned qb,
+                                          int t, int l, int dn, size_t per_r, u128& c0, u128& c1) {
+    const int P_ = T.P;
+    const size_t KN = (size_t)T.K * T.N;
+    Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
+#pragma unroll 4
+    for (int j = 0; j < dn; ++j) {
+        const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
+        acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * KN)));
+        if constexpr (EXPLICIT_A)
+            acc3_mac(a1, v, split30(__builtin_nontemporal_load(akey + (size_t)j * KN)));
+        else
+            acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
+        if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
+            acc3_fold(c0, a0);
+            acc3_fold(c1, a1);
+        }
+    }
+    acc3_fold(c0, a0);
+    acc3_fold(c1, a1);
+}
 __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items, const u64* const* uniq, const u64* ext,
                                                 u64* acc, int l, int R, int t0) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
@@ -816,20 +842,10 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     const u64 cx = seeded_ctr_mix(pt, n);
     const unsigned qb = 64 - __clzll(RD.q);
     u128 c0 = {0, 0}, c1 = {0, 0};
-    Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
-#pragma unroll 4
-    for (int j = 0; j < dn; ++j) {
-        const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
-        acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * K * N)));
-        acc3_mac(a1, v, split30(it.akey ? __builtin_nontemporal_load(it.akey + (size_t)j * K * N + (size_t)pt * N + n)
-                                        : seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
-        if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
-            acc3_fold(c0, a0);
-            acc3_fold(c1, a1);
-        }
-    }
-    acc3_fold(c0, a0);
-    acc3_fold(c1, a1);
+    if (it.akey)
+        ks_digits<true>(T, ex, own, key, it.akey + (size_t)pt * N + n, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
+    else
+        ks_digits<false>(T, ex, own, key, nullptr, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
     acc[(((size_t)r * 2 + 0) * E + t) * N + n] = reduce128(c0.lo, c0.hi, RD);
     acc[(((size_t)r * 2 + 1) * E + t) * N + n] = reduce128(c1.lo, c1.hi, RD);
 }
@@ -859,20 +875,10 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
         const u64* key = it.key + (size_t)t * N + n;
         const u64* seeds = it.key + (size_t)T.dnum * K * N;
         u128 c0 = {0, 0}, c1 = {0, 0};
-        Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
-#pragma unroll 4
-        for (int j = 0; j < dn; ++j) {
-            const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
-            acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * K * N)));
-            acc3_mac(a1, v, split30(it.akey ? __builtin_nontemporal_load(it.akey + (size_t)j * K * N + (size_t)t * N + n)
-                                            : seeded_uniform_x(seeds[j] + cx, q, qb)));
-            if ((j & 7) == 7) {
-                acc3_fold(c0, a0);
-                acc3_fold(c1, a1);
-            }
-        }
-        acc3_fold(c0, a0);
-        acc3_fold(c1, a1);
+        if (it.akey)
+            ks_digits<true>(T, ex, own, key, it.akey + (size_t)t * N + n, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
+        else
+            ks_digits<false>(T, ex, own, key, nullptr, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
         s0 = addmod(s0, reduce128(c0.lo, c0.hi, RD), q);
         s1 = addmod(s1, reduce128(c1.lo, c1.hi, RD), q);
         sadd = addmod(sadd, it.add0[(size_t)t * N + sn], q);
