@@ -11,6 +11,13 @@
 //   k_sample / k_swk / ...         deterministic key generation and encryption helpers
 // Every integer result is reduced to [0, q): limbs are bit-identical to oracle/ckks_oracle.c.
 #include "fhs_kernels.h"
+typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+#ifndef FHS_KSIP_PARTS
+#define FHS_KSIP_PARTS 1
+#endif
+#ifndef FHS_KSIP_VEC
+#define FHS_KSIP_VEC 1
+#endif
 #include "fhs_ntt.h"
 
 #include <cstdio>
@@ -855,11 +862,14 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
 // sum_r ModDown(acc_r) + sigma_r(c0_r) (k_giant_sum adds the special-limb conversion).  Writes
 // bpart[c][t][n] into the r = 0 slot of acc (acc[0][c][t], t < l), which nothing else uses.
 __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* items, const u64* const* uniq,
-                                                    const u64* ext, u64* acc, int l, int R) {
+                                                    const u64* ext, u64* acc, int l, int R, int nparts) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
-    int t, m;
-    if (!xcd_touter(l, NB, t, m)) return;
+    int t, mp;
+    if (!xcd_touter(l, NB * nparts, t, mp)) return;
+    // rotations [r0, r1) of part `part`; its partial sum goes to acc slot `part` (k_giant_sum adds them)
+    const int m = mp % NB, part = mp / NB;
+    const int r0 = (int)((long long)part * R / nparts), r1 = (int)((long long)(part + 1) * R / nparts);
     const int n = (m << 8) + threadIdx.x;
     const size_t per_r = (size_t)E * N;
     const RedU RD = redu(PK(T, t));
@@ -867,7 +877,7 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
     const u64 cx = seeded_ctr_mix(t, n);
     const unsigned qb = 64 - __clzll(q);
     u64 s0 = 0, s1 = 0, sadd = 0;
-    for (int r = 0; r < R; ++r) {
+    for (int r = r0; r < r1; ++r) {
         const KsItem it = items[r];
         const int sn = galois_src(n, it.elt, T.logN);
         const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
@@ -884,8 +894,103 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
         sadd = addmod(sadd, it.add0[(size_t)t * N + sn], q);
     }
     const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
-    acc[((size_t)0 * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
-    acc[((size_t)1 * E + t) * N + n] = shoup(s1, pinv, pinv_s, q);
+    acc[(((size_t)part * 2 + 0) * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
+    acc[(((size_t)part * 2 + 1) * E + t) * N + n] = shoup(s1, pinv, pinv_s, q);
+}
+
+// k_ks_ip_sum with two coefficients per thread (FHS_KSIP_VEC == 2): 16-byte key loads, and each
+// group of 4 digits issues all its loads before the multiply-accumulates.
+template <bool EXPLICIT_A>
+__device__ __forceinline__ void ks_digits2(const u64* const ex[2], const u64* const own[2], const u64* key,
+                                           const u64* akey, const u64* seeds, const u64 cx[2], u64 q, unsigned qb,
+                                           int t, int l, int P_, int dn, size_t per_r, size_t KN, u128 c0[2],
+                                           u128 c1[2]) {
+    Acc3 a0[2] = {{0, 0, 0}, {0, 0, 0}}, a1[2] = {{0, 0, 0}, {0, 0, 0}};
+    int j = 0;
+    for (; j < dn; j += 4) {
+        const int nj = min(4, dn - j);
+        u64 v[4][2];
+        u64x2_t b[4], a[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u < nj) {
+                const int jj = j + u;
+                const bool own_limb = t >= jj * P_ && t < min(jj * P_ + P_, l);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) v[u][h] = own_limb ? own[h][0] : ex[h][(size_t)jj * per_r];
+                b[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(key + (size_t)jj * KN));
+                if constexpr (EXPLICIT_A)
+                    a[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(akey + (size_t)jj * KN));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u < nj) {
+                const int jj = j + u;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const Split30 sv = split30(v[u][h]);
+                    acc3_mac(a0[h], sv, split30(h ? b[u].y : b[u].x));
+                    u64 av;
+                    if constexpr (EXPLICIT_A) av = h ? a[u].y : a[u].x;
+                    else av = seeded_uniform_x(seeds[jj] + cx[h], q, qb);
+                    acc3_mac(a1[h], sv, split30(av));
+                }
+            }
+        }
+        if ((j & 4) == 4 || j + 4 >= dn) {   // folded at least every 8 products
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                acc3_fold(c0[h], a0[h]);
+                acc3_fold(c1[h], a1[h]);
+            }
+        }
+    }
+}
+__global__ void __launch_bounds__(256) k_ks_ip_sum2(DevTables T, const KsItem* items, const u64* const* uniq,
+                                                     const u64* ext, u64* acc, int l, int R) {
+    const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
+    const int NB = N >> 9;
+    int t, m;
+    if (!xcd_touter(l, NB, t, m)) return;
+    const int n0 = ((m << 8) + threadIdx.x) * 2;
+    const size_t per_r = (size_t)E * N;
+    const RedU RD = redu(PK(T, t));
+    const u64 q = RD.q;
+    const u64 cx[2] = {seeded_ctr_mix(t, n0), seeded_ctr_mix(t, n0 + 1)};
+    const unsigned qb = 64 - __clzll(q);
+    u64 s0[2] = {0, 0}, s1[2] = {0, 0}, sadd[2] = {0, 0};
+    for (int r = 0; r < R; ++r) {
+        const KsItem it = items[r];
+        const int sn[2] = {galois_src(n0, it.elt, T.logN), galois_src(n0 + 1, it.elt, T.logN)};
+        const u64* ex[2];
+        const u64* own[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            ex[h] = ext + ((size_t)it.src * dn * E + t) * N + sn[h];
+            own[h] = uniq[it.src] + (size_t)t * N + sn[h];
+        }
+        const u64* key = it.key + (size_t)t * N + n0;
+        const u64* seeds = it.key + (size_t)T.dnum * K * N;
+        u128 c0[2] = {{0, 0}, {0, 0}}, c1[2] = {{0, 0}, {0, 0}};
+        if (it.akey)
+            ks_digits2<true>(ex, own, key, it.akey + (size_t)t * N + n0, seeds, cx, q, qb, t, l, P_, dn, per_r,
+                             (size_t)K * N, c0, c1);
+        else
+            ks_digits2<false>(ex, own, key, nullptr, seeds, cx, q, qb, t, l, P_, dn, per_r, (size_t)K * N, c0, c1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            s0[h] = addmod(s0[h], reduce128(c0[h].lo, c0[h].hi, RD), q);
+            s1[h] = addmod(s1[h], reduce128(c1[h].lo, c1[h].hi, RD), q);
+            sadd[h] = addmod(sadd[h], it.add0[(size_t)t * N + sn[h]], q);
+        }
+    }
+    const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        acc[((size_t)0 * E + t) * N + n0 + h] = addmod(shoup(s0[h], pinv, pinv_s, q), sadd[h], q);
+        acc[((size_t)1 * E + t) * N + n0 + h] = shoup(s1[h], pinv, pinv_s, q);
+    }
 }
 
 // Giant steps, ModUp fused with the key inner product: one workgroup per (target limb t, rotation r)
@@ -1331,11 +1436,10 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
 // Block = 4 waves sharing one 64-coefficient slice of limb i: the slice of all G baby steps
 // (both components) is staged once in LDS, each wave then streams the diagonals of its giant
 // groups (g = wave, wave+4, ...) from HBM with lazy 128-bit accumulation.
-typedef u64 u64x2 __attribute__((ext_vector_type(2)));
 template <int VEC>
 __device__ __forceinline__ void ld_diag(const u64* p, u64* out) {
     if constexpr (VEC == 2) {
-        const u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(p));
+        const u64x2_t t = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
         out[0] = t.x;
         out[1] = t.y;
     } else {
@@ -1417,7 +1521,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
 // is bit-identical to rotating and adding one giant step at a time (bg:478-483).
 // base_c = (sum_r acc_r,c) P^-1 + [c==0] sum_r galois_r(inner_r.c0) + inner_0.c ;  convsum_c = sum_r conv(y_r,c)
 __global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, const u64* inner0, u64* base,
-                            u64* convsum, int l, int R, int first) {
+                            u64* convsum, int l, int R, int first, int nparts) {
     const int N = T.N, P_ = T.P, E = l + P_;
     const size_t S = (size_t)l * N;
     const size_t total = 2 * S;
@@ -1447,6 +1551,7 @@ __global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, con
         }
         u64 cv = reduce128(cs.lo, cs.hi, P);
         u64 bv = bpart[((size_t)comp * E + i) * N + n];
+        for (int p = 1; p < nparts; ++p) bv = addmod(bv, bpart[(((size_t)p * 2 + comp) * E + i) * N + n], q);
         if (first) {
             bv = addmod(bv, inner0[idx], q);
         } else {
@@ -1509,13 +1614,26 @@ static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, in
     launch_modup<LOGN>(T, uniq, b.acoef, b.vcnt, b.ext, l, U, st);
     FHS_TMARK(tm, KID_MODUP, 0, st);
 }
+// rotations per k_ks_ip_sum thread: the giant sum is split into parts over more workgroups (more loads
+// in flight), each writing its partial into an unused acc slot; k_giant_sum adds the parts
+static int ksip_parts(int R) {
+    static const int v = [] {
+        const char* e = getenv("FHESPEAR_KSIP_PARTS");
+        return e ? std::max(1, std::min(16, atoi(e))) : FHS_KSIP_PARTS;
+    }();
+    return std::max(1, std::min(v, R));
+}
 template <int LOGN>
 static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* const* uniq, int R, int l, const KsBufs& b,
                            hipStream_t st, const KTimer* tm) {
     const int NB = T.N >> 8;
     FHS_TMARK(tm, KID_KS_IP, 1, st);
     hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(T.P, R * NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R, l);
-    hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
+    if (FHS_KSIP_VEC == 2 && T.N >= 512)
+        hipLaunchKernelGGL(k_ks_ip_sum2, dim3(xcd_grid(l, NB / 2)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
+    else
+        hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB * ksip_parts(R))), dim3(256), 0, st, T, it, uniq, b.ext, b.acc,
+                           l, R, ksip_parts(R));
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
     hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, st, T, b.acc, b.ycoef, l, R);
@@ -1697,7 +1815,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                 FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sm);
                 FHS_TMARK(tm, KID_GIANT_SUM, 1, sm);
                 hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, b.acc, b.ycoef, inner, base,
-                                   convsum, l, R, 1);
+                                   convsum, l, R, 1, 1);
                 FHS_TMARK(tm, KID_GIANT_SUM, 0, sm);
                 FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
                 hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum,
@@ -1728,7 +1846,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             giant_ip_stage<LOGN>(T, it + rb(c), uq + rb(c), Rc, l, bc, sa, tm);
             FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
             hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, bc.acc, bc.ycoef, inner, base,
-                               convsum, l, Rc, c == 0 ? 1 : 0);
+                               convsum, l, Rc, c == 0 ? 1 : 0, (FHS_KSIP_VEC == 2 && T.N >= 512) ? 1 : ksip_parts(Rc));
             FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
         }
         hipEventRecord(ev_end, sa);

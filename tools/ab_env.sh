@@ -9,7 +9,7 @@ steps=${AB_STEPS:-10}
 for spec in "$@"; do
     name=${spec%% *}
     envs=${spec#"$name"}
-    line=$(env $envs timeout -k 10 300 python3 bench.py --config "$cfg" --steps "$steps" --warmup 3 --no-cpu-baseline) || {
+    line=$(env $envs timeout -k 10 300 python3 bench.py --config "$cfg" --steps "$steps" --warmup 3 --no-cpu-baseline --no-block) || {
         echo "variant $name failed (rc $?)" >> "$out"
         exit 1
     }
