@@ -823,6 +823,17 @@ void ock_encrypt_asymmetric(const ock_ctx* c, const uint8_t* rng32, uint64_t cou
     }
     free(u); free(e0); free(e1); free(ut); free(t0); free(t1);
 }
+/* pyPhantom.random_plaintexts(ctx, seed, count, ...) plaintext k (the bench's i.i.d. uniform diagonals,
+ * not secret): stream key sm(seed ^ sm(7 << 56 | k)); limb i, coefficient n = (rnd(2m) 2^64 + rnd(2m+1))
+ * mod q_i with m = i N + n (fhs_kernels.hip k_sample, SAMPLE_TESTDATA). */
+void ock_random_plaintext(const ock_ctx* c, uint64_t seed, uint64_t k, int l, uint64_t* out) {
+    uint64_t key = ock_splitmix64(seed ^ ock_splitmix64((7ULL << 56) | k)), N = c->N;
+    for (int i = 0; i < l; i++)
+        for (uint64_t n = 0; n < N; n++) {
+            uint64_t ctr = 2 * ((uint64_t)i * N + n);
+            out[(size_t)i * N + n] = reduce128(ock_rnd(key, ctr), ock_rnd(key, ctr + 1), c->q[i]);
+        }
+}
 void ock_decrypt(const ock_ctx* c, const uint64_t* s_ntt, const uint64_t* ct, int ncomp, int l, uint64_t* pt) {
     uint64_t N = c->N; size_t S = (size_t)l * N;
     for (int i = 0; i < l; i++) {

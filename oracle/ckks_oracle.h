@@ -104,6 +104,8 @@ void ock_encrypt_symmetric(const ock_ctx* c, const uint8_t* key32, uint64_t coun
 void ock_encrypt_asymmetric(const ock_ctx* c, const uint8_t* rng32, uint64_t counter, const uint64_t* pk,
                             const uint64_t* pt, int l, uint64_t* ct);
 void ock_decrypt(const ock_ctx* c, const uint64_t* s_ntt, const uint64_t* ct, int ncomp, int l, uint64_t* pt);
+/* the bench's random plaintext k of seed (pyPhantom.random_plaintexts, not secret) at l limbs */
+void ock_random_plaintext(const ock_ctx* c, uint64_t seed, uint64_t k, int l, uint64_t* out);
 
 /* ---- CKKS encoder (pb:138-156); slots = N/2; values interleaved (re, im) ---- */
 void ock_encode_complex(const ock_ctx* c, const double* re_im, size_t n, double scale, int l, uint64_t* pt);

@@ -40,6 +40,7 @@ def lib():
         L.ock_ctx_create.restype = C.c_void_p
         L.ock_ctx_create.argtypes = [C.c_uint64, _u64p, C.c_int, C.c_int]
         L.ock_ctx_set_ks_mode.argtypes = [C.c_void_p, C.c_int]
+        L.ock_random_plaintext.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, _u64p]
         L.ock_ctx_set_ks_mode.restype = C.c_int
         L.ock_ctx_destroy.argtypes = [C.c_void_p]
         L.ock_create_coeff_modulus.argtypes = [C.c_uint64, C.POINTER(C.c_int), C.c_int, _u64p]
@@ -175,6 +176,12 @@ class Oracle:
         a = np.ascontiguousarray(limb, dtype=np.uint64).copy()
         lib().ock_ntt_inv(self._h, _p(a), prime_idx)
         return a
+
+    def random_plaintext(self, seed: int, k: int, l: int):
+        """pyPhantom.random_plaintexts(ctx, seed, ...)[k] at l limbs (test data)."""
+        out = np.empty((l, self.N), dtype=np.uint64)
+        lib().ock_random_plaintext(self._h, seed, k, l, _p(out))
+        return out
 
     def set_key_switch_mode(self, mode: str):
         """'exact' (default: exact centred ModUp, ModDown without rounding) or 'seal' (P = 1:

@@ -51,3 +51,55 @@ def test_cfg5_ffn_chain_24_blocks_n32768(require_gpu):
     assert sum(r["bootstrap_seconds"] is not None for r in recs) >= 3
     assert recs[-1]["corr"] > 0.999                                   # tf:298
     assert all(r["corr"] > 0.999 for r in recs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["cfg1", "cfg2"])
+def test_full_matvec_bit_exact_vs_oracle(require_gpu, tmp_path, cfg):
+    """BASELINE configs[0]/[1] at full size, limb for limb against the C oracle (the
+    full-size checks were GPU-vs-GPU only): the 45 (cfg2) hoisted baby rotations against the oracle's
+    individual rotations, and the fused BSGS against the oracle's loop (bg:464-485) evaluated giant
+    group by giant group in a pool of CPU processes, then summed and rescaled."""
+    import multiprocessing as mp
+    import os
+    import pyPhantom as ph
+    from oracle.oracle import Oracle
+    N, L0, P, D = {"cfg1": (8192, 24, 3, 1024), "cfg2": (16384, 36, 3, 2048)}[cfg]
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    seed, pt_seed = 17, 29
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(P)
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(steps, N))))
+    parms.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * (L0 + P)))
+    ctx = ph.context(parms)
+    primes = [int(q) for q in ctx.primes]
+    sk = ph.secret_key(ctx, seed=seed)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    x = np.random.default_rng(3).normal(0, 0.1, D)
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), 2.0 ** 59))
+    pts = ph.random_plaintexts(ctx, pt_seed, D, ct.chain_index(), 2.0 ** 59)
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk).to_numpy()
+    baby_path = str(tmp_path / "baby.npy")
+    np.save(baby_path, np.stack([b.to_numpy() for b in baby]))
+    o = Oracle(N, primes, P)
+    assert np.array_equal(o.random_plaintext(pt_seed, 5, L0), pts[5].to_numpy())   # same diagonals
+    del pts, baby, gk
+    tasks = [("baby", b, N, primes, P, seed, pt_seed, G, D, baby_path) for b in range(1, G)]
+    tasks += [("giant", g, N, primes, P, seed, pt_seed, G, D, baby_path) for g in range(B)]
+    workers = max(1, min(16, (os.cpu_count() or 2) - 1, len(tasks)))
+    import _fullsize_worker
+    with mp.get_context("spawn").Pool(workers) as pool:
+        res = pool.map(_fullsize_worker.run, tasks, chunksize=1)
+    bad = [b for kind, (b, ok) in zip((t[0] for t in tasks), res) if kind == "baby" and not ok]
+    assert not bad, f"hoisted baby rotations differ from the oracle at steps {bad}"
+    giant = [r for t, r in zip(tasks, res) if t[0] == "giant"]
+    acc = None
+    for _, term in sorted(giant, key=lambda r: r[0]):
+        acc = term if acc is None else o.add(acc, term)
+    want = o.rescale(acc)
+    assert np.array_equal(y, want), "fused BSGS differs from the oracle loop at full size"
