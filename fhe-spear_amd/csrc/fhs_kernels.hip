@@ -12,6 +12,20 @@
 // Every integer result is reduced to [0, q): limbs are bit-identical to oracle/ckks_oracle.c.
 #include "fhs_kernels.h"
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+// Register caps for co-residency of the pipelined giant steps (A/B): FHS_MODUP_WPE = 5 caps ModUp at
+// 102 VGPRs, so its two workgroups per CU leave ~96 per SIMD for a key-inner-product wave;
+// FHS_KSIP_VGPR = min waves per SIMD for the key inner products (0: compiler's choice).
+#ifndef FHS_KSIP_VGPR
+#define FHS_KSIP_VGPR 0
+#endif
+#ifndef FHS_MODUP_WPE
+#define FHS_MODUP_WPE 4   // min waves per SIMD of k_modup_h (5: <= 102 VGPRs)
+#endif
+#if FHS_KSIP_VGPR
+#define FHS_KSIP_ATTR __attribute__((amdgpu_waves_per_eu(FHS_KSIP_VGPR)))
+#else
+#define FHS_KSIP_ATTR
+#endif
 #ifndef FHS_KSIP_PARTS
 #define FHS_KSIP_PARTS 1
 #endif
@@ -669,11 +683,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 // the upper half in registers while the lower half is transformed in LDS, then transforms it.
 // Same values as k_modup (same butterflies, same lazy bounds: < q + 2 q log N).
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
+__global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(DevTables T, const u64* const* uniq,
                                                                  const u64* acoef, const unsigned char* vcnt, u64* ext,
                                                                  int l, int U) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;   // 16 coefficient pairs per thread
+    #if FHS_MODUP_WPE > 4   // dynamic LDS: the compiler then honours the waves-per-SIMD bound (register cap)
+    extern __shared__ __attribute__((aligned(16))) u64 lds[];
+#else
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
+#endif
     const int tid = threadIdx.x;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     int t, mi;
@@ -778,7 +796,8 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     const int mgrid = FHS_MODUP_MAP == 1 ? xcd_grid(E, dn * U) : FHS_MODUP_MAP == 2 ? xcd_grid_m(E, dn * U) : E * dn * U;
     if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
-        const int pad = modup_pad();
+        int pad = modup_pad();
+        if (FHS_MODUP_WPE > 4) pad += (int)(((1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16) * 8);
         static bool attr = false;
         if (pad && !attr) {
             hipFuncSetAttribute(reinterpret_cast<const void*>(&k_modup_h<LOGN>),
@@ -829,7 +848,7 @@ __device__ __forceinline__ void ks_digits(const DevTables& T, const u64* ex, con
     acc3_fold(c0, a0);
     acc3_fold(c1, a1);
 }
-__global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items, const u64* const* uniq, const u64* ext,
+__global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip(DevTables T, const KsItem* items, const u64* const* uniq, const u64* ext,
                                                 u64* acc, int l, int R, int t0) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
@@ -861,7 +880,7 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
 // scaled by P^-1 and with the rotated c0's added (comp 0) -- the t < l part of
 // sum_r ModDown(acc_r) + sigma_r(c0_r) (k_giant_sum adds the special-limb conversion).  Writes
 // bpart[c][t][n] into the r = 0 slot of acc (acc[0][c][t], t < l), which nothing else uses.
-__global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* items, const u64* const* uniq,
+__global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip_sum(DevTables T, const KsItem* items, const u64* const* uniq,
                                                     const u64* ext, u64* acc, int l, int R, int nparts) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
@@ -1703,6 +1722,13 @@ static hipError_t launch_inner(const DevTables& T, const u64* const* baby, const
 // 1024-thread workgroup per CU with the 32 accumulators per thread left ~60 registers for the NTT
 // (spills), every barrier stalls all 16 waves, and the Shoup products with the on-the-fly companion
 // add ~70 VALU instructions per digit and coefficient to a kernel that is already VALU-bound.
+static bool bsgs_pipe() {
+    static const bool on = [] {
+        const char* e = getenv("FHESPEAR_BSGS_PIPE");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
 static bool giant_fused(const DevTables& T) {
     static const bool on = [] {
         const char* e = getenv("FHESPEAR_GIANT_FUSED");
@@ -1822,6 +1848,56 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                                    out, l);
                 FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
             }
+        });
+        return hipGetLastError();
+    }
+    if (C > 1 && !split && bsgs_pipe()) {
+        // Pipelined giant steps (FHESPEAR_BSGS_PIPE=1): INTT + centred counts of all R inputs in one
+        // launch, then ModUp chunk by chunk on `main` while `aux` runs the previous chunk's key inner
+        // products (memory-bound, no LDS: they fit beside the two ModUp workgroups of a CU when
+        // register caps leave room); chunk c's t < l partial sum goes to acc slot c, the special-limb
+        // INTT and the giant sum run once over all R at the end.  Same residues as the serial path.
+        FHS_DISPATCH_LOGN(T.logN, {
+            const KsBufs all = ks_carve(T, ws, R, R, l);
+            const size_t E = l + T.P, dn = (l + T.P - 1) / T.P;
+            hipStreamWaitEvent(sm, evH[0], 0);
+            FHS_TMARK(tm, KID_KS_INTT, 1, sm);
+            if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
+                hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * R), dim3((1 << LOGN) / 32), 0, sm, T, uq, all.acoef, l, R);
+            else
+                hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * R), dim3((1 << LOGN) / 16), 0, sm, T, uq, all.acoef, l, R);
+            hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)R * dn * N)), dim3(256), 0, sm, T, all.acoef, all.vcnt,
+                               l, R);
+            FHS_TMARK(tm, KID_KS_INTT, 0, sm);
+            const int NB = T.N >> 8;
+            for (int c = 0; c < C; ++c) {
+                const int Rc = rb(c + 1) - rb(c);
+                const KsBufs bc = ks_at(T, all, rb(c), rb(c), l);
+                FHS_TMARK(tm, KID_MODUP, 1, sm);
+                launch_modup<LOGN>(T, uq + rb(c), bc.acoef, bc.vcnt, bc.ext, l, Rc, sm);
+                FHS_TMARK(tm, KID_MODUP, 0, sm);
+                hipEventRecord(evF[c], sm);
+                hipStreamWaitEvent(sa, evF[c], 0);
+                FHS_TMARK(tm, KID_KS_IP, 1, sa);
+                hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(T.P, Rc * NB)), dim3(256), 0, sa, T, it + rb(c), uq + rb(c), bc.ext,
+                                   bc.acc, l, Rc, l);
+                hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, sa, T, it + rb(c), uq + rb(c), bc.ext,
+                                   all.acc + (size_t)c * 2 * E * N, l, Rc, 1);
+                FHS_TMARK(tm, KID_KS_IP, 0, sa);
+            }
+            FHS_TMARK(tm, KID_SPECIAL_INTT, 1, sa);
+            hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, sa, T, all.acc,
+                               all.ycoef, l, R);
+            FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sa);
+            FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
+            hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, all.acc, all.ycoef, inner, base,
+                               convsum, l, R, 1, C);
+            FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
+            hipEventRecord(ev_end, sa);
+            hipStreamWaitEvent(sm, ev_end, 0);
+            FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
+            hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum, out, l);
+            FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
         });
         return hipGetLastError();
     }
