@@ -136,6 +136,9 @@ def main():
     ap.add_argument("--no-block", action="store_true",
                     help="skip the measured RWKV-block leg (cfg3 on the same ranks) of the default line")
     ap.add_argument("--block-steps", type=int, default=3)
+    ap.add_argument("--block-dealt", action="store_true",
+                    help="block leg over N GPUs: deal each stage's projections only (default at N > 1: latency "
+                         "mode, each projection's giant steps sharded over a rank group as with --split)")
     ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--split", action="store_true",
                     help="cfg3 over N GPUs: latency mode, giant steps of each projection sharded over a rank group")
@@ -380,7 +383,11 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup):
     rng = np.random.default_rng(5)
     blk = rb.BlockWeights(rng, 1, D, F, H)
     srv = rb.Server(ph, cfg["N"], cfg["L0"], cfg["P"], D, device=local)
-    run = rb.BlockRunner(srv, blk, True, dist, rank, world, split=getattr(args, "split", False))
+    # sec/block is one token's latency: at N > 1 the stages' projections shard their giant steps over
+    # rank groups unless --block-dealt
+    split = getattr(args, "split", False) or (world > 1 and not getattr(args, "block_dealt", False)
+                                              and args.config == "cfg2")
+    run = rb.BlockRunner(srv, blk, True, dist, rank, world, split=split)
     x = rng.standard_normal(D)
     st = (x, np.zeros(D), np.zeros(D), np.zeros((H, 64, 64)), rng.standard_normal(D))
 
@@ -419,7 +426,7 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup):
                "stages_ms": {k: round(1e3 * v / steps, 2) for k, v in stage.items()},
                "max_abs_err_vs_plaintext_block": err,
                "workload": cfg["workload"], "n_gpus": world,
-               "parallelism": (f"giant-step-split projections x{world}" if getattr(args, "split", False)
+               "parallelism": (f"giant-step-split projections x{world}" if split
                                else f"stage-dealt projections x{world}") + (" + RCCL broadcast/gather" if world > 1 else "")}
     del run, srv
     return res
