@@ -130,9 +130,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rotations", type=int, default=8)
-    ap.add_argument("--cpu-sample-diagonals", type=int, default=170)
-    ap.add_argument("--cpu-reps", type=int, default=3)
+    ap.add_argument("--cpu-sample-rotations", type=int, default=6)
+    ap.add_argument("--cpu-sample-diagonals", type=int, default=128)
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed reps per worker (after one warmup rep); "
+                                                              "BASELINE.md plan: median of >= 5")
     ap.add_argument("--no-block", action="store_true",
                     help="skip the measured RWKV-block leg (cfg3 on the same ranks) of the default line")
     ap.add_argument("--block-steps", type=int, default=3)
@@ -537,7 +538,7 @@ def cpu_baseline(cfg, primes, args):
     return {"value": round(1.0 / per_matvec, 5), "unit": "matvec/s", "cores": W, "kind": "port",
             "cpu_model": cpu_model(),
             "sample": f"build C oracle (oracle/ckks_oracle.c), not TenSEAL (not importable, SURVEY §8c): {W} "
-                      f"processes x {args.cpu_reps} reps x ({nr} of {rot} rotations + {nd} of {D} "
+                      f"processes x (1 warmup + {args.cpu_reps} timed reps) x ({nr} of {rot} rotations + {nd} of {D} "
                       f"multiply_plain/add) at L0={L0}, N={N}, non-hoisted rotations as the reference issues "
                       f"them; median rep per worker, slowest worker extrapolated to one matvec "
                       f"({wall:.1f} s wall sampled per worker)",

@@ -19,7 +19,7 @@ def worker(N, primes, P, G, nr, nd, seed, barrier, out, reps=1):
     pt = np.stack([rng.integers(0, primes[i], N, dtype=np.uint64) for i in range(L0)])
     barrier.wait()
     tr, td = [], []
-    for _ in range(reps):
+    for rep in range(reps + 1):   # rep 0 is the warmup
         t0 = time.perf_counter()
         for _ in range(nr):
             o.rotate(ct, key, G)
@@ -28,6 +28,7 @@ def worker(N, primes, P, G, nr, nd, seed, barrier, out, reps=1):
         for _ in range(nd - 1):
             acc = o.add(acc, o.multiply_plain(ct, pt))
         t2 = time.perf_counter()
-        tr.append(t1 - t0)
-        td.append(t2 - t1)
+        if rep:
+            tr.append(t1 - t0)
+            td.append(t2 - t1)
     out.put((tr, td))
