@@ -1733,6 +1733,62 @@ static int decode_limbs(const fhs_context* c, double scale, int l) {
     }
     return l;
 }
+// constants of the centred CRT over the first l limbs for the GPU composition (l <= kCrtMaxL): the
+// same Q, hat, inv-hat (+ Shoup companion) and Q/2 words crt_compose derives on the host
+static void crt_consts(const fhs_context* c, int l, fhs::CrtConsts& K) {
+    K = fhs::CrtConsts{};
+    K.l = l;
+    K.W = l + 1;
+    const int W = K.W;
+    K.Q[0] = 1;
+    for (int i = 0; i < l; ++i) {
+        hu128 carry = 0;
+        for (int w = 0; w < W; ++w) {
+            const hu128 t = (hu128)K.Q[w] * c->q[i] + carry;
+            K.Q[w] = (uint64_t)t;
+            carry = t >> 64;
+        }
+    }
+    for (int i = 0; i < l; ++i) {
+        uint64_t* h = K.hat[i];
+        h[0] = 1;
+        uint64_t hm = 1;
+        for (int k = 0; k < l; ++k) {
+            if (k == i) continue;
+            hu128 carry = 0;
+            for (int w = 0; w < W; ++w) {
+                const hu128 t = (hu128)h[w] * c->q[k] + carry;
+                h[w] = (uint64_t)t;
+                carry = t >> 64;
+            }
+            hm = h_mulmod(hm, c->q[k] % c->q[i], c->q[i]);
+        }
+        K.q[i] = c->q[i];
+        K.ihat[i] = h_inv(hm, c->q[i]);
+        K.ihat_s[i] = (uint64_t)(((hu128)K.ihat[i] << 64) / c->q[i]);
+    }
+    for (int w = 0; w < W; ++w) K.halfQ[w] = (K.Q[w] >> 1) | (w + 1 < W ? K.Q[w + 1] << 63 : 0);
+}
+// INTT of the first k limbs and their centred CRT composition on the GPU: N doubles to the host
+static fhs_status decode_coeffs_dev(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<double>& m) {
+    const size_t N = c->N, bytes = 8ull * k * N;
+    fhs::CrtConsts K;
+    crt_consts(c, k, K);
+    uint64_t *tmp = nullptr, *dbl = nullptr;
+    HIPCHK(dalloc(c, &tmp, bytes), "decode");
+    hipError_t e = dalloc(c, &dbl, 8 * N);
+    if (e != hipSuccess) { dfree(c, tmp, bytes); return hip_fail(e, "decode"); }
+    e = hipMemcpyAsync(tmp, pt->d, bytes, hipMemcpyDeviceToDevice, c->st);
+    if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, tmp, k, k, 1, 0, c->st);
+    if (e == hipSuccess) e = fhs::launch_crt_compose(K, tmp, reinterpret_cast<double*>(dbl), (int)N, c->st);
+    m.resize(N);
+    if (e == hipSuccess) e = hipMemcpyAsync(m.data(), dbl, 8 * N, hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    dfree(c, dbl, 8 * N);
+    dfree(c, tmp, bytes);
+    if (e != hipSuccess) return hip_fail(e, "decode");
+    return FHS_OK;
+}
 static fhs_status decode_coeffs(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<uint64_t>& host) {
     const size_t N = c->N, bytes = 8ull * k * N;
     uint64_t* tmp = nullptr;
@@ -1745,6 +1801,17 @@ static fhs_status decode_coeffs(fhs_context* c, const fhs_plaintext* pt, int k, 
     dfree(c, tmp, bytes);
     return FHS_OK;
 }
+// centred coefficients of the first k limbs as doubles: composed on the GPU up to kCrtMaxL limbs (same
+// arithmetic, same doubles as the host composition, which FHESPEAR_DECODE_HOST_CRT=1 forces)
+static fhs_status decode_compose(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<double>& m) {
+    static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;   // A/B and test knob
+    if (k <= fhs::kCrtMaxL && !host_crt) return decode_coeffs_dev(c, pt, k, m);
+    std::vector<uint64_t> host;
+    const fhs_status s = decode_coeffs(c, pt, k, host);
+    if (s != FHS_OK) return s;
+    crt_compose(c, host, k, m);
+    return FHS_OK;
+}
 extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double* re_im) {
     ENTER(c);
     if (!pt || !re_im) return fail(FHS_ERR_INVALID, "decode: null argument");
@@ -1753,24 +1820,20 @@ extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double
     static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;   // A/B and test knob
     const int k = full ? l : decode_limbs(c, pt->scale, l), kk = std::min(l, k + 1);
     HostTrace ht;
-    std::vector<uint64_t> host;
-    fhs_status s = decode_coeffs(c, pt, kk, host);
-    if (s != FHS_OK) return s;
-    ht.mark("decode: intt + copy");
     std::vector<double> m;
-    crt_compose(c, host, kk, m);
+    fhs_status s = decode_compose(c, pt, kk, m);
+    if (s != FHS_OK) return s;
     if (k < kk) {   // |x| < Q_k / 4 (first k limbs) makes the k-limb and kk-limb compositions equal
         double qk = 1.0;
         for (int i = 0; i < k; ++i) qk *= (double)c->q[i];
         double mx = 0;
         for (size_t i = 0; i < N; ++i) mx = std::max(mx, std::fabs(m[i]));
         if (!(mx < 0.25 * qk) && kk < l) {   // |x| too large for the shortcut: all l limbs
-            s = decode_coeffs(c, pt, l, host);
+            s = decode_compose(c, pt, l, m);
             if (s != FHS_OK) return s;
-            crt_compose(c, host, l, m);
         }
     }
-    ht.mark("decode: crt");
+    ht.mark("decode: intt + crt");
     // slots z_j = m(zeta^(5^j)) = sum_{k < N/2} (m_k + i m_{k+N/2}) zeta^k omega^(s_j k), omega = zeta^4,
     // 5^j = 4 s_j + 1: an N/2-point FFT of the twisted half-pairs, read at s_j = slot_index[j] / 2
     const size_t n = N / 2;

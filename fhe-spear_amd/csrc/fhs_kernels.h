@@ -117,6 +117,17 @@ hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, 
                               double* out, hipStream_t st);
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st);
 hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st);
+// Centred CRT composition of the first l <= kCrtMaxL limbs (coefficient form) of one polynomial into
+// doubles, the exact integer converted word by word from the top (the host decoder's arithmetic,
+// fhs_host.hip crt_compose, so both give the same doubles)
+constexpr int kCrtMaxL = 7;
+struct CrtConsts {
+    int l, W;
+    u64 q[kCrtMaxL], ihat[kCrtMaxL], ihat_s[kCrtMaxL];
+    u64 hat[kCrtMaxL][kCrtMaxL + 1];
+    u64 Q[kCrtMaxL + 1], halfQ[kCrtMaxL + 1];
+};
+hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st);
 
 // per-limb constants for k_scalar (value mod q_i and its Shoup companion)
 constexpr int kMaxScalarLimbs = 64;

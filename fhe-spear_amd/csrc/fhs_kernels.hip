@@ -2260,6 +2260,70 @@ hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int coun
     return hipGetLastError();
 }
 
+// ============================================================================ decode: centred CRT
+__global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double* __restrict__ out, int N) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const int l = K.l, W = K.W;
+    u64 x[kCrtMaxL + 2];
+#pragma unroll
+    for (int w = 0; w < kCrtMaxL + 2; ++w) x[w] = 0;
+    for (int i = 0; i < l; ++i) {
+        const u64 a = limbs[(size_t)i * N + n], qi = K.q[i];
+        const u64 qh = __umul64hi(a, K.ihat_s[i]);
+        u64 y = a * K.ihat[i] - qh * qi;
+        if (y >= qi) y -= qi;
+        u64 carry = 0;   // x += hat_i * y over W words (each partial < 2^128: hi word + carries fit)
+        for (int w = 0; w < W; ++w) {
+            const u64 lo = K.hat[i][w] * y, hi = __umul64hi(K.hat[i][w], y);
+            const u64 s1 = lo + x[w];
+            const u64 c1 = s1 < lo;
+            const u64 s2 = s1 + carry;
+            const u64 c2 = s2 < s1;
+            x[w] = s2;
+            carry = hi + c1 + c2;
+        }
+        x[W] += carry;
+        for (;;) {   // x < 2Q: at most one subtraction
+            bool ge = x[W] != 0;
+            if (!ge) {
+                ge = true;
+                for (int w = W - 1; w >= 0; --w)
+                    if (x[w] != K.Q[w]) { ge = x[w] > K.Q[w]; break; }
+            }
+            if (!ge) break;
+            u64 br = 0;
+            for (int w = 0; w < W; ++w) {
+                const u64 qa = K.Q[w] + br;
+                const u64 nb = (qa < br) || (x[w] < qa);
+                x[w] -= qa;
+                br = nb;
+            }
+            x[W] -= br;
+        }
+    }
+    bool neg = false;
+    for (int w = W - 1; w >= 0; --w)
+        if (x[w] != K.halfQ[w]) { neg = x[w] > K.halfQ[w]; break; }
+    if (neg) {
+        u64 br = 0;
+        for (int w = 0; w < W; ++w) {
+            const u64 xa = x[w] + br;
+            const u64 nb = (xa < br) || (K.Q[w] < xa);
+            x[w] = K.Q[w] - xa;
+            br = nb;
+        }
+    }
+    double v = 0;   // v 2^64 is exact, so one rounding per step as on the host
+    for (int w = W - 1; w >= 0; --w) v = __dadd_rn(__dmul_rn(v, 18446744073709551616.0), (double)x[w]);
+    out[n] = neg ? -v : v;
+}
+hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st) {
+    if (K.l < 1 || K.l > kCrtMaxL || K.W != K.l + 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_crt_compose, dim3((N + 255) / 256), dim3(256), 0, st, K, limbs, out, N);
+    return hipGetLastError();
+}
+
 // ============================================================================ bootstrapping primitives
 // Constant products / sums (ckks_bootstrapper: pre-scale, EvalMod's Chebyshev coefficients and
 // constants, scale alignment).  A constant polynomial c has NTT image c in every slot, so both ops

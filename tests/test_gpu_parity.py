@@ -349,13 +349,23 @@ sq = ph.relinearize(ctx, prod, rk)
 q = [int(v) for v in ph.create_coeff_modulus(N, [59] * (L0 + P))][:L0]
 junk = ph.plaintext_from_numpy(ctx, np.stack([rng.integers(0, q[i], N, dtype=np.uint64) for i in range(L0)]), 1, 2.0 ** 40)
 out = [np.array(enc.decode_complex_vector(ctx, p)) for p in (pt, sk.decrypt(ctx, ct), sk.decrypt(ctx, sq), junk)]
+# a 7-limb ring: uniform limbs take the all-limb fallback through the widest GPU composition
+parms7 = ph.params(ph.scheme_type.ckks)
+parms7.set_poly_modulus_degree(N); parms7.set_special_modulus_size(1)
+parms7.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * 8))
+ctx7 = ph.context(parms7); enc7 = ph.ckks_encoder(ctx7)
+q7 = [int(v) for v in ctx7.primes][:7]
+for scale in (2.0 ** 40, 2.0 ** 100):
+    junk7 = ph.plaintext_from_numpy(ctx7, np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in q7]), 1, scale)
+    out.append(np.array(enc7.decode_complex_vector(ctx7, junk7)))
 np.save(sys.argv[1], np.stack(out))
 '''
 
 
 def test_decode_shortcut_equals_full_crt(require_gpu, tmp_path):
     """fhs_decode composes the centred CRT from the first k limbs (+1 as a check, full fallback);
-    its output must be bitwise identical to composing all limbs (FHESPEAR_DECODE_FULL=1): a
+    its output must be bitwise identical to composing all limbs (FHESPEAR_DECODE_FULL=1), and the
+    GPU composition (k_crt_compose, up to 7 limbs) to the host's (FHESPEAR_DECODE_HOST_CRT=1): a
     plaintext at 2^40, a fresh decryption at 2^59, a squared one at 2^118 and uniformly random limbs
     (|x| ~ Q/2, which takes the fallback)."""
     import os
@@ -365,17 +375,19 @@ def test_decode_shortcut_equals_full_crt(require_gpu, tmp_path):
     script.write_text(_DECODE_SCRIPT)
     pyp = str(REPO / "fhe-spear_amd" / "python")
     outs = []
-    for full in (False, True):
+    for i, knob in enumerate((None, "FHESPEAR_DECODE_FULL", "FHESPEAR_DECODE_HOST_CRT")):
         env = dict(os.environ)
         env.pop("FHESPEAR_DECODE_FULL", None)
-        if full:
-            env["FHESPEAR_DECODE_FULL"] = "1"
-        f = tmp_path / f"dec_{int(full)}.npy"
+        env.pop("FHESPEAR_DECODE_HOST_CRT", None)
+        if knob:
+            env[knob] = "1"
+        f = tmp_path / f"dec_{i}.npy"
         r = subprocess.run([_sys.executable, str(script), str(f), pyp], env=env, capture_output=True, text=True,
                            timeout=120)
         assert r.returncode == 0, r.stderr[-3000:]
         outs.append(np.load(f))
     assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
+    assert np.array_equal(outs[0].view(np.uint64), outs[2].view(np.uint64))
 
 
 _ENCODE_SCRIPT = r'''
