@@ -230,6 +230,10 @@ struct fhs_context {
     int device = 0;
     hipStream_t st = nullptr;
     hipStream_t st_aux = nullptr;          // second stream of the pipelined BSGS (memory-bound kernels)
+    // CU-partitioned stream pair for the pipelined BSGS (FHESPEAR_PIPE_CUS = k: k of every 32 CUs
+    // for the memory-bound stream, the rest for ModUp), with the events that order them on `st`
+    hipStream_t st_pm = nullptr, st_pa = nullptr;
+    hipEvent_t ev_pin = nullptr, ev_pout = nullptr;
     std::vector<hipEvent_t> bsgs_ev;       // cross-stream ordering events of launch_bsgs
     int bsgs_chunks = 1;                   // FHESPEAR_BSGS_CHUNKS (overlap measured slower)
     int bsgs_split_h = 0;                  // FHESPEAR_BSGS_SPLIT_H
@@ -363,6 +367,8 @@ static void free_key(fhs_context* c, uint64_t* key) {
 static void ctx_sync(fhs_context* c) {
     hipStreamSynchronize(c->st);
     if (c->st_aux) hipStreamSynchronize(c->st_aux);
+    if (c->st_pm) hipStreamSynchronize(c->st_pm);
+    if (c->st_pa) hipStreamSynchronize(c->st_pa);
 }
 // every cached block back to the device (the caller holds c->mu)
 static void trim_cache(fhs_context* c) {
@@ -805,6 +811,19 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     for (auto& ev : c->bsgs_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "bsgs events");
     if (const char* ch = getenv("FHESPEAR_BSGS_CHUNKS")) c->bsgs_chunks = std::max(1, std::min(16, atoi(ch)));
     if (const char* sh = getenv("FHESPEAR_BSGS_SPLIT_H")) c->bsgs_split_h = atoi(sh) != 0;
+    if (const char* pc = getenv("FHESPEAR_PIPE_CUS")) {
+        // mask word w bit b = CU 32 w + b: b < k in every word gives k CUs of each XCD (32 per XCD)
+        // whether the driver numbers CUs XCD-major or round-robin over the 8 XCDs
+        const int k = std::max(1, std::min(31, atoi(pc)));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, c->device), "device properties");
+        const int words = (prop.multiProcessorCount + 31) / 32;
+        std::vector<uint32_t> ma(words, (1u << k) - 1), mm(words, ~((1u << k) - 1));
+        HIPCHK(hipExtStreamCreateWithCUMask(&c->st_pa, words, ma.data()), "aux CU-mask stream");
+        HIPCHK(hipExtStreamCreateWithCUMask(&c->st_pm, words, mm.data()), "main CU-mask stream");
+        HIPCHK(hipEventCreateWithFlags(&c->ev_pin, hipEventDisableTiming), "pipe events");
+        HIPCHK(hipEventCreateWithFlags(&c->ev_pout, hipEventDisableTiming), "pipe events");
+    }
     c->stager = fhs::Stager{c.get(), stage_h2d};
     HIPCHK(hipMalloc(&c->items_dev, (sizeof(KsItem) + sizeof(void*)) * fhs_context::kMaxItems), "items buffer");
     c->tables.push_back(c->items_dev);
@@ -839,9 +858,13 @@ static void ctx_free(fhs_context* c) {
         Guard g(c);
         flush(c);
         hipStreamSynchronize(c->st);
-        if (c->st_aux) hipStreamSynchronize(c->st_aux);
+        ctx_sync(c);
         for (auto ev : c->bsgs_ev) hipEventDestroy(ev);
         if (c->st_aux) hipStreamDestroy(c->st_aux);
+        if (c->st_pm) hipStreamDestroy(c->st_pm);
+        if (c->st_pa) hipStreamDestroy(c->st_pa);
+        if (c->ev_pin) hipEventDestroy(c->ev_pin);
+        if (c->ev_pout) hipEventDestroy(c->ev_pout);
         for (void* p : c->tables) hipFree(p);
         for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
             if (c->scr[k]) hipFree(c->scr[k]);
@@ -2173,12 +2196,22 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     uint64_t* sum = nullptr;
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_SUM, 16 * S, &sum), "bsgs sum");
     ht.mark("workspaces");
-    const fhs::BsgsStreams ss{c->st, c->st_aux, c->bsgs_ev.data(), (int)c->bsgs_ev.size(), c->bsgs_chunks,
-                              c->bsgs_split_h};
+    const bool cu_split = c->st_pm && c->bsgs_chunks > 1;
+    if (cu_split) {   // the CU-partitioned pair runs the whole BSGS, ordered after and before `st`
+        HIPCHK(hipEventRecord(c->ev_pin, c->st), "bsgs");
+        HIPCHK(hipStreamWaitEvent(c->st_pm, c->ev_pin, 0), "bsgs");
+        HIPCHK(hipStreamWaitEvent(c->st_pa, c->ev_pin, 0), "bsgs");
+    }
+    const fhs::BsgsStreams ss{cu_split ? c->st_pm : c->st, cu_split ? c->st_pa : c->st_aux, c->bsgs_ev.data(),
+                              (int)c->bsgs_ev.size(), c->bsgs_chunks, c->bsgs_split_h};
     HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), akeys.data(), giant_elts, inner, sum, ws, wsb,
                             c->items_dev,
                             c->stager, ss, tm),
            "bsgs");
+    if (cu_split) {
+        HIPCHK(hipEventRecord(c->ev_pout, c->st_pm), "bsgs");
+        HIPCHK(hipStreamWaitEvent(c->st, c->ev_pout, 0), "bsgs");
+    }
     ht.mark("launch bsgs");
     fhs_ciphertext* r;
     if (!rescale) {
