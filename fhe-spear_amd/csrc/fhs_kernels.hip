@@ -26,6 +26,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #else
 #define FHS_KSIP_ATTR
 #endif
+#ifndef FHS_KSIP_UNROLL
+#define FHS_KSIP_UNROLL 2   // digits of the key inner product unrolled together (2: 64 VGPRs, 8 waves/SIMD)
+#endif
 #ifndef FHS_KSIP_PARTS
 #define FHS_KSIP_PARTS 1
 #endif
@@ -832,7 +835,7 @@ __device__ __forceinline__ void ks_digits(const DevTables& T, const u64* ex, con
     const int P_ = T.P;
     const size_t KN = (size_t)T.K * T.N;
     Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
-#pragma unroll 4
+#pragma unroll FHS_KSIP_UNROLL
     for (int j = 0; j < dn; ++j) {
         const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
         acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * KN)));
