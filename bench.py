@@ -357,6 +357,11 @@ def main():
                        "rotations_per_matvec": (G - 1) + (B - 1), "projections_per_rank": 1,
                        "parallelism": f"projection-parallel x{world}" + (" + RCCL gather" if world > 1 else "")},
             "sec_per_rwkv_block_8proj": block.get("sec_per_block") if block else None,
+            # north_star's block as 8 independent projections, one per GPU, outputs gathered to rank 0:
+            # this line's matvec leg at N ranks is exactly that (one projection per rank per step + RCCL
+            # gather), so 8 projections take 8 / value seconds; the client-aided block above keeps the
+            # reference's stage dependencies (r,k,v -> o -> FFN key -> FFN value) and is the latency figure
+            "sec_per_8proj_independent": round(8.0 / value, 6),
             "rwkv_block": block,
             "roofline": roof,
             "hadamard_roofline": had_roof,
