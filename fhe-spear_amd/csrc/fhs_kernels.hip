@@ -184,11 +184,11 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
     if constexpr (!ntt_half<LOGN>()) {
         constexpr int TH = N / 16;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = load(tid + c * TH);
+        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(tid + c * TH);
         __syncthreads();
         ntt_fwd_lds<LOGN, RL>(lds, tid, tw, R.q, R.lazy);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) store(tid + c * TH, fwd_canon(lds[lds_pad(tid + c * TH)], R));
+        for (int c = 0; c < 16; ++c) store(tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
     } else {
         constexpr int NH = N / 2, TH = N / 32;
         const u64 q = R.q, q2 = 2 * q;
@@ -199,7 +199,7 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
         for (int c = 0; c < 16; ++c) {
             const int e = tid + c * TH;
             const u64 xl = load(e), tt = shoup_lazy(load(e + NH), w0, w0p, q);
-            lds[lds_pad(e)] = xl + tt;
+            lds[row_pad<TH>(tid, c)] = xl + tt;
             hi[c] = xl + (q2 - tt);
         }
 #pragma unroll 1
@@ -207,12 +207,12 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
             if (h) {
                 __syncthreads();
 #pragma unroll
-                for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = hi[c];
+                for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
             }
             __syncthreads();
             ntt_fwd_lds<LOGN - 1, 3>(lds, tid, tw, q, R.lazy, 1 + h);
 #pragma unroll
-            for (int c = 0; c < 16; ++c) store(h * NH + tid + c * TH, fwd_canon(lds[lds_pad(tid + c * TH)], R));
+            for (int c = 0; c < 16; ++c) store(h * NH + tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
         }
     }
 }
@@ -225,11 +225,11 @@ __device__ __forceinline__ void inv_limb(u64* lds, int tid, const u64* __restric
     if constexpr (!ntt_half<LOGN>()) {
         constexpr int TH = N / 16;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = load(tid + c * TH);
+        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(tid + c * TH);
         __syncthreads();
         ntt_inv_lds<LOGN, RL>(lds, tid, tw, q, s0, s0s, s1, s1s);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) store(tid + c * TH, csub(lds[lds_pad(tid + c * TH)], q));
+        for (int c = 0; c < 16; ++c) store(tid + c * TH, csub(lds[row_pad<TH>(tid, c)], q));
     } else {
         constexpr int NH = N / 2, TH = N / 32;
         u64 lo[16];
@@ -237,19 +237,19 @@ __device__ __forceinline__ void inv_limb(u64* lds, int tid, const u64* __restric
         for (int h = 0; h < 2; ++h) {
             if (h) __syncthreads();
 #pragma unroll
-            for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = load(h * NH + tid + c * TH);
+            for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(h * NH + tid + c * TH);
             __syncthreads();
             ntt_inv_half_lds<LOGN - 1, 3>(lds, tid, tw, q, 1 + h);
             if (h == 0) {
 #pragma unroll
-                for (int c = 0; c < 16; ++c) lo[c] = lds[lds_pad(tid + c * TH)];
+                for (int c = 0; c < 16; ++c) lo[c] = lds[row_pad<TH>(tid, c)];
             }
         }
         const u64 q2 = 2 * q;
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
             const int e = tid + c * TH;
-            const u64 X = lo[c], Y = lds[lds_pad(e)];
+            const u64 X = lo[c], Y = lds[row_pad<TH>(tid, c)];
             store(e, csub(shoup_lazy(X + Y, s0, s0s, q), q));
             store(NH + e, csub(shoup_lazy(X - Y + q2, s1, s1s, q), q));
         }
@@ -462,13 +462,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const
     const PrimeK& P = PK(T, i);
     const u64* src = uniq[u] + (size_t)i * N;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[tid + c * TH];
+    for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = src[tid + c * TH];
     __syncthreads();
     const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
     ntt_inv_lds<LOGN, FHS_NTT_RL>(lds, tid, T.tw_inv + (size_t)i * N * 2, P.q, cst[0], cst[1], cst[2], cst[3]);
     u64* dst = acoef + ((size_t)u * l + i) * N;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[lds_pad(tid + k * TH)], P.q);
+    for (int k = 0; k < 16; ++k) dst[tid + k * TH] = csub(lds[row_pad<TH>(tid, k)], P.q);
     }
 }
 
@@ -492,12 +492,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
     for (int h = 0; h < 2; ++h) {
         if (h) __syncthreads();
 #pragma unroll
-        for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = src[h * NH + tid + c * TH];
+        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = src[h * NH + tid + c * TH];
         __syncthreads();
         ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL>(lds, tid, tw, q, 1 + h);
         if (h == 0) {
 #pragma unroll
-            for (int c = 0; c < 16; ++c) lo[c] = lds[lds_pad(tid + c * TH)];
+            for (int c = 0; c < 16; ++c) lo[c] = lds[row_pad<TH>(tid, c)];
         }
     }
     const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
@@ -506,7 +506,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        const u64 X = lo[c], Y = lds[lds_pad(e)];
+        const u64 X = lo[c], Y = lds[row_pad<TH>(tid, c)];
         dst[e] = csub(shoup_lazy(X + Y, s0, s0s, q), q);
         dst[NH + e] = csub(shoup_lazy(X - Y + q2, s1, s1s, q), q);
     }
@@ -675,7 +675,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        o[e] = fwd_canon(lds[lds_pad(e)], R);
+        o[e] = fwd_canon(lds[row_pad<TH>(tid, c)], R);
     }
     }
 }
@@ -761,7 +761,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
         for (int k = 0; k < CH; ++k) {   // global stage 0: (e, e + N/2), twiddle psi^rev(1)
             const int e = tid + (ch * CH + k) * TH;
             const u64 tt = shoup_lazy(x[CH + k], w0, w0p, m);
-            lds[lds_pad(e)] = x[k] + tt;
+            lds[row_pad<TH>(tid, ch * CH + k)] = x[k] + tt;
             hi[ch * CH + k] = x[k] + (q2 - tt);
         }
     }
@@ -770,7 +770,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
         if (h) {   // lower half written out: the upper half moves from registers into LDS
             __syncthreads();
 #pragma unroll
-            for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = hi[c];
+            for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
         }
         __syncthreads();
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, m, R.lazy, 1 + h);
@@ -778,7 +778,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
             const int e = tid + c * TH;
-            oh[e] = fwd_canon(lds[lds_pad(e)], R);
+            oh[e] = fwd_canon(lds[row_pad<TH>(tid, c)], R);
         }
     }
 }
@@ -1224,7 +1224,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
         const int e = tid + kk * TH;
         u128 s = {0, 0};
         for (int k = 0; k < P_; ++k) mac128(s, y[(size_t)k * N + e], T.md_hat[(size_t)k * T.L0 + i]);
-        lds[lds_pad(e)] = submod(reduce128(s.lo, s.hi, P), halfq, q);
+        lds[row_pad<TH>(tid, kk)] = submod(reduce128(s.lo, s.hi, P), halfq, q);
     }
     __syncthreads();
     const RedU RU = redu(P);
@@ -1236,7 +1236,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
-        const u64 v = fwd_canon(lds[lds_pad(e)], RU);
+        const u64 v = fwd_canon(lds[row_pad<TH>(tid, c)], RU);
         const u64 a = acc[(((size_t)r * 2 + comp) * E + i) * N + e];
         u64 res = shoup(submod(a, v, q), pinv, pinv_s, q);
         if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
@@ -1301,7 +1301,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
         for (int k = 0; k < 2; ++k) {   // global stage 0: (e, e + N/2)
             const int e = tid + (ch * 2 + k) * TH;
             const u64 tt = shoup_lazy(x[2 + k], w0, w0p, q);
-            lds[lds_pad(e)] = x[k] + tt;
+            lds[row_pad<TH>(tid, ch * 2 + k)] = x[k] + tt;
             hi[ch * 2 + k] = x[k] + (q2 - tt);
         }
     }
@@ -1315,14 +1315,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
         if (h) {
             __syncthreads();
 #pragma unroll
-            for (int c = 0; c < 16; ++c) lds[lds_pad(tid + c * TH)] = hi[c];
+            for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
         }
         __syncthreads();
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, q, RU.lazy, 1 + h);
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
             const int e = h * NH + tid + c * TH;
-            const u64 v = fwd_canon(lds[lds_pad(tid + c * TH)], RU);
+            const u64 v = fwd_canon(lds[row_pad<TH>(tid, c)], RU);
             u64 res = shoup(submod(ac[e], v, q), pinv, pinv_s, q);
             if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
             o[e] = res;

@@ -19,6 +19,28 @@
 namespace fhs {
 
 __device__ __forceinline__ int lds_pad(int e) { return e + (e >> 4); }
+// lds_pad(j0 + k TL) for the k-th element of a butterfly group, base = lds_pad(j0), as base plus a
+// compile-time offset wherever that is exact, so the LDS accesses take immediate offsets instead of
+// three address instructions each: TL % 16 == 0 (the stride adds whole pad blocks), or a group
+// that lies inside one aligned 16-word block (its span TL GS divides 16 and j0 % (TL GS) < TL).
+// lds_pad(tid + c TH) for the c-th row of a thread's strided sweep: lds_pad(tid) + a compile-time
+// offset when TH % 16 == 0 (c is unrolled, so the LDS access takes it as an immediate offset)
+template <int TH>
+__device__ __forceinline__ int row_pad(int tid, int c) {
+    if constexpr (TH % 16 == 0)
+        return lds_pad(tid) + c * (TH + TH / 16);
+    else
+        return lds_pad(tid + c * TH);
+}
+template <int TL, int GS>
+__device__ __forceinline__ int grp_pad(int j0, int base, int k) {
+    if constexpr (TL % 16 == 0)
+        return base + k * (TL + TL / 16);
+    else if constexpr (16 % (TL * GS) == 0)
+        return base + k * TL;
+    else
+        return lds_pad(j0 + k * TL);
+}
 
 __device__ __forceinline__ void ld_tw(const u64* __restrict__ tw, int idx, u64& w, u64& wp) {
     const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(tw + 2 * idx);
@@ -57,9 +79,17 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
         const int blk = TL >= 64 ? __builtin_amdgcn_readfirstlane(gid) / TL : gid / TL, off = gid % TL;
 #endif
         const int j0 = blk * 2 * TF + off;
+#ifdef FHS_NO_GRP_PAD
+        const int base = 0;
+#define FHS_GRP_ADDR(k) lds_pad(j0 + (k) * TL)
+#else
+        const int base = lds_pad(j0);
+#define FHS_GRP_ADDR(k) grp_pad<TL, GS>(j0, base, (k))
+#endif
+        (void)base;
         u64 x[GS];
 #pragma unroll
-        for (int k = 0; k < GS; ++k) x[k] = lds[lds_pad(j0 + k * TL)];
+        for (int k = 0; k < GS; ++k) x[k] = lds[FHS_GRP_ADDR(k)];
         if constexpr (FWD) {
 #pragma unroll
             for (int u = 0; u < R; ++u) {
@@ -98,7 +128,8 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
             }
         }
 #pragma unroll
-        for (int k = 0; k < GS; ++k) lds[lds_pad(j0 + k * TL)] = x[k];
+        for (int k = 0; k < GS; ++k) lds[FHS_GRP_ADDR(k)] = x[k];
+#undef FHS_GRP_ADDR
     }
 }
 
