@@ -50,6 +50,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #ifndef FHS_INNER_VEC
 #define FHS_INNER_VEC 2       // consecutive coefficients per lane in k_bsgs_inner (2: 16-byte loads)
 #endif
+#ifndef FHS_INNER_PREFETCH
+#define FHS_INNER_PREFETCH 0  // k_bsgs_inner: first diagonal batch requested before the LDS staging barrier
+#endif
 #ifndef FHS_MODUP_HALF
 #define FHS_MODUP_HALF 1      // k_modup_h: half-limb LDS, two workgroups per CU
 #endif
@@ -172,16 +175,31 @@ constexpr size_t lds_bytes() { return (size_t)((1 << LOGN) + (1 << LOGN) / 16) *
                               // (A/B at N = 16384: 2048-diagonal encode + matvec 18.64 -> 18.12 ms, bench unchanged)
 #endif
 template <int LOGN> constexpr bool ntt_half() { return LOGN >= FHS_NTT_HALF_MIN; }
-template <int LOGN> constexpr int ntt_threads() { return ntt_half<LOGN>() ? (1 << LOGN) / 32 : (1 << LOGN) / 16; }
-template <int LOGN> constexpr int ntt_lds_words() {
-    return ntt_half<LOGN>() ? (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16 : (1 << LOGN) + (1 << LOGN) / 16;
+template <int LOGN, bool H = ntt_half<LOGN>()> constexpr int ntt_threads() { return H ? (1 << LOGN) / 32 : (1 << LOGN) / 16; }
+template <int LOGN, bool H = ntt_half<LOGN>()> constexpr int ntt_lds_words() {
+    return H ? (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16 : (1 << LOGN) + (1 << LOGN) / 16;
 }
+// Launches with fewer workgroups than CUs (one transform per workgroup: the key switch's special
+// limbs, rescale, the giant-step tail) are latency-bound: there the full-limb form (both halves in
+// LDS at once, 1024 threads at N = 16384) finishes a transform in about half the time of the
+// half-limb form, which transforms its two halves one after the other.  Same values.
+#ifndef FHS_FULL_FORM_MAX_WG
+#define FHS_FULL_FORM_MAX_WG 256
+#endif
+#define FHS_NTT_LAUNCH(K, nwg, grid, st, ...)                                                          \
+    do {                                                                                               \
+        constexpr bool FH_ = (LOGN > 14);   /* the full-limb form needs N <= 16384 */                   \
+        if ((nwg) < FHS_FULL_FORM_MAX_WG && !FH_)                                                      \
+            hipLaunchKernelGGL((K<LOGN, FH_>), grid, dim3(ntt_threads<LOGN, FH_>()), 0, st, __VA_ARGS__); \
+        else                                                                                           \
+            hipLaunchKernelGGL((K<LOGN>), grid, dim3(ntt_threads<LOGN>()), 0, st, __VA_ARGS__);        \
+    } while (0)
 // forward: load(e) < 2q for every e < N; store(e, v) receives the canonical NTT value
-template <int LOGN, int RL, class Load, class Store>
+template <int LOGN, int RL, bool H = ntt_half<LOGN>(), class Load, class Store>
 __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restrict__ tw, const RedU& R, Load load,
                                          Store store) {
     constexpr int N = 1 << LOGN;
-    if constexpr (!ntt_half<LOGN>()) {
+    if constexpr (!H) {
         constexpr int TH = N / 16;
 #pragma unroll
         for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(tid + c * TH);
@@ -218,11 +236,11 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
 }
 // inverse with the last stage scaled by (s0, s1) (N^-1 and any per-limb constant folded in);
 // load(e) < 2q; store(e, v) receives the canonical coefficient
-template <int LOGN, int RL, class Load, class Store>
+template <int LOGN, int RL, bool H = ntt_half<LOGN>(), class Load, class Store>
 __device__ __forceinline__ void inv_limb(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
                                          u64 s1, u64 s1s, Load load, Store store) {
     constexpr int N = 1 << LOGN;
-    if constexpr (!ntt_half<LOGN>()) {
+    if constexpr (!H) {
         constexpr int TH = N / 16;
 #pragma unroll
         for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(tid + c * TH);
@@ -404,25 +422,25 @@ hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int l
 
 // ============================================================================ rescale (pb:185)
 // 1) last limb of each component -> coefficient form (scratch[comp])
-template <int LOGN>
-__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_rescale_intt(DevTables T, const u64* in, u64* scratch, int l) {
+template <int LOGN, bool H = ntt_half<LOGN>()>
+__global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_rescale_intt(DevTables T, const u64* in, u64* scratch, int l) {
     constexpr int N = 1 << LOGN;
-    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN, H>()];
     const int comp = blockIdx.x, pi = l - 1;
     const PrimeK& P = PK(T, pi);
     const u64* src = in + ((size_t)comp * l + pi) * N;
     u64* dst = scratch + (size_t)comp * N;
     const u64 half = P.q >> 1, q = P.q;
-    inv_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, q, P.ninv, P.ninv_s, P.w1ninv,
+    inv_limb<LOGN, FHS_NTT_RL, H>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, q, P.ninv, P.ninv_s, P.w1ninv,
                                P.w1ninv_s, [&](int e) { return src[e]; },
                                [&](int e, u64 v) { dst[e] = addmod(v, half, q); });
 }
 // 2) per (i < l-1, comp): NTT_i([v mod q_i] - [half mod q_i]) and combine (a_i - t) * q_last^-1
-template <int LOGN>
-__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_rescale_ntt(DevTables T, const u64* in, const u64* scratch,
+template <int LOGN, bool H = ntt_half<LOGN>()>
+__global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_rescale_ntt(DevTables T, const u64* in, const u64* scratch,
                                                                      u64* out, int l) {
     constexpr int N = 1 << LOGN;
-    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN, H>()];
     const int i = blockIdx.x, comp = blockIdx.y;
     const PrimeK& P = PK(T, i);
     const RedU RU = redu(P);
@@ -431,7 +449,7 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_rescale_ntt(DevTables T
     const u64* src = scratch + (size_t)comp * N;
     const u64* a = in + ((size_t)comp * l + i) * N;
     u64* o = out + ((size_t)comp * (l - 1) + i) * N;
-    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)i * N * 2, RU,
+    fwd_limb<LOGN, FHS_NTT_RL, H>(lds, threadIdx.x, T.tw_fwd + (size_t)i * N * 2, RU,
                                [&](int e) { return submod(reduce64(src[e], P), hq, q); },
                                [&](int e, u64 t) { o[e] = shoup(submod(a[e], t, q), inv, inv_s, q); });
 }
@@ -439,10 +457,8 @@ hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scra
                           hipStream_t st, const KTimer* tm) {
     FHS_TMARK(tm, KID_RESCALE, 1, st);
     FHS_DISPATCH_LOGN(T.logN, {
-        hipLaunchKernelGGL((k_rescale_intt<LOGN>), dim3(ncomp), dim3(ntt_threads<LOGN>()), 0, st, T,
-                           in, scratch, l);
-        hipLaunchKernelGGL((k_rescale_ntt<LOGN>), dim3(l - 1, ncomp), dim3(ntt_threads<LOGN>()), 0, st,
-                           T, in, scratch, out, l);
+        FHS_NTT_LAUNCH(k_rescale_intt, ncomp, dim3(ncomp), st, T, in, scratch, l);
+        FHS_NTT_LAUNCH(k_rescale_ntt, (l - 1) * ncomp, dim3(l - 1, ncomp), st, T, in, scratch, out, l);
     });
     FHS_TMARK(tm, KID_RESCALE, 0, st);
     return hipGetLastError();
@@ -454,8 +470,8 @@ hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scra
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const u64* const* uniq, u64* acoef, int l, int U) {
     constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[ntt_half<LOGN>() ? 1 : (1 << LOGN) + (1 << LOGN) / 16];
-    if constexpr (!ntt_half<LOGN>()) {   // full-limb form: N <= 16384 only
+    __shared__ __attribute__((aligned(16))) u64 lds[LOGN > 14 ? 1 : (1 << LOGN) + (1 << LOGN) / 16];
+    if constexpr (LOGN <= 14) {   // full-limb form: N <= 16384 only (small launches, ks_intt_half())
     const int tid = threadIdx.x;
     int i, u;
     if (!plain_tm(l, U, i, u)) return;
@@ -510,6 +526,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
         dst[e] = csub(shoup_lazy(X + Y, s0, s0s, q), q);
         dst[NH + e] = csub(shoup_lazy(X - Y + q2, s1, s1s, q), q);
     }
+}
+
+// k_ks_intt_h (half limb, two workgroups per CU) unless the launch has fewer workgroups than CUs
+// (e.g. the baby-step input alone, l workgroups): then the full-limb k_ks_intt halves the latency.
+template <int LOGN>
+static bool ks_intt_half(int nwg) {
+    if (LOGN <= 14 && nwg < FHS_FULL_FORM_MAX_WG) return false;
+    return (FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>();
 }
 
 // Exact centred-extension count, slow path (|frac - 1/2| < 2^-58; never seen on random data
@@ -568,13 +592,13 @@ __device__ __noinline__ int centered_exact(const u64* y, const u64* qs, int ns, 
 // (a2) v[u][j][n] = round(sum_{u in digit j} y_u / q_u): fixed-point fast path (error < 2 ns ulp
 // of 2^-64), exact fallback within 64 ulp of a half (oracle: ock_centered_count).
 __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, int l, int U) {
+    // grid (N / 256, U dn): the (input, digit) pair is per workgroup, so no 64-bit index division
     const int N = T.N, P_ = T.P, dn = (l + P_ - 1) / P_;
-    const size_t total = (size_t)U * dn * N;
-    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (size_t)gridDim.x * blockDim.x) {
-        const int n = (int)(idx % N);
-        const int j = (int)((idx / N) % dn);
-        const int u = (int)(idx / ((size_t)N * dn));
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y % dn, u = blockIdx.y / dn;
+    if (n >= N || u >= U) return;
+    const size_t idx = ((size_t)u * dn + j) * N + n;
+    {
         const int s0 = j * P_, ns = min(s0 + P_, l) - s0;
         const u64* yb = acoef + ((size_t)u * l + s0) * N + n;
         int v;
@@ -584,8 +608,8 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
             const u64* R = T.modup_R + (((size_t)l * T.dnum + j) * P_) * 2;
             u64 lo = 0, ys[8], qs[8];
             int carry = 0;
+            for (int k = 0; k < ns; ++k) ys[k] = yb[(size_t)k * N];
             for (int k = 0; k < ns; ++k) {
-                ys[k] = yb[(size_t)k * N];
                 qs[k] = PK(T, s0 + k).q;
                 const u64 F = ys[k] * R[2 * k + 1] + __umul64hi(ys[k], R[2 * k]);
                 lo += F;
@@ -597,6 +621,10 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
         }
         vout[idx] = (unsigned char)v;
     }
+}
+static void launch_centered(const DevTables& T, const u64* acoef, unsigned char* vout, int l, int U, hipStream_t st) {
+    const int dn = (l + T.P - 1) / T.P;
+    hipLaunchKernelGGL(k_centered, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, vout, l, U);
 }
 
 // (b1) ModUp + NTT: ext[u][j][t] = NTT_t(centred conv_{digit j -> t}(y_u)) for t outside digit
@@ -729,6 +757,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
         Acc3 a3[2 * CH];
 #pragma unroll
         for (int k = 0; k < 2 * CH; ++k) a3[k] = Acc3{0, 0, 0};
+        // the centred counts of this chunk, loaded together up front (one latency, not one per element)
+        uint32_t vv[2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) vv[k] = vb[tid + (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0)];
 #pragma unroll 1
         for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
             const Split30 hw = split30(hat[(size_t)w * K]);
@@ -743,17 +775,19 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
             for (int k = 0; k < 2 * CH; ++k) acc3_mac(a3[k], split30(y[k]), hw);
         }
         u64 x[2 * CH];
+        if (R.cpm) {   // - v Q_S folded into L as v (m - Q_S mod m); result in [0, 2q)
 #pragma unroll
-        for (int k = 0; k < 2 * CH; ++k) {
-            const int e = tid + (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);
-            if (R.cpm) {   // - v Q_S folded into L as v (m - Q_S mod m); result in [0, 2q)
-                const uint32_t v = vb[e];
+            for (int k = 0; k < 2 * CH; ++k) {
+                const uint32_t v = vv[k];
                 const u64 vq = mul32w(v, (uint32_t)negQ) + ((u64)(v * (uint32_t)(negQ >> 32)) << 32);
                 x[k] = acc3_reduce_pm(a3[k].L + vq, a3[k].M, a3[k].H, R.b, R.d);
-            } else {
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2 * CH; ++k) {
                 u128 acc = {0, 0};
                 acc3_fold(acc, a3[k]);
-                mac128(acc, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
+                mac128(acc, (u64)(ns - vv[k]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
                 x[k] = submod(reduce128(acc.lo, acc.hi, R), nsQm, m);
             }
         }
@@ -1182,11 +1216,11 @@ __global__ void __launch_bounds__(256) k_giant_ip_reduce(DevTables T, const KsIt
 }
 
 // (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
-template <int LOGN>
-__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ks_special_intt(DevTables T, const u64* acc, u64* ycoef, int l,
+template <int LOGN, bool H = ntt_half<LOGN>()>
+__global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_ks_special_intt(DevTables T, const u64* acc, u64* ycoef, int l,
                                                                          int R) {
     constexpr int N = 1 << LOGN;
-    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN, H>()];
     const int k = blockIdx.x, comp = blockIdx.y, r = blockIdx.z;
     const int P_ = T.P, E = l + P_, pi = T.L0 + k;
     const PrimeK& P = PK(T, pi);
@@ -1194,7 +1228,7 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ks_special_intt(DevTabl
     u64* dst = ycoef + (((size_t)r * 2 + comp) * P_ + k) * N;
     const u64* cst = T.md_intt + (size_t)k * 4;
     const u64 p = P.q, half = T.ks_seal ? p >> 1 : 0;   // SEAL: + floor(p/2) turns the floor into rounding
-    inv_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3],
+    inv_limb<LOGN, FHS_NTT_RL, H>(lds, threadIdx.x, T.tw_inv + (size_t)pi * N * 2, P.q, cst[0], cst[1], cst[2], cst[3],
                                [&](int e) { return src[e]; }, [&](int e, u64 v) { dst[e] = csub(csub(v, p) + half, p); });
 }
 
@@ -1386,11 +1420,11 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     unsigned char* vcnt = reinterpret_cast<unsigned char*>(ycoef + (size_t)R * 2 * T.P * N);
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
+    if (ks_intt_half<LOGN>(l * U))
         hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, l, U);
     else
         hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, acoef, l, U);
-    hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, acoef, vcnt, l, U);
+    launch_centered(T, acoef, vcnt, l, U, st);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
     launch_modup<LOGN>(T, uniq, acoef, vcnt, ext, l, U, st);
@@ -1400,7 +1434,7 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
                        0);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, st, T, acc, ycoef, l, R);
+    FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), st, T, acc, ycoef, l, R);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
     *acc_out = acc;
     *ycoef_out = ycoef;
@@ -1477,13 +1511,25 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     const int N = T.N;
     const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t S = (size_t)l * N;
+    const size_t off = (size_t)i * N + n0 + lane * VEC;
+#if FHS_INNER_PREFETCH
+    // the first 8 diagonals of this wave's first group are requested before the baby-step slice is
+    // staged, so the staging and its barrier overlap the diagonal stream instead of stalling it
+    u64 pf[8][VEC];
+    bool have_pf = false;
+    if (g0 + wave < g1 && min(G, D - (g0 + wave) * G) >= 8) {
+        const u64* const* pg0 = pts + (size_t)(g0 + wave) * G;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + off, pf[u]);
+        have_pf = true;
+    }
+#endif
     for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
         const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
         sb[idx] = pack30(baby[b][comp * S + (size_t)i * N + n0 + c]);
     }
     __syncthreads();
     const RedU R = redu(PK(T, i));
-    const size_t off = (size_t)i * N + n0 + lane * VEC;
     for (int g = g0 + wave; g < g1; g += WAVES) {
         const int bmax = min(G, D - g * G);
         if (bmax <= 0) continue;
@@ -1499,8 +1545,19 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
         // 8 diagonal loads in flight per wave-iteration, folded into the 128-bit sums every 8
         for (; b + 8 <= bmax; b += 8) {
             u64 p[8][VEC];
+#if FHS_INNER_PREFETCH
+            if (have_pf) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + off, p[u]);
+                for (int u = 0; u < 8; ++u)
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) p[u][v] = pf[u][v];
+                have_pf = false;
+            } else
+#endif
+            {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + off, p[u]);
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u)
 #pragma unroll
@@ -1584,17 +1641,17 @@ __global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, con
         base[idx] = bv;
     }
 }
-template <int LOGN>
-__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_giant_final(DevTables T, const u64* base, const u64* convsum,
+template <int LOGN, bool H = ntt_half<LOGN>()>
+__global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_giant_final(DevTables T, const u64* base, const u64* convsum,
                                                                      u64* out, int l) {
     constexpr int N = 1 << LOGN;
-    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN, H>()];
     const int i = blockIdx.x, comp = blockIdx.y;
     const PrimeK& P = PK(T, i);
     const RedU RU = redu(P);
     const size_t off = ((size_t)comp * l + i) * N;
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1], q = RU.q;
-    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)i * N * 2, RU,
+    fwd_limb<LOGN, FHS_NTT_RL, H>(lds, threadIdx.x, T.tw_fwd + (size_t)i * N * 2, RU,
                                [&](int e) { return convsum[off + e]; },
                                [&](int e, u64 v) { out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, q), q); });
 }
@@ -1626,11 +1683,11 @@ static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, in
     const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
     const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
-    if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
+    if (ks_intt_half<LOGN>(l * U))
         hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, b.acoef, l, U);
     else
         hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, b.acoef, l, U);
-    hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)U * dn * N)), dim3(256), 0, st, T, b.acoef, b.vcnt, l, U);
+    launch_centered(T, b.acoef, b.vcnt, l, U, st);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
     launch_modup<LOGN>(T, uniq, b.acoef, b.vcnt, b.ext, l, U, st);
@@ -1658,7 +1715,7 @@ static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* cons
                            l, R, ksip_parts(R));
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
-    hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, st, T, b.acc, b.ycoef, l, R);
+    FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), st, T, b.acc, b.ycoef, l, R);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
 }
 
@@ -1823,13 +1880,12 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                 const KsBufs b = ks_carve(T, ws, R, R, l);
                 const int E = l + T.P, dn = (l + T.P - 1) / T.P;
                 FHS_TMARK(tm, KID_KS_INTT, 1, sm);
-                if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
+                if (ks_intt_half<LOGN>(l * R))
                     hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * R), dim3((1 << LOGN) / 32), 0, sm, T, uq, b.acoef, l,
                                        R);
                 else
                     hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * R), dim3((1 << LOGN) / 16), 0, sm, T, uq, b.acoef, l, R);
-                hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)R * dn * N)), dim3(256), 0, sm, T, b.acoef, b.vcnt,
-                                   l, R);
+                launch_centered(T, b.acoef, b.vcnt, l, R, sm);
                 FHS_TMARK(tm, KID_KS_INTT, 0, sm);
                 FHS_TMARK(tm, KID_KS_FUSED, 1, sm);
                 hipLaunchKernelGGL((k_ks_giant_fused<LOGN>), dim3(xcd_grid(E, R)), dim3((1 << LOGN) / 16), 0, sm, T, it, uq,
@@ -1839,16 +1895,14 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                 hipLaunchKernelGGL(k_giant_ip_reduce, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, it, b.acc, l, R);
                 FHS_TMARK(tm, KID_KS_IP, 0, sm);
                 FHS_TMARK(tm, KID_SPECIAL_INTT, 1, sm);
-                hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, sm, T, b.acc,
-                                   b.ycoef, l, R);
+                FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), sm, T, b.acc, b.ycoef, l, R);
                 FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sm);
                 FHS_TMARK(tm, KID_GIANT_SUM, 1, sm);
                 hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, b.acc, b.ycoef, inner, base,
                                    convsum, l, R, 1, 1);
                 FHS_TMARK(tm, KID_GIANT_SUM, 0, sm);
                 FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-                hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum,
-                                   out, l);
+                FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), sm, T, base, convsum, out, l);
                 FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
             }
         });
@@ -1865,12 +1919,11 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             const size_t E = l + T.P, dn = (l + T.P - 1) / T.P;
             hipStreamWaitEvent(sm, evH[0], 0);
             FHS_TMARK(tm, KID_KS_INTT, 1, sm);
-            if ((FHS_INTT_HALF && LOGN >= 9) || ntt_half<LOGN>())
+            if (ks_intt_half<LOGN>(l * R))
                 hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * R), dim3((1 << LOGN) / 32), 0, sm, T, uq, all.acoef, l, R);
             else
                 hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * R), dim3((1 << LOGN) / 16), 0, sm, T, uq, all.acoef, l, R);
-            hipLaunchKernelGGL(k_centered, dim3(eltwise_grid((size_t)R * dn * N)), dim3(256), 0, sm, T, all.acoef, all.vcnt,
-                               l, R);
+            launch_centered(T, all.acoef, all.vcnt, l, R, sm);
             FHS_TMARK(tm, KID_KS_INTT, 0, sm);
             const int NB = T.N >> 8;
             for (int c = 0; c < C; ++c) {
@@ -1889,8 +1942,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                 FHS_TMARK(tm, KID_KS_IP, 0, sa);
             }
             FHS_TMARK(tm, KID_SPECIAL_INTT, 1, sa);
-            hipLaunchKernelGGL((k_ks_special_intt<LOGN>), dim3(T.P, 2, R), dim3(ntt_threads<LOGN>()), 0, sa, T, all.acc,
-                               all.ycoef, l, R);
+            FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), sa, T, all.acc, all.ycoef, l, R);
             FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sa);
             FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
             hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, all.acc, all.ycoef, inner, base,
@@ -1899,7 +1951,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             hipEventRecord(ev_end, sa);
             hipStreamWaitEvent(sm, ev_end, 0);
             FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-            hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum, out, l);
+            FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), sm, T, base, convsum, out, l);
             FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
         });
         return hipGetLastError();
@@ -1931,7 +1983,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         hipEventRecord(ev_end, sa);
         hipStreamWaitEvent(sm, ev_end, 0);
         FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-        hipLaunchKernelGGL((k_giant_final<LOGN>), dim3(l, 2), dim3(ntt_threads<LOGN>()), 0, sm, T, base, convsum, out, l);
+        FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), sm, T, base, convsum, out, l);
         FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
     });
     return hipGetLastError();
