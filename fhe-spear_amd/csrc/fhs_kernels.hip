@@ -51,7 +51,7 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_INNER_VEC 2       // consecutive coefficients per lane in k_bsgs_inner (2: 16-byte loads)
 #endif
 #ifndef FHS_INNER_PREFETCH
-#define FHS_INNER_PREFETCH 0  // k_bsgs_inner: first diagonal batch requested before the LDS staging barrier
+#define FHS_INNER_PREFETCH 1  // k_bsgs_inner: first diagonal batch requested before the LDS staging barrier
 #endif
 #ifndef FHS_MODUP_HALF
 #define FHS_MODUP_HALF 1      // k_modup_h: half-limb LDS, two workgroups per CU
