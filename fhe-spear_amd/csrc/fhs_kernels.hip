@@ -50,6 +50,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #ifndef FHS_INNER_VEC
 #define FHS_INNER_VEC 2       // consecutive coefficients per lane in k_bsgs_inner (2: 16-byte loads)
 #endif
+#ifndef FHS_MODUP_Y3
+#define FHS_MODUP_Y3 0        // k_modup_h: a 3-limb digit's conversion loads issued together per chunk
+#endif
 #ifndef FHS_INNER_PREFETCH
 #define FHS_INNER_PREFETCH 1  // k_bsgs_inner: first diagonal batch requested before the LDS staging barrier
 #endif
@@ -761,6 +764,24 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
         uint32_t vv[2 * CH];
 #pragma unroll
         for (int k = 0; k < 2 * CH; ++k) vv[k] = vb[tid + (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0)];
+#if FHS_MODUP_Y3
+        if (ns == 3) {   // the usual digit of P = 3 limbs: all of the chunk's loads issued together
+            u64 y[3][2 * CH];
+#pragma unroll
+            for (int w = 0; w < 3; ++w)
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    y[w][k] = yb[(size_t)w * N + tid + (ch * CH + k) * TH];
+                    y[w][CH + k] = yb[(size_t)w * N + tid + (ch * CH + k) * TH + NH];
+                }
+#pragma unroll
+            for (int w = 0; w < 3; ++w) {
+                const Split30 hw = split30(hat[(size_t)w * K]);
+#pragma unroll
+                for (int k = 0; k < 2 * CH; ++k) acc3_mac(a3[k], split30(y[w][k]), hw);
+            }
+        } else
+#endif
 #pragma unroll 1
         for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
             const Split30 hw = split30(hat[(size_t)w * K]);
@@ -1353,13 +1374,37 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
         }
         __syncthreads();
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, q, RU.lazy, 1 + h);
+        // outputs in batches of 4 whose accumulator (and rotated c0) loads are issued together, with
+        // the add / no-add choice outside the loop (one latency per batch, not one per coefficient)
+        if (add) {
+            const u64* ad = add + (size_t)i * N;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            const int e = h * NH + tid + c * TH;
-            const u64 v = fwd_canon(lds[row_pad<TH>(tid, c)], RU);
-            u64 res = shoup(submod(ac[e], v, q), pinv, pinv_s, q);
-            if (add) res = addmod(res, add[(size_t)i * N + galois_src(e, aelt, LOGN)], q);
-            o[e] = res;
+            for (int c0 = 0; c0 < 16; c0 += 4) {
+                u64 av[4], dv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int e = h * NH + tid + (c0 + k) * TH;
+                    av[k] = ac[e];
+                    dv[k] = ad[galois_src(e, aelt, LOGN)];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const u64 v = fwd_canon(lds[row_pad<TH>(tid, c0 + k)], RU);
+                    o[h * NH + tid + (c0 + k) * TH] = addmod(shoup(submod(av[k], v, q), pinv, pinv_s, q), dv[k], q);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int c0 = 0; c0 < 16; c0 += 4) {
+                u64 av[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) av[k] = ac[h * NH + tid + (c0 + k) * TH];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const u64 v = fwd_canon(lds[row_pad<TH>(tid, c0 + k)], RU);
+                    o[h * NH + tid + (c0 + k) * TH] = shoup(submod(av[k], v, q), pinv, pinv_s, q);
+                }
+            }
         }
     }
 }
@@ -1599,26 +1644,43 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
 //   sum_r ModDown(acc_r) = (sum_r acc_r - NTT(sum_r conv(y_r))) * P^-1   (mod q_i)
 // is bit-identical to rotating and adding one giant step at a time (bg:478-483).
 // base_c = (sum_r acc_r,c) P^-1 + [c==0] sum_r galois_r(inner_r.c0) + inner_0.c ;  convsum_c = sum_r conv(y_r,c)
-__global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, const u64* inner0, u64* base,
-                            u64* convsum, int l, int R, int first, int nparts) {
+// Grid (N / 256, 2 components, ceil(l / FHS_GSUM_ICH) target-limb chunks).  The conversion is linear
+// in the rotations, so sum_r sum_k y_rk hat_ki = sum_k hat_ki (sum_r y_rk): each thread sums its
+// coefficient's R P special values once as exact 128-bit integers (< R 2^60) and reduces those P sums
+// into each target limb of its chunk -- the same residues as converting rotation by rotation, with
+// the special values read once per chunk instead of once per target limb.
+#ifndef FHS_GSUM_ICH
+#define FHS_GSUM_ICH 4
+#endif
+__global__ void __launch_bounds__(256) k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, const u64* inner0,
+                                                   u64* base, u64* convsum, int l, int R, int first, int nparts) {
     const int N = T.N, P_ = T.P, E = l + P_;
+    const int n = blockIdx.x * blockDim.x + threadIdx.x, comp = blockIdx.y;
+    if (n >= N) return;
+    const int i0 = blockIdx.z * FHS_GSUM_ICH, i1 = min(i0 + FHS_GSUM_ICH, l);
     const size_t S = (size_t)l * N;
-    const size_t total = 2 * S;
-    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (size_t)gridDim.x * blockDim.x) {
-        const int comp = (int)(idx / S);
-        const int i = (int)((idx % S) / N), n = (int)(idx % N);
+    constexpr int PMAX = 8;   // special primes per context (context_create limit)
+    u64 ylo[PMAX], yhi[PMAX];
+#pragma unroll
+    for (int k = 0; k < PMAX; ++k) ylo[k] = yhi[k] = 0;
+    for (int r = 0; r < R; ++r) {
+        const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N + n;
+#pragma unroll
+        for (int k = 0; k < PMAX; ++k) {
+            if (k < P_) {
+                const u64 v = y[(size_t)k * N];
+                ylo[k] += v;
+                yhi[k] += ylo[k] < v;
+            }
+        }
+    }
+    for (int i = i0; i < i1; ++i) {
         const PrimeK& P = PK(T, i);
         const u64 q = P.q;
         u128 cs = {0, 0};
-        int cnt = 0;
-        for (int r = 0; r < R; ++r) {
-            const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N + n;
-            for (int k = 0; k < P_; ++k) {
-                mac128(cs, y[(size_t)k * N], T.md_hat[(size_t)k * T.L0 + i]);
-                if (++cnt == 48) { cs.lo = reduce128(cs.lo, cs.hi, P); cs.hi = 0; cnt = 0; }
-            }
-        }
+#pragma unroll
+        for (int k = 0; k < PMAX; ++k)
+            if (k < P_) mac128(cs, reduce128(ylo[k], yhi[k], P), T.md_hat[(size_t)k * T.L0 + i]);
         // chunks of rotations accumulate mod q: both sums are linear in the rotations
         if (T.ks_seal) {   // SEAL rounding: each of the R conversions carries - floor(p/2) mod q_i
             u128 h = {0, 0};
@@ -1629,6 +1691,7 @@ __global__ void k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, con
             cs.lo = submod(cs.lo, rh, q);
         }
         u64 cv = reduce128(cs.lo, cs.hi, P);
+        const size_t idx = (size_t)comp * S + (size_t)i * N + n;
         u64 bv = bpart[((size_t)comp * E + i) * N + n];
         for (int p = 1; p < nparts; ++p) bv = addmod(bv, bpart[(((size_t)p * 2 + comp) * E + i) * N + n], q);
         if (first) {
@@ -1898,7 +1961,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                 FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), sm, T, b.acc, b.ycoef, l, R);
                 FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sm);
                 FHS_TMARK(tm, KID_GIANT_SUM, 1, sm);
-                hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, b.acc, b.ycoef, inner, base,
+                hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0, sm, T, b.acc, b.ycoef, inner, base,
                                    convsum, l, R, 1, 1);
                 FHS_TMARK(tm, KID_GIANT_SUM, 0, sm);
                 FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
@@ -1945,7 +2008,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), sa, T, all.acc, all.ycoef, l, R);
             FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sa);
             FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
-            hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, all.acc, all.ycoef, inner, base,
+            hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0, sa, T, all.acc, all.ycoef, inner, base,
                                convsum, l, R, 1, C);
             FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
             hipEventRecord(ev_end, sa);
@@ -1976,7 +2039,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
             hipStreamWaitEvent(sa, evF[c], 0);
             giant_ip_stage<LOGN>(T, it + rb(c), uq + rb(c), Rc, l, bc, sa, tm);
             FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
-            hipLaunchKernelGGL(k_giant_sum, dim3(eltwise_grid(2 * S)), dim3(256), 0, sa, T, bc.acc, bc.ycoef, inner, base,
+            hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0, sa, T, bc.acc, bc.ycoef, inner, base,
                                convsum, l, Rc, c == 0 ? 1 : 0, (FHS_KSIP_VEC == 2 && T.N >= 512) ? 1 : ksip_parts(Rc));
             FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
         }
