@@ -303,10 +303,12 @@ def test_pseudo_mersenne_reduction_matches_bigint(orc):
 def test_device_ntt_passes_emulated_match_direct_evaluation(tmp_path):
     """fhs_ntt.h's forward (Harvey and lazy) and inverse passes, compiled for the host through a
     shim header and run thread-by-thread between barriers, against a direct O(N^2) evaluation
-    a(psi^(2 rev(i) + 1)) -- the same convention the oracle pins (test_ntt_is_evaluation_at_odd_powers)."""
+    a(psi^(2 rev(i) + 1)) -- the same convention the oracle pins (test_ntt_is_evaluation_at_odd_powers).
+    The Shoup products take their plain C form here (FHS_ASM_SHOUP=0): the default form is gfx950
+    inline asm, pinned bit-exact against the oracle by the GPU tests."""
     import subprocess
     exe = tmp_path / "ntt_emu"
-    subprocess.run(["g++", "-O2", "-std=c++17", f"-I{REPO / 'tools/debug/shim'}", f"-I{REPO / 'fhe-spear_amd/csrc'}",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-DFHS_ASM_SHOUP=0", f"-I{REPO / 'tools/debug/shim'}", f"-I{REPO / 'fhe-spear_amd/csrc'}",
                     str(REPO / "tools/debug/ntt_emu.cpp"), "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
