@@ -608,19 +608,35 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
         if (ns == 1) {   // SEAL: the limb's residue in [0, q) is lifted as is
             v = T.ks_seal ? 0 : (yb[0] > (PK(T, s0).q >> 1) ? 1 : 0);
         } else {
+            // fixed-point fast path in registers (a guarded unrolled loop: no private arrays, so no
+            // scratch traffic); the exact path re-reads the digit into its own arrays
             const u64* R = T.modup_R + (((size_t)l * T.dnum + j) * P_) * 2;
-            u64 lo = 0, ys[8], qs[8];
+            constexpr int PMAX = 8;   // digit size P (context_create limit)
+            u64 y[PMAX];
+#pragma unroll
+            for (int k = 0; k < PMAX; ++k) y[k] = k < ns ? yb[(size_t)k * N] : 0;
+            u64 lo = 0;
             int carry = 0;
-            for (int k = 0; k < ns; ++k) ys[k] = yb[(size_t)k * N];
-            for (int k = 0; k < ns; ++k) {
-                qs[k] = PK(T, s0 + k).q;
-                const u64 F = ys[k] * R[2 * k + 1] + __umul64hi(ys[k], R[2 * k]);
-                lo += F;
-                carry += lo < F;
+#pragma unroll
+            for (int k = 0; k < PMAX; ++k) {
+                if (k < ns) {
+                    const u64 F = y[k] * R[2 * k + 1] + __umul64hi(y[k], R[2 * k]);
+                    lo += F;
+                    carry += lo < F;
+                }
             }
             const u64 half = 1ULL << 63;
             const u64 d = lo >= half ? lo - half : half - lo;
-            v = d > 64 ? carry + (lo >= half ? 1 : 0) : centered_exact(ys, qs, ns, carry);
+            if (d > 64) {
+                v = carry + (lo >= half ? 1 : 0);
+            } else {
+                u64 ys[PMAX], qs[PMAX];
+                for (int k = 0; k < ns; ++k) {
+                    ys[k] = yb[(size_t)k * N];
+                    qs[k] = PK(T, s0 + k).q;
+                }
+                v = centered_exact(ys, qs, ns, carry);
+            }
         }
         vout[idx] = (unsigned char)v;
     }
