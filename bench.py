@@ -43,6 +43,7 @@ CONFIGS = {
                  workload="client-aided RWKV-7 block d=2048 F=8192 N=16384 L0=36 P=3: 8 BSGS projections, "
                           "pre-encoded diagonals resident in HBM"),
 }
+SK_SEED, INPUT_SEED, DIAG_SEED = 1000, 10000, 2   # tests/golden/make_bench_digest.py
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 BFLY_PEAK_GOPS = 1466.6        # measured lazy NTT butterflies/s, registers only (tools/microbench/bfly.hip)
 
@@ -104,6 +105,19 @@ def latest_traffic_record(config):
     return None, None
 
 
+def limb_digest_check(config, limbs, suffix=""):
+    """SHA-256 of the output limbs vs the oracle's digest of the same workload (rank 0 seeds)."""
+    import hashlib
+    got = hashlib.sha256(np.ascontiguousarray(limbs).tobytes()).hexdigest()
+    man = json.loads((REPO / "tests" / "golden" / "manifest.json").read_text()).get("bench_digests", {})
+    rec = man.get(config + suffix)
+    key = f"{config}{suffix}_sha256_match"
+    if rec is None:
+        return {key: None, "sha256": got, "note": "no oracle digest committed for this configuration"}
+    return {key: got == rec["sha256"], "sha256": got, "oracle_sha256": rec["sha256"],
+            "source": "tests/golden/manifest.json bench_digests (C oracle, tests/golden/make_bench_digest.py)"}
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -137,6 +151,8 @@ def main():
     ap.add_argument("--no-block", action="store_true",
                     help="skip the measured RWKV-block leg (cfg3 on the same ranks) of the default line")
     ap.add_argument("--block-steps", type=int, default=3)
+    ap.add_argument("--no-seal", action="store_true", help="skip the SEAL-convention (P = 1) matvec leg")
+    ap.add_argument("--seal-steps", type=int, default=5)
     ap.add_argument("--block-dealt", action="store_true",
                     help="block leg over N GPUs: deal each stage's projections only (default at N > 1: latency "
                          "mode, each projection's giant steps sharded over a rank group as with --split)")
@@ -177,16 +193,16 @@ def main():
     parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(steps, N))))
     parms.set_coeff_modulus(primes)
     ctx = ph.context(parms, device=local)
-    sk = ph.secret_key(ctx, seed=1000 + rank)
+    sk = ph.secret_key(ctx, seed=SK_SEED + rank)
     gk = sk.create_galois_keys(ctx)
-    enc = ph.ckks_encoder(ctx)
     scale = 2.0 ** 59
-    rng = np.random.default_rng(rank)
-    x = rng.normal(0, 0.1, D)
-    pt_x = enc.encode_double_vector(ctx, np.tile(x, (N // 2) // D), scale)
+    # input: a fresh symmetric encryption of a uniformly random plaintext (integer-exact, so the C
+    # oracle reproduces it: tests/golden/make_bench_digest.py) -- the key switches and products see
+    # uniformly random limbs either way
+    pt_x = ph.random_plaintexts(ctx, INPUT_SEED + rank, 1, 1, scale)[0]
     ct = sk.encrypt_symmetric(ctx, pt_x)
     level = ct.chain_index()
-    pts = ph.random_plaintexts(ctx, 2 + rank, D, level, scale)
+    pts = ph.random_plaintexts(ctx, DIAG_SEED + rank, D, level, scale)
     ctx.synchronize()
 
     gather_buf = None
@@ -257,21 +273,35 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    # correctness guard on the timed output: decrypts without error and has the expected level
+    # correctness guard on the timed output: the level, and on rank 0 the SHA-256 of its limbs against
+    # the digest the C oracle computed for this exact workload (tests/golden/manifest.json)
     assert y.chain_index() == level + 1
+    parity = limb_digest_check(args.config, y.to_numpy()) if rank == 0 else None
 
     if dist is not None:
         import torch
         tm = torch.tensor([median_ms], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         median_ms = float(tm.item())
+    seal = None
+    if world == 1 and args.config == "cfg2" and not args.no_seal:
+        # north_star's bit-exact claim is stated against SEAL's switch_key_inplace convention: the same
+        # matvec in that mode (P = 1, dnum = L0, every rotation decomposed on its own, no hoisting)
+        del pts, ct, y, gk, sk, pt_x
+        ctx.synchronize()
+        del ctx
+        try:
+            seal = seal_leg(args, ph, cfg)
+        except Exception as e:   # reported, never hidden
+            seal = {"error": f"{type(e).__name__}: {e}"[:400]}
     block = None
     if not args.no_block and args.config == "cfg2":
         # the metric's second half, measured: one client-aided RWKV-7 block (cfg3 shapes) on the same
         # ranks, after this configuration's memory is released
-        del pts, ct, y, gk, sk, pt_x
-        ctx.synchronize()
-        del ctx
+        if seal is None:
+            del pts, ct, y, gk, sk, pt_x
+            ctx.synchronize()
+            del ctx
         try:
             block = run_block(args, ph, dist, rank, world, local, args.block_steps, 1)
         except Exception as e:   # reported, never hidden: the matvec line stands on its own
@@ -352,7 +382,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (random uniform diagonals mod q_i, fresh encryption of N(0,0.1^2) input)",
+            "data": "synthetic (random uniform diagonals mod q_i, fresh encryption of a random uniform plaintext)",
             "config": {"workload": cfg["workload"], "N": N, "L0": L0, "P": P, "d": D, "G": G, "B": B,
                        "rotations_per_matvec": (G - 1) + (B - 1), "projections_per_rank": 1,
                        "parallelism": f"projection-parallel x{world}" + (" + RCCL gather" if world > 1 else "")},
@@ -363,11 +393,16 @@ def main():
             # reference's stage dependencies (r,k,v -> o -> FFN key -> FFN value) and is the latency figure
             "sec_per_8proj_independent": round(8.0 / value, 6),
             "rwkv_block": block,
+            # the same matvec in SEAL's key-switch convention (P = 1, non-hoisted): the convention of
+            # north_star's bit-exact claim; `value` above is the default exact-centred hoisted P = 3 mode
+            "seal_mode_value": seal.get("value") if seal else None,
+            "seal_mode": seal,
             "roofline": roof,
             "hadamard_roofline": had_roof,
             "ntt_valu_roofline": valu,
             "matvec_roofline": matvec_roof,
             "kernels": rows,
+            "parity": parity,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args)
@@ -375,6 +410,47 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def seal_leg(args, ph, cfg):
+    """cfg2's matvec with context.set_key_switch_mode('seal'): primes [59] x (L0 + 1), one special
+    prime, SEAL's switch_key_inplace per rotation (DESIGN.md §3 SEAL convention).  Same seeds as the
+    main leg; output limbs checked against the oracle's digest of this mode (bench_digests cfg2_seal)."""
+    N, L0, D = cfg["N"], cfg["L0"], cfg["D"]
+    G, B = bsgs_params(D)
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(1)
+    parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(steps, N))))
+    parms.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * (L0 + 1)))
+    ctx = ph.context(parms)
+    ctx.set_key_switch_mode("seal")
+    sk = ph.secret_key(ctx, seed=SK_SEED)
+    gk = sk.create_galois_keys(ctx)
+    scale = 2.0 ** 59
+    ct = sk.encrypt_symmetric(ctx, ph.random_plaintexts(ctx, INPUT_SEED, 1, 1, scale)[0])
+    pts = ph.random_plaintexts(ctx, DIAG_SEED, D, ct.chain_index(), scale)
+
+    def step():
+        baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+        return ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    step()
+    ctx.synchronize()
+    evs = []
+    for _ in range(args.seal_steps):
+        e0 = ph.Event(ctx)
+        y = step()
+        evs.append((e0, ph.Event(ctx)))
+    ctx.synchronize()
+    med = float(np.median([a.elapsed_ms(b) for a, b in evs]))
+    res = {"value": round(1000.0 / med, 3), "unit": "matvec/s", "median_ms_per_step": round(med, 3),
+           "steps": args.seal_steps, "P": 1, "dnum": L0, "hoisting": False,
+           "workload": f"BSGS matvec d={D} N={N} L0={L0} P=1, SEAL switch_key_inplace convention",
+           "parity": limb_digest_check("cfg2", y.to_numpy(), "_seal")}
+    del y, pts, ct, gk, sk
+    ctx.synchronize()
+    return res
 
 
 def run_block(args, ph, dist, rank, world, local, steps, warmup):

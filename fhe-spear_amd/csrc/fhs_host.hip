@@ -229,14 +229,6 @@ struct PendingRot {
 struct fhs_context {
     int device = 0;
     hipStream_t st = nullptr;
-    hipStream_t st_aux = nullptr;          // second stream of the pipelined BSGS (memory-bound kernels)
-    // CU-partitioned stream pair for the pipelined BSGS (FHESPEAR_PIPE_CUS = k: k of every 32 CUs
-    // for the memory-bound stream, the rest for ModUp), with the events that order them on `st`
-    hipStream_t st_pm = nullptr, st_pa = nullptr;
-    hipEvent_t ev_pin = nullptr, ev_pout = nullptr;
-    std::vector<hipEvent_t> bsgs_ev;       // cross-stream ordering events of launch_bsgs
-    int bsgs_chunks = 1;                   // FHESPEAR_BSGS_CHUNKS (overlap measured slower)
-    int bsgs_split_h = 0;                  // FHESPEAR_BSGS_SPLIT_H
     std::recursive_mutex mu;
     uint64_t N = 0;
     int logN = 0, L0 = 0, P = 0, K = 0, dnum = 0;
@@ -309,6 +301,7 @@ struct fhs_secret_key {
     uint64_t* s;   // K limbs, NTT
     PrfKey key;    // 256-bit PRF key all secret randomness is drawn from
     uint64_t ctr;  // symmetric-encryption counter
+    uint64_t pk_gen = 0;   // public keys generated so far (each gets its own mask stream)
 };
 struct fhs_public_key {
     fhs_context* ctx;
@@ -337,10 +330,15 @@ static void ctx_retain(fhs_context* c) { c->refs.fetch_add(1); }
 // first and returns every cached block.
 static std::mutex g_live_mu;
 static std::set<fhs_context*> g_live;
-static void release_cached_blocks(fhs_context* c);
+static void trim_cache(fhs_context* c);
 static void release_at_exit() {
+    // try_lock, as trim_other_caches: a thread still inside a context (holding c->mu, possibly about
+    // to take g_live_mu on its out-of-memory path) keeps that context's cache rather than deadlock exit
     std::lock_guard<std::mutex> lk(g_live_mu);
-    for (fhs_context* c : g_live) release_cached_blocks(c);
+    for (fhs_context* c : g_live) {
+        std::unique_lock<std::recursive_mutex> cl(c->mu, std::try_to_lock);
+        if (cl.owns_lock()) trim_cache(c);
+    }
 }
 static void ctx_release(fhs_context* c);
 
@@ -366,9 +364,6 @@ static void free_key(fhs_context* c, uint64_t* key) {
 
 static void ctx_sync(fhs_context* c) {
     hipStreamSynchronize(c->st);
-    if (c->st_aux) hipStreamSynchronize(c->st_aux);
-    if (c->st_pm) hipStreamSynchronize(c->st_pm);
-    if (c->st_pa) hipStreamSynchronize(c->st_pa);
 }
 // every cached block back to the device (the caller holds c->mu)
 static void trim_cache(fhs_context* c) {
@@ -391,10 +386,6 @@ static void trim_other_caches(fhs_context* self) {
         std::unique_lock<std::recursive_mutex> cl(c->mu, std::try_to_lock);
         if (cl.owns_lock()) trim_cache(c);
     }
-}
-static void release_cached_blocks(fhs_context* c) {
-    std::lock_guard<std::recursive_mutex> lk(c->mu);
-    trim_cache(c);
 }
 static void evict_cold(fhs_context* c, size_t keep) {
     std::vector<void*> victims;
@@ -806,24 +797,6 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     }
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->ring), fhs_context::kRingBytes, hipHostMallocDefault),
            "staging ring");
-    HIPCHK(hipStreamCreateWithFlags(&c->st_aux, hipStreamNonBlocking), "aux stream");
-    c->bsgs_ev.resize(2 + 2 * 16);
-    for (auto& ev : c->bsgs_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "bsgs events");
-    if (const char* ch = getenv("FHESPEAR_BSGS_CHUNKS")) c->bsgs_chunks = std::max(1, std::min(16, atoi(ch)));
-    if (const char* sh = getenv("FHESPEAR_BSGS_SPLIT_H")) c->bsgs_split_h = atoi(sh) != 0;
-    if (const char* pc = getenv("FHESPEAR_PIPE_CUS")) {
-        // mask word w bit b = CU 32 w + b: b < k in every word gives k CUs of each XCD (32 per XCD)
-        // whether the driver numbers CUs XCD-major or round-robin over the 8 XCDs
-        const int k = std::max(1, std::min(31, atoi(pc)));
-        hipDeviceProp_t prop;
-        HIPCHK(hipGetDeviceProperties(&prop, c->device), "device properties");
-        const int words = (prop.multiProcessorCount + 31) / 32;
-        std::vector<uint32_t> ma(words, (1u << k) - 1), mm(words, ~((1u << k) - 1));
-        HIPCHK(hipExtStreamCreateWithCUMask(&c->st_pa, words, ma.data()), "aux CU-mask stream");
-        HIPCHK(hipExtStreamCreateWithCUMask(&c->st_pm, words, mm.data()), "main CU-mask stream");
-        HIPCHK(hipEventCreateWithFlags(&c->ev_pin, hipEventDisableTiming), "pipe events");
-        HIPCHK(hipEventCreateWithFlags(&c->ev_pout, hipEventDisableTiming), "pipe events");
-    }
     c->stager = fhs::Stager{c.get(), stage_h2d};
     HIPCHK(hipMalloc(&c->items_dev, (sizeof(KsItem) + sizeof(void*)) * fhs_context::kMaxItems), "items buffer");
     c->tables.push_back(c->items_dev);
@@ -859,12 +832,6 @@ static void ctx_free(fhs_context* c) {
         flush(c);
         hipStreamSynchronize(c->st);
         ctx_sync(c);
-        for (auto ev : c->bsgs_ev) hipEventDestroy(ev);
-        if (c->st_aux) hipStreamDestroy(c->st_aux);
-        if (c->st_pm) hipStreamDestroy(c->st_pm);
-        if (c->st_pa) hipStreamDestroy(c->st_pa);
-        if (c->ev_pin) hipEventDestroy(c->ev_pin);
-        if (c->ev_pout) hipEventDestroy(c->ev_pout);
         for (void* p : c->tables) hipFree(p);
         for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
             if (c->scr[k]) hipFree(c->scr[k]);
@@ -1237,9 +1204,12 @@ extern "C" fhs_status fhs_gen_public_key(fhs_context* c, fhs_secret_key* sk, fhs
     ENTER(c);
     if (!sk || !out) return fail(FHS_ERR_INVALID, "null argument");
     auto* pk = new fhs_public_key{c, nullptr, PrfKey{}, 1ull << 20};
-    for (int w = 0; w < 4; ++w) {   // rng = 256 PRF bits of stream ST_PK_RNG
+    // rng = 256 PRF bits of stream (ST_PK_RNG, generation): two public keys of one secret key never
+    // share encryption masks (their key material is the same, so shared masks would reveal m1 - m2)
+    const uint64_t gen = sk->pk_gen++;
+    for (int w = 0; w < 4; ++w) {
         uint64_t w0, w1;
-        prf128(sk->key, stream_id(ST_PK_RNG, 0, 0), (uint32_t)w, w0, w1);
+        prf128(sk->key, stream_id(ST_PK_RNG, gen, 0), (uint32_t)w, w0, w1);
         pk->rng.k[2 * w] = (uint32_t)w0;
         pk->rng.k[2 * w + 1] = (uint32_t)(w0 >> 32);
     }
@@ -2196,22 +2166,9 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     uint64_t* sum = nullptr;
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_SUM, 16 * S, &sum), "bsgs sum");
     ht.mark("workspaces");
-    const bool cu_split = c->st_pm && c->bsgs_chunks > 1;
-    if (cu_split) {   // the CU-partitioned pair runs the whole BSGS, ordered after and before `st`
-        HIPCHK(hipEventRecord(c->ev_pin, c->st), "bsgs");
-        HIPCHK(hipStreamWaitEvent(c->st_pm, c->ev_pin, 0), "bsgs");
-        HIPCHK(hipStreamWaitEvent(c->st_pa, c->ev_pin, 0), "bsgs");
-    }
-    const fhs::BsgsStreams ss{cu_split ? c->st_pm : c->st, cu_split ? c->st_pa : c->st_aux, c->bsgs_ev.data(),
-                              (int)c->bsgs_ev.size(), c->bsgs_chunks, c->bsgs_split_h};
     HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), akeys.data(), giant_elts, inner, sum, ws, wsb,
-                            c->items_dev,
-                            c->stager, ss, tm),
+                            c->items_dev, c->stager, c->st, tm),
            "bsgs");
-    if (cu_split) {
-        HIPCHK(hipEventRecord(c->ev_pout, c->st_pm), "bsgs");
-        HIPCHK(hipStreamWaitEvent(c->st, c->ev_pout, 0), "bsgs");
-    }
     ht.mark("launch bsgs");
     fhs_ciphertext* r;
     if (!rescale) {

@@ -51,7 +51,7 @@ struct KsItem {
 
 // Optional per-kernel event timer (bench.py): rec(ctx, id, begin, stream) is called around launches.
 enum KernelId { KID_BSGS_INNER = 0, KID_MODUP = 1, KID_KS_IP = 2, KID_MODDOWN = 3, KID_KS_INTT = 4, KID_SPECIAL_INTT = 5,
-                KID_GIANT_SUM = 6, KID_GIANT_FINAL = 7, KID_RESCALE = 8, KID_KS_FUSED = 9, KID_COUNT = 10 };
+                KID_GIANT_SUM = 6, KID_GIANT_FINAL = 7, KID_RESCALE = 8, KID_COUNT = 10 };
 struct KTimer {
     void* ctx;
     void (*rec)(void* ctx, int id, int begin, hipStream_t st);
@@ -81,22 +81,14 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
                             const KTimer* tm);
 size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l);
 
-size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l);
-// Two-stream pipelined Hadamard + giant steps (fhs_kernels.hip launch_bsgs).  ev holds nev >= 4
-// events (2 + 2 * chunks used); the result is ordered on `main` when the call returns.
-struct BsgsStreams {
-    hipStream_t main, aux;
-    const hipEvent_t* ev;
-    int nev;
-    int chunks;
-    int split_hadamard;   // 1: Hadamard per chunk on the aux stream; 0: one Hadamard launch on main
-};
+// Hadamard + giant steps of the fused BSGS (fhs_kernels.hip launch_bsgs), enqueued on `st`.
 size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
 // giant_elts (host, B entries, may be null): Galois element of giant group g (g >= 1); null means
 // 5^(g G) mod 2N (the BSGS matvec of bg:464-485).  Group 0 is never rotated.
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
-                       u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm);
+                       u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
+                       const KTimer* tm);
 // CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
 // apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,

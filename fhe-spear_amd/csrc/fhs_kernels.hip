@@ -12,28 +12,8 @@
 // Every integer result is reduced to [0, q): limbs are bit-identical to oracle/ckks_oracle.c.
 #include "fhs_kernels.h"
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
-// Register caps for co-residency of the pipelined giant steps (A/B): FHS_MODUP_WPE = 5 caps ModUp at
-// 102 VGPRs, so its two workgroups per CU leave ~96 per SIMD for a key-inner-product wave;
-// FHS_KSIP_VGPR = min waves per SIMD for the key inner products (0: compiler's choice).
-#ifndef FHS_KSIP_VGPR
-#define FHS_KSIP_VGPR 0
-#endif
-#ifndef FHS_MODUP_WPE
-#define FHS_MODUP_WPE 4   // min waves per SIMD of k_modup_h (5: <= 102 VGPRs)
-#endif
-#if FHS_KSIP_VGPR
-#define FHS_KSIP_ATTR __attribute__((amdgpu_waves_per_eu(FHS_KSIP_VGPR)))
-#else
-#define FHS_KSIP_ATTR
-#endif
 #ifndef FHS_KSIP_UNROLL
 #define FHS_KSIP_UNROLL 2   // digits of the key inner product unrolled together (2: 64 VGPRs, 8 waves/SIMD)
-#endif
-#ifndef FHS_KSIP_PARTS
-#define FHS_KSIP_PARTS 1
-#endif
-#ifndef FHS_KSIP_VEC
-#define FHS_KSIP_VEC 1
 #endif
 #include "fhs_ntt.h"
 
@@ -43,62 +23,18 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #include <vector>
 #include <algorithm>
 
-// build-time tuning knobs (A/B variants are built with -D...; defaults are the shipped choice)
-#ifndef FHS_INNER_WAVES
+// Tuning constants (each chosen by an A/B on the cfg2 bench, limbs unchanged; the rejected
+// alternatives and their records are listed in DESIGN.md and profiles/r0*/ab_*).
 #define FHS_INNER_WAVES 16     // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
-#endif
-#ifndef FHS_INNER_VEC
-#define FHS_INNER_VEC 2       // consecutive coefficients per lane in k_bsgs_inner (2: 16-byte loads)
-#endif
-#ifndef FHS_MODUP_Y3
-#define FHS_MODUP_Y3 0        // k_modup_h: a 3-limb digit's conversion loads issued together per chunk
-#endif
-#ifndef FHS_INNER_PREFETCH
-#define FHS_INNER_PREFETCH 1  // k_bsgs_inner: first diagonal batch requested before the LDS staging barrier
-#endif
-#ifndef FHS_MODUP_HALF
-#define FHS_MODUP_HALF 1      // k_modup_h: half-limb LDS, two workgroups per CU
-#endif
-#ifndef FHS_INNER_LDS_MIN
-#define FHS_INNER_LDS_MIN 0
-#endif
-#ifndef FHS_MODDOWN_HALF
-#define FHS_MODDOWN_HALF 1
-#endif
-#ifndef FHS_INTT_HALF
-#define FHS_INTT_HALF 1       // k_ks_intt_h: half-limb LDS inverse NTT
-#endif
-#ifndef FHS_MODUPH_CH
-#define FHS_MODUPH_CH 2
-#endif
-#ifndef FHS_MODUPH_RL
-#define FHS_MODUPH_RL 3
-#endif
-#ifndef FHS_MODUP_MAP
-#define FHS_MODUP_MAP 1     // block->(limb, input) map of k_modup: 0 plain, 1 XCD t-inner, 2 XCD m-major
-                            // (A/B at cfg2, profiles/r01/ab_modup.log: 1 = 2.71 ms, 2 = 2.80, 0 = 2.90)
-#endif
-#ifndef FHS_MODDOWN_MAP
-#define FHS_MODDOWN_MAP 0
-#endif
-#ifndef FHS_MODUP_CH
-#define FHS_MODUP_CH 4
-#endif
-#ifndef FHS_MODUP_RL
-#define FHS_MODUP_RL 4         // radix (log2) of the register passes in k_modup's NTT
-#endif
-#ifndef FHS_FUSED_CH
-#define FHS_FUSED_CH 2         // k_ks_giant_fused: coefficients per conversion chunk
-#endif
-#ifndef FHS_FUSED_RL
-#define FHS_FUSED_RL 3         // k_ks_giant_fused: radix (log2) of the NTT register passes
-#endif
-#ifndef FHS_FUSED_GROUP
-#define FHS_FUSED_GROUP 4      // k_ks_giant_fused: key products scheduled in groups of this many coefficients
-#endif
-#ifndef FHS_NTT_RL
+#define FHS_INNER_VEC 2        // consecutive coefficients per lane in k_bsgs_inner (16-byte loads)
+#define FHS_MODUP_HALF 1       // k_modup_h: half-limb LDS, two workgroups per CU
+#define FHS_MODDOWN_HALF 1     // k_moddown_h: half-limb LDS
+#define FHS_INTT_HALF 1        // k_ks_intt_h: half-limb LDS inverse NTT
+#define FHS_MODUPH_CH 2        // k_modup_h: coefficient pairs per conversion chunk
+#define FHS_MODUPH_RL 3        // k_modup_h: radix (log2) of the NTT register passes
+#define FHS_MODUP_CH 4         // k_modup (full-limb form): coefficients per conversion chunk
+#define FHS_MODUP_RL 4         // k_modup (full-limb form): radix (log2) of the NTT register passes
 #define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
-#endif
 
 namespace fhs {
 
@@ -657,13 +593,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     const int tid = threadIdx.x;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     int t, mi;
-#if FHS_MODUP_MAP == 1
     if (!xcd_tinner(E, dn * U, t, mi)) return;
-#elif FHS_MODUP_MAP == 2
-    if (!xcd_mmajor(E, dn * U, t, mi)) return;
-#else
-    if (!plain_tm(E, dn * U, t, mi)) return;
-#endif
     const int j = mi % dn, u = mi / dn;
     const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
     u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
@@ -703,22 +633,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 #pragma unroll
         for (int k = 0; k < CH; ++k) {
             const int e = tid + (half * CH + k) * TH;
-#ifdef FHS_EXP_NOCONV
-            lds[lds_pad(e)] = acc[k].lo ^ vb[e];
-#else
             mac128(acc[k], (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
             lds[lds_pad(e)] = submod(reduce128(acc[k].lo, acc[k].hi, R), nsQm, m);
-#endif
         }
     }
     __syncthreads();
-#ifndef FHS_EXP_NONTT
-#ifdef FHS_EXP_TW0
-    ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd, m, R.lazy);   // experiment: one shared table
-#else
     ntt_fwd_lds<LOGN, FHS_MODUP_RL>(lds, tid, T.tw_fwd + (size_t)pt * N * 2, m, R.lazy);
-#endif
-#endif
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int e = tid + c * TH;
@@ -733,25 +653,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 // the upper half in registers while the lower half is transformed in LDS, then transforms it.
 // Same values as k_modup (same butterflies, same lazy bounds: < q + 2 q log N).
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(DevTables T, const u64* const* uniq,
+__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
                                                                  const u64* acoef, const unsigned char* vcnt, u64* ext,
                                                                  int l, int U) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;   // 16 coefficient pairs per thread
-    #if FHS_MODUP_WPE > 4   // dynamic LDS: the compiler then honours the waves-per-SIMD bound (register cap)
-    extern __shared__ __attribute__((aligned(16))) u64 lds[];
-#else
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
-#endif
     const int tid = threadIdx.x;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     int t, mi;
-#if FHS_MODUP_MAP == 1
     if (!xcd_tinner(E, dn * U, t, mi)) return;
-#elif FHS_MODUP_MAP == 2
-    if (!xcd_mmajor(E, dn * U, t, mi)) return;
-#else
-    if (!plain_tm(E, dn * U, t, mi)) return;
-#endif
     const int j = mi % dn, u = mi / dn;
     const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
     u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
@@ -780,24 +690,6 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
         uint32_t vv[2 * CH];
 #pragma unroll
         for (int k = 0; k < 2 * CH; ++k) vv[k] = vb[tid + (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0)];
-#if FHS_MODUP_Y3
-        if (ns == 3) {   // the usual digit of P = 3 limbs: all of the chunk's loads issued together
-            u64 y[3][2 * CH];
-#pragma unroll
-            for (int w = 0; w < 3; ++w)
-#pragma unroll
-                for (int k = 0; k < CH; ++k) {
-                    y[w][k] = yb[(size_t)w * N + tid + (ch * CH + k) * TH];
-                    y[w][CH + k] = yb[(size_t)w * N + tid + (ch * CH + k) * TH + NH];
-                }
-#pragma unroll
-            for (int w = 0; w < 3; ++w) {
-                const Split30 hw = split30(hat[(size_t)w * K]);
-#pragma unroll
-                for (int k = 0; k < 2 * CH; ++k) acc3_mac(a3[k], split30(y[w][k]), hw);
-            }
-        } else
-#endif
 #pragma unroll 1
         for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
             const Split30 hw = split30(hat[(size_t)w * K]);
@@ -854,33 +746,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, FHS_MODUP_WPE) k_modup_h(Dev
     }
 }
 
-// Extra (unused) LDS per k_modup_h workgroup, FHESPEAR_MODUP_PAD bytes (A/B knob, default 0): a pad
-// that caps ModUp at one workgroup per CU leaves LDS and registers for the memory-bound kernels of the
-// other stream (launch_bsgs chunks).
-static int modup_pad() {
-    static const int v = [] {
-        const char* e = getenv("FHESPEAR_MODUP_PAD");
-        return e ? std::max(0, std::min(65536, atoi(e))) : 0;
-    }();
-    return v;
-}
 template <int LOGN>
 static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* acoef, const unsigned char* vcnt,
                          u64* ext, int l, int U, hipStream_t st) {
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
-    const int mgrid = FHS_MODUP_MAP == 1 ? xcd_grid(E, dn * U) : FHS_MODUP_MAP == 2 ? xcd_grid_m(E, dn * U) : E * dn * U;
-    if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
-        int pad = modup_pad();
-        if (FHS_MODUP_WPE > 4) pad += (int)(((1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16) * 8);
-        static bool attr = false;
-        if (pad && !attr) {
-            hipFuncSetAttribute(reinterpret_cast<const void*>(&k_modup_h<LOGN>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, pad);
-            attr = true;
-        }
-        hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), pad, st, T, uniq, acoef, vcnt, ext, l,
-                           U);
-    }
+    const int mgrid = xcd_grid(E, dn * U);
+    if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>())
+        hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
 }
@@ -922,7 +794,7 @@ __device__ __forceinline__ void ks_digits(const DevTables& T, const u64* ex, con
     acc3_fold(c0, a0);
     acc3_fold(c1, a1);
 }
-__global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip(DevTables T, const KsItem* items, const u64* const* uniq, const u64* ext,
+__global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items, const u64* const* uniq, const u64* ext,
                                                 u64* acc, int l, int R, int t0) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
@@ -954,15 +826,12 @@ __global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip(DevTables T, const 
 // scaled by P^-1 and with the rotated c0's added (comp 0) -- the t < l part of
 // sum_r ModDown(acc_r) + sigma_r(c0_r) (k_giant_sum adds the special-limb conversion).  Writes
 // bpart[c][t][n] into the r = 0 slot of acc (acc[0][c][t], t < l), which nothing else uses.
-__global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip_sum(DevTables T, const KsItem* items, const u64* const* uniq,
-                                                    const u64* ext, u64* acc, int l, int R, int nparts) {
+__global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* items, const u64* const* uniq,
+                                                    const u64* ext, u64* acc, int l, int R) {
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
-    int t, mp;
-    if (!xcd_touter(l, NB * nparts, t, mp)) return;
-    // rotations [r0, r1) of part `part`; its partial sum goes to acc slot `part` (k_giant_sum adds them)
-    const int m = mp % NB, part = mp / NB;
-    const int r0 = (int)((long long)part * R / nparts), r1 = (int)((long long)(part + 1) * R / nparts);
+    int t, m;
+    if (!xcd_touter(l, NB, t, m)) return;
     const int n = (m << 8) + threadIdx.x;
     const size_t per_r = (size_t)E * N;
     const RedU RD = redu(PK(T, t));
@@ -970,7 +839,7 @@ __global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip_sum(DevTables T, co
     const u64 cx = seeded_ctr_mix(t, n);
     const unsigned qb = 64 - __clzll(q);
     u64 s0 = 0, s1 = 0, sadd = 0;
-    for (int r = r0; r < r1; ++r) {
+    for (int r = 0; r < R; ++r) {
         const KsItem it = items[r];
         const int sn = galois_src(n, it.elt, T.logN);
         const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
@@ -987,269 +856,8 @@ __global__ void __launch_bounds__(256) FHS_KSIP_ATTR k_ks_ip_sum(DevTables T, co
         sadd = addmod(sadd, it.add0[(size_t)t * N + sn], q);
     }
     const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
-    acc[(((size_t)part * 2 + 0) * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
-    acc[(((size_t)part * 2 + 1) * E + t) * N + n] = shoup(s1, pinv, pinv_s, q);
-}
-
-// k_ks_ip_sum with two coefficients per thread (FHS_KSIP_VEC == 2): 16-byte key loads, and each
-// group of 4 digits issues all its loads before the multiply-accumulates.
-template <bool EXPLICIT_A>
-__device__ __forceinline__ void ks_digits2(const u64* const ex[2], const u64* const own[2], const u64* key,
-                                           const u64* akey, const u64* seeds, const u64 cx[2], u64 q, unsigned qb,
-                                           int t, int l, int P_, int dn, size_t per_r, size_t KN, u128 c0[2],
-                                           u128 c1[2]) {
-    Acc3 a0[2] = {{0, 0, 0}, {0, 0, 0}}, a1[2] = {{0, 0, 0}, {0, 0, 0}};
-    int j = 0;
-    for (; j < dn; j += 4) {
-        const int nj = min(4, dn - j);
-        u64 v[4][2];
-        u64x2_t b[4], a[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (u < nj) {
-                const int jj = j + u;
-                const bool own_limb = t >= jj * P_ && t < min(jj * P_ + P_, l);
-#pragma unroll
-                for (int h = 0; h < 2; ++h) v[u][h] = own_limb ? own[h][0] : ex[h][(size_t)jj * per_r];
-                b[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(key + (size_t)jj * KN));
-                if constexpr (EXPLICIT_A)
-                    a[u] = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(akey + (size_t)jj * KN));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (u < nj) {
-                const int jj = j + u;
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const Split30 sv = split30(v[u][h]);
-                    acc3_mac(a0[h], sv, split30(h ? b[u].y : b[u].x));
-                    u64 av;
-                    if constexpr (EXPLICIT_A) av = h ? a[u].y : a[u].x;
-                    else av = seeded_uniform_x(seeds[jj] + cx[h], q, qb);
-                    acc3_mac(a1[h], sv, split30(av));
-                }
-            }
-        }
-        if ((j & 4) == 4 || j + 4 >= dn) {   // folded at least every 8 products
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                acc3_fold(c0[h], a0[h]);
-                acc3_fold(c1[h], a1[h]);
-            }
-        }
-    }
-}
-__global__ void __launch_bounds__(256) k_ks_ip_sum2(DevTables T, const KsItem* items, const u64* const* uniq,
-                                                     const u64* ext, u64* acc, int l, int R) {
-    const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
-    const int NB = N >> 9;
-    int t, m;
-    if (!xcd_touter(l, NB, t, m)) return;
-    const int n0 = ((m << 8) + threadIdx.x) * 2;
-    const size_t per_r = (size_t)E * N;
-    const RedU RD = redu(PK(T, t));
-    const u64 q = RD.q;
-    const u64 cx[2] = {seeded_ctr_mix(t, n0), seeded_ctr_mix(t, n0 + 1)};
-    const unsigned qb = 64 - __clzll(q);
-    u64 s0[2] = {0, 0}, s1[2] = {0, 0}, sadd[2] = {0, 0};
-    for (int r = 0; r < R; ++r) {
-        const KsItem it = items[r];
-        const int sn[2] = {galois_src(n0, it.elt, T.logN), galois_src(n0 + 1, it.elt, T.logN)};
-        const u64* ex[2];
-        const u64* own[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            ex[h] = ext + ((size_t)it.src * dn * E + t) * N + sn[h];
-            own[h] = uniq[it.src] + (size_t)t * N + sn[h];
-        }
-        const u64* key = it.key + (size_t)t * N + n0;
-        const u64* seeds = it.key + (size_t)T.dnum * K * N;
-        u128 c0[2] = {{0, 0}, {0, 0}}, c1[2] = {{0, 0}, {0, 0}};
-        if (it.akey)
-            ks_digits2<true>(ex, own, key, it.akey + (size_t)t * N + n0, seeds, cx, q, qb, t, l, P_, dn, per_r,
-                             (size_t)K * N, c0, c1);
-        else
-            ks_digits2<false>(ex, own, key, nullptr, seeds, cx, q, qb, t, l, P_, dn, per_r, (size_t)K * N, c0, c1);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            s0[h] = addmod(s0[h], reduce128(c0[h].lo, c0[h].hi, RD), q);
-            s1[h] = addmod(s1[h], reduce128(c1[h].lo, c1[h].hi, RD), q);
-            sadd[h] = addmod(sadd[h], it.add0[(size_t)t * N + sn[h]], q);
-        }
-    }
-    const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        acc[((size_t)0 * E + t) * N + n0 + h] = addmod(shoup(s0[h], pinv, pinv_s, q), sadd[h], q);
-        acc[((size_t)1 * E + t) * N + n0 + h] = shoup(s1[h], pinv, pinv_s, q);
-    }
-}
-
-// Giant steps, ModUp fused with the key inner product: one workgroup per (target limb t, rotation r)
-// runs the dnum digits in turn -- centred conversion of digit j's limbs into limb t, forward NTT in
-// LDS -- and multiplies each result straight into the two key components, so the extended limbs
-// never go to HBM and the key stream overlaps the NTT work.  acc[r][c][t][n] = sum_j
-// ext_j[t][sigma_r(n)] key_j[c][t][n] mod q_t: the same residues k_modup + k_ks_ip produce.
-// The products are Shoup multiplications with the NTT value as the fixed operand (its companion
-// floor(e 2^64 / q) - {0,1} from the Barrett constant: e r1 + hi(e r0)), each < 2q; the sums stay
-// below 2^64 without reduction when 2 dnum q < 2^64 (`lazy`), else they are kept below 2q.
-template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_giant_fused(DevTables T, const KsItem* items,
-                                                                     const u64* const* uniq, const u64* acoef,
-                                                                     const unsigned char* vcnt, u64* acc, int l, int R) {
-    constexpr int N = 1 << LOGN, TH = N / 16;
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << LOGN) + (1 << LOGN) / 16];
-    const int tid = threadIdx.x;
-    const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
-    int t, r;
-    if (!xcd_tinner(E, R, t, r)) return;
-    const int pt = t < l ? t : T.L0 + (t - l);
-    const PrimeK& PM = PK(T, pt);
-    const RedU RU = redu(PM);
-    const u64 q = RU.q, q2 = 2 * q, r0 = rfl64(PM.r0), r1 = rfl64(PM.r1);
-    const bool lazy = q < (~0ull) / (2 * (u64)dn);
-    const KsItem it = items[r];
-    const u64* keyb = it.key + (size_t)pt * N;
-    const u64* seeds = it.key + (size_t)T.dnum * K * N;
-    const u64* own = uniq[it.src] + (size_t)t * N;
-    const unsigned qb = 64 - __clzll(q);
-    const u64* tw = T.tw_fwd + (size_t)pt * N * 2;
-    // automorphism: output slot n reads slot galois_src(n); for n = tid + c TH the exponent
-    // 2 rev(n) + 1 splits into a per-thread part and a per-c constant, so each source slot costs a
-    // multiply-add and a bit reversal
-    const u64 m2 = (u64)2 << LOGN;
-    const unsigned rt = __brev((unsigned)tid) >> (32 - LOGN);   // rev(tid) (tid < TH: top 4 bits of rev clear)
-    const u64 ebase = ((2 * (u64)rt + 1) * it.elt) & (m2 - 1);
-    // per-coefficient values are recomputed from `tl`, a copy of tid laundered once per digit, so
-    // the compiler cannot hoist 16 addresses, sources and counters out of the digit loop (that
-    // costs ~80 registers and spills)
-    int tl = tid;
-    u64 eb = ebase;
-    auto src_of = [&](int c) {
-        const u64 e2 = (eb + 2 * (u64)(__brev((unsigned)c) >> 28) * it.elt) & (m2 - 1);
-        return (int)(__brev((unsigned)((e2 - 1) >> 1)) >> (32 - LOGN));
-    };
-    u64 A0[16], A1[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) A0[c] = A1[c] = 0;
-    auto mac = [&](int c, u64 e, int j) {   // e < q
-        const u64 ep = mullo64x(e, r1) + mulhi64x(e, r0);
-        const int n = tl + c * TH;
-        const u64 b = __builtin_nontemporal_load(keyb + (size_t)j * K * N + n);
-        const u64 a = it.akey ? __builtin_nontemporal_load(it.akey + (size_t)j * K * N + (size_t)pt * N + n)
-                              : seeded_uniform_x(seeds[j] + seeded_ctr_mix(pt, n), q, qb);
-        const u64 pb = mullo64x(b, e) - mullo64x(mulhi64x(b, ep), q);
-        const u64 pa = mullo64x(a, e) - mullo64x(mulhi64x(a, ep), q);
-        if (lazy) {
-            A0[c] += pb;
-            A1[c] += pa;
-        } else {
-            A0[c] = csub(A0[c] + pb, q2);
-            A1[c] = csub(A1[c] + pa, q2);
-        }
-    };
-#pragma unroll 1
-    for (int j = 0; j < dn; ++j) {
-        tl = tid;
-        eb = ebase;
-        asm volatile("" : "+v"(tl), "+v"(eb));
-        const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
-        if (t >= s0 && t < s1) {   // own limb of digit j: the input limb itself (workgroup-uniform branch)
-#pragma unroll
-            for (int c = 0; c < 16; ++c) {
-                mac(c, own[src_of(c)], j);
-                if ((c & (FHS_FUSED_GROUP - 1)) == FHS_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
-            }
-            continue;
-        }
-        const u64* yb = acoef + ((size_t)it.src * l + s0) * N;
-        const u64* hat = T.modup_hat + (((size_t)l * T.dnum + j) * P_) * K + pt;
-        const u64* qv = T.modup_Q + (((size_t)l * T.dnum + j) * K + pt) * 2;
-        const u64 Qm = qv[0], nsQm = qv[1], negQ = Qm ? q - Qm : 0;
-        const unsigned char* vb = vcnt + ((size_t)it.src * dn + j) * N;
-        constexpr int CH = FHS_FUSED_CH;
-#pragma unroll 1
-        for (int ch = 0; ch < 16 / CH; ++ch) {
-            Acc3 a3[CH];
-#pragma unroll
-            for (int k = 0; k < CH; ++k) a3[k] = Acc3{0, 0, 0};
-#pragma unroll 1
-            for (int w = 0; w < ns; ++w) {   // ns <= 8 products per Acc3
-                const Split30 hw = split30(hat[(size_t)w * K]);
-                const u64* yw = yb + (size_t)w * N + tid + ch * CH * TH;
-                u64 y[CH];
-#pragma unroll
-                for (int k = 0; k < CH; ++k) y[k] = yw[k * TH];
-#pragma unroll
-                for (int k = 0; k < CH; ++k) acc3_mac(a3[k], split30(y[k]), hw);
-            }
-#pragma unroll
-            for (int k = 0; k < CH; ++k) {
-                const int e = tid + (ch * CH + k) * TH;
-                u64 x;
-                if (RU.cpm) {   // - v Q_S folded into L as v (q - Q_S mod q); result in [0, 2q)
-                    const uint32_t v = vb[e];
-                    const u64 vq = mul32w(v, (uint32_t)negQ) + ((u64)(v * (uint32_t)(negQ >> 32)) << 32);
-                    x = acc3_reduce_pm(a3[k].L + vq, a3[k].M, a3[k].H, RU.b, RU.d);
-                } else {
-                    u128 s = {0, 0};
-                    acc3_fold(s, a3[k]);
-                    mac128(s, (u64)(ns - vb[e]), Qm);   // + (ns - v) Q_S, then - ns Q_S below
-                    x = submod(reduce128(s.lo, s.hi, RU), nsQm, q);
-                }
-                lds[lds_pad(e)] = x;
-            }
-        }
-        __syncthreads();
-        ntt_fwd_lds<LOGN, FHS_FUSED_RL>(lds, tid, tw, q, RU.lazy);
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            mac(c, fwd_canon(lds[lds_pad(src_of(c))], RU), j);
-            if ((c & (FHS_FUSED_GROUP - 1)) == FHS_FUSED_GROUP - 1) __builtin_amdgcn_sched_barrier(0);
-        }
-        __syncthreads();   // every read of this digit's transform precedes the next digit's writes
-    }
-    u64* o0 = acc + (((size_t)r * 2 + 0) * E + t) * N;
-    u64* o1 = acc + (((size_t)r * 2 + 1) * E + t) * N;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const int n = tid + c * TH;
-        u64 a0 = A0[c], a1 = A1[c];
-        if (lazy) {   // < 2 dn q
-            a0 = reduce128(a0, 0, RU);
-            a1 = reduce128(a1, 0, RU);
-        } else {
-            a0 = csub(a0, q);
-            a1 = csub(a1, q);
-        }
-        o0[n] = a0;
-        o1[n] = a1;
-    }
-}
-
-// Giant steps after k_ks_giant_fused, limbs t < l: bpart[c][t][n] = P^-1 sum_r acc[r][c][t][n]
-// + [c == 0] sum_r sigma_r(c0_r)[t][n], written in place into the r = 0 slot (k_ks_ip_sum's output).
-__global__ void __launch_bounds__(256) k_giant_ip_reduce(DevTables T, const KsItem* items, u64* acc, int l, int R) {
-    const int N = T.N, P_ = T.P, E = l + P_;
-    const size_t total = (size_t)2 * l * N;
-    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-         idx += (size_t)gridDim.x * blockDim.x) {
-        const int comp = (int)(idx / ((size_t)l * N));
-        const int t = (int)((idx / N) % l), n = (int)(idx % N);
-        const RedU RD = redu(PK(T, t));
-        const u64 q = RD.q;
-        u64 s = 0, sadd = 0;
-        for (int r = 0; r < R; ++r) {
-            s = addmod(s, acc[(((size_t)r * 2 + comp) * E + t) * N + n], q);
-            if (comp == 0) {
-                const KsItem it = items[r];
-                sadd = addmod(sadd, it.add0[(size_t)t * N + galois_src(n, it.elt, T.logN)], q);
-            }
-        }
-        const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
-        acc[((size_t)comp * E + t) * N + n] = addmod(shoup(s, pinv, pinv_s, q), sadd, q);
-    }
+    acc[((size_t)0 * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
+    acc[((size_t)1 * E + t) * N + n] = shoup(s1, pinv, pinv_s, q);
 }
 
 // (c) special limbs of the accumulator -> coefficient form, scaled by inv(P / p_k)
@@ -1279,11 +887,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
     const int tid = threadIdx.x;
     const int P_ = T.P, E = l + P_;
     int i, m;
-#if FHS_MODDOWN_MAP == 1
-    if (!xcd_tinner(l, 2 * R, i, m)) return;
-#else
     if (!plain_tm(l, 2 * R, i, m)) return;
-#endif
     const int comp = m & 1, r = m >> 1;
     const PrimeK& P = PK(T, i);
     const u64 q = P.q;
@@ -1542,7 +1146,7 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
         if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>())
             hipLaunchKernelGGL((k_moddown_h<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc, ycoef, l, R);
         else
-        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(FHS_MODDOWN_MAP == 1 ? xcd_grid(l, 2 * R) : l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
+        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
         FHS_TMARK(tm, KID_MODDOWN, 0, st);
     });
     return hipGetLastError();
@@ -1573,7 +1177,6 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t S = (size_t)l * N;
     const size_t off = (size_t)i * N + n0 + lane * VEC;
-#if FHS_INNER_PREFETCH
     // the first 8 diagonals of this wave's first group are requested before the baby-step slice is
     // staged, so the staging and its barrier overlap the diagonal stream instead of stalling it
     u64 pf[8][VEC];
@@ -1584,7 +1187,6 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
         for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + off, pf[u]);
         have_pf = true;
     }
-#endif
     for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
         const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
         sb[idx] = pack30(baby[b][comp * S + (size_t)i * N + n0 + c]);
@@ -1606,7 +1208,6 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
         // 8 diagonal loads in flight per wave-iteration, folded into the 128-bit sums every 8
         for (; b + 8 <= bmax; b += 8) {
             u64 p[8][VEC];
-#if FHS_INNER_PREFETCH
             if (have_pf) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u)
@@ -1614,7 +1215,6 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
                     for (int v = 0; v < VEC; ++v) p[u][v] = pf[u][v];
                 have_pf = false;
             } else
-#endif
             {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + off, p[u]);
@@ -1669,7 +1269,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
 #define FHS_GSUM_ICH 4
 #endif
 __global__ void __launch_bounds__(256) k_giant_sum(DevTables T, const u64* bpart, const u64* ycoef, const u64* inner0,
-                                                   u64* base, u64* convsum, int l, int R, int first, int nparts) {
+                                                   u64* base, u64* convsum, int l, int R) {
     const int N = T.N, P_ = T.P, E = l + P_;
     const int n = blockIdx.x * blockDim.x + threadIdx.x, comp = blockIdx.y;
     if (n >= N) return;
@@ -1697,7 +1297,6 @@ __global__ void __launch_bounds__(256) k_giant_sum(DevTables T, const u64* bpart
 #pragma unroll
         for (int k = 0; k < PMAX; ++k)
             if (k < P_) mac128(cs, reduce128(ylo[k], yhi[k], P), T.md_hat[(size_t)k * T.L0 + i]);
-        // chunks of rotations accumulate mod q: both sums are linear in the rotations
         if (T.ks_seal) {   // SEAL rounding: each of the R conversions carries - floor(p/2) mod q_i
             u128 h = {0, 0};
             mac128(h, (u64)R, T.md_pinv[3 * T.L0 + i]);
@@ -1708,14 +1307,7 @@ __global__ void __launch_bounds__(256) k_giant_sum(DevTables T, const u64* bpart
         }
         u64 cv = reduce128(cs.lo, cs.hi, P);
         const size_t idx = (size_t)comp * S + (size_t)i * N + n;
-        u64 bv = bpart[((size_t)comp * E + i) * N + n];
-        for (int p = 1; p < nparts; ++p) bv = addmod(bv, bpart[(((size_t)p * 2 + comp) * E + i) * N + n], q);
-        if (first) {
-            bv = addmod(bv, inner0[idx], q);
-        } else {
-            cv = addmod(cv, convsum[idx], q);
-            bv = addmod(bv, base[idx], q);
-        }
+        const u64 bv = addmod(bpart[((size_t)comp * E + i) * N + n], inner0[idx], q);
         convsum[idx] = cv;
         base[idx] = bv;
     }
@@ -1735,7 +1327,7 @@ __global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_giant_final(DevTab
                                [&](int e, u64 v) { out[off + e] = submod(base[off + e], shoup(v, pinv, pinv_s, q), q); });
 }
 
-// ---- key-switch stages on explicit buffers (the pipelined BSGS launcher runs them per chunk)
+// ---- key-switch stages of the BSGS giant steps
 struct KsBufs {
     u64 *acoef, *ext, *acc, *ycoef;
     unsigned char* vcnt;
@@ -1750,36 +1342,19 @@ static KsBufs ks_carve(const DevTables& T, u64* ws, int R, int U, int l) {
     b.vcnt = reinterpret_cast<unsigned char*>(b.ycoef + (size_t)R * 2 * T.P * N);
     return b;
 }
-// view of items [r0, ..) with inputs [u0, ..): items' src must then be relative to u0
-static KsBufs ks_at(const DevTables& T, const KsBufs& b, int r0, int u0, int l) {
-    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
-    return KsBufs{b.acoef + (size_t)u0 * l * N, b.ext + (size_t)u0 * dn * E * N, b.acc + (size_t)r0 * 2 * E * N,
-                  b.ycoef + (size_t)r0 * 2 * T.P * N, b.vcnt + (size_t)u0 * dn * N};
-}
 template <int LOGN>
 static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, int l, const KsBufs& b, hipStream_t st,
                            const KTimer* tm) {
-    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
-    const dim3 blk((1 << LOGN) / 16);
     FHS_TMARK(tm, KID_KS_INTT, 1, st);
     if (ks_intt_half<LOGN>(l * U))
         hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uniq, b.acoef, l, U);
     else
-        hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), blk, 0, st, T, uniq, b.acoef, l, U);
+        hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), dim3((1 << LOGN) / 16), 0, st, T, uniq, b.acoef, l, U);
     launch_centered(T, b.acoef, b.vcnt, l, U, st);
     FHS_TMARK(tm, KID_KS_INTT, 0, st);
     FHS_TMARK(tm, KID_MODUP, 1, st);
     launch_modup<LOGN>(T, uniq, b.acoef, b.vcnt, b.ext, l, U, st);
     FHS_TMARK(tm, KID_MODUP, 0, st);
-}
-// rotations per k_ks_ip_sum thread: the giant sum is split into parts over more workgroups (more loads
-// in flight), each writing its partial into an unused acc slot; k_giant_sum adds the parts
-static int ksip_parts(int R) {
-    static const int v = [] {
-        const char* e = getenv("FHESPEAR_KSIP_PARTS");
-        return e ? std::max(1, std::min(16, atoi(e))) : FHS_KSIP_PARTS;
-    }();
-    return std::max(1, std::min(v, R));
 }
 template <int LOGN>
 static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* const* uniq, int R, int l, const KsBufs& b,
@@ -1787,40 +1362,18 @@ static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* cons
     const int NB = T.N >> 8;
     FHS_TMARK(tm, KID_KS_IP, 1, st);
     hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(T.P, R * NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R, l);
-    if (FHS_KSIP_VEC == 2 && T.N >= 512)
-        hipLaunchKernelGGL(k_ks_ip_sum2, dim3(xcd_grid(l, NB / 2)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
-    else
-        hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB * ksip_parts(R))), dim3(256), 0, st, T, it, uniq, b.ext, b.acc,
-                           l, R, ksip_parts(R));
+    hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
     FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), st, T, b.acc, b.ycoef, l, R);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
 }
 
-// Pipelined BSGS (Hadamard + giant steps) on two streams.  The giant rotations are cut into
-// `chunks` groups; the aux stream runs the memory-bound kernels (Hadamard chunk c, then key inner
-// products + giant sums), the main stream the VALU-bound ones (INTT, centred ModUp + NTT), so one
-// chunk's ModUp overlaps the next chunk's Hadamard and the previous chunk's inner product.  Chunks
-// only reorder independent work: the limbs are identical to the serial schedule.
-size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) { return bsgs_giant_workspace_bytes(T, R, l); }
-
-// Hadamard shape (coefficients per lane, waves per LDS slice): FHESPEAR_INNER="vec,waves" (A/B knob;
-// default FHS_INNER_VEC, FHS_INNER_WAVES).  Fewer waves leave registers for a co-scheduled ModUp.
-struct InnerShape {
-    int vec, waves;
-};
-static InnerShape inner_shape() {
-    static const InnerShape s = [] {
-        InnerShape r{FHS_INNER_VEC, FHS_INNER_WAVES};
-        if (const char* e = getenv("FHESPEAR_INNER")) {
-            int v = 0, w = 0;
-            if (sscanf(e, "%d,%d", &v, &w) == 2 && (v == 1 || v == 2) && (w == 4 || w == 8 || w == 16)) r = {v, w};
-        }
-        return r;
-    }();
-    return s;
+// core key-switch workspace of the R giant rotations, then base | convsum (2 ciphertexts)
+size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) {
+    return keyswitch_workspace_bytes(T, R, R, l) + 8 * (size_t)T.N * 4 * l;
 }
+
 template <int VEC, int WAVES>
 static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, const u64* const* pts, int G, int g0,
                                  int g1, int D, int l, u64* inner, hipStream_t st) {
@@ -1828,85 +1381,42 @@ static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, con
     static bool attr = false;
     if (!attr) {   // dynamic LDS above 64 KiB must be opted into
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)std::max<size_t>(64 * 2 * W * 8, FHS_INNER_LDS_MIN));
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * 2 * W * 8));
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const size_t sh = std::max<size_t>((size_t)G * 2 * W * 8, FHS_INNER_LDS_MIN);
-    hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES>), dim3(T.N / W, l), dim3(64 * WAVES), sh, st, T, baby, pts, G, g0,
-                       g1, D, l, inner);
+    hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES>), dim3(T.N / W, l), dim3(64 * WAVES), (size_t)G * 2 * W * 8, st, T,
+                       baby, pts, G, g0, g1, D, l, inner);
     return hipGetLastError();
 }
-static hipError_t launch_inner(const DevTables& T, const u64* const* baby, const u64* const* pts, int G, int g0, int g1,
-                               int D, int l, u64* inner, hipStream_t st) {
-    const InnerShape s = inner_shape();
-#define FHS_INNER_CASE(V, Wv) \
-    if (s.vec == V && s.waves == Wv) return launch_inner_t<V, Wv>(T, baby, pts, G, g0, g1, D, l, inner, st);
-    FHS_INNER_CASE(2, 16) FHS_INNER_CASE(2, 8) FHS_INNER_CASE(2, 4) FHS_INNER_CASE(1, 16) FHS_INNER_CASE(1, 8)
-    FHS_INNER_CASE(1, 4)
-#undef FHS_INNER_CASE
-    return hipErrorInvalidValue;
-}
 
-// Pipelined BSGS (Hadamard + giant steps) on two streams.  The giant rotations are cut into
-// `chunks` groups.  Main stream: INTT + centred ModUp + NTT of chunk c (VALU-bound) as soon as its
-// inner products exist.  Aux stream: Hadamard of chunk c + 1, then the key inner products and the
-// running giant sum of chunk c (memory-bound), so a chunk's ModUp can share the CUs with the next
-// chunk's Hadamard and the previous chunk's key reads.  Chunks only reorder independent work: the
-// limbs are identical to the serial schedule.
-// Giant steps through k_ks_giant_fused (N = 256 .. 16384) when FHESPEAR_GIANT_FUSED=1 (A/B knob).
-// Off by default: limb-identical, but at cfg2 the fused kernel takes 5.05-5.14 ms against 4.0 ms
-// for k_modup_h + k_ks_ip/k_ks_ip_sum of the giant steps (profiles/r02/ab_giant_fused.jsonl): one
-// 1024-thread workgroup per CU with the 32 accumulators per thread left ~60 registers for the NTT
-// (spills), every barrier stalls all 16 waves, and the Shoup products with the on-the-fly companion
-// add ~70 VALU instructions per digit and coefficient to a kernel that is already VALU-bound.
-static bool bsgs_pipe() {
-    static const bool on = [] {
-        const char* e = getenv("FHESPEAR_BSGS_PIPE");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-static bool giant_fused(const DevTables& T) {
-    static const bool on = [] {
-        const char* e = getenv("FHESPEAR_GIANT_FUSED");
-        return e && atoi(e) != 0;
-    }();
-    return on && T.logN >= 8 && T.logN <= 14 && !T.ks_seal;
-}
+// Hadamard (every giant group's inner product), then the giant steps: INTT + centred ModUp + NTT of
+// the B - 1 inner products (one ModUp each), key inner products with the automorphism applied on the
+// fly, special-limb INTT, the giant sum before ModDown (k_giant_sum) and one ModDown NTT per output
+// limb (k_giant_final).  One stream, serial: the limbs are those of the reference loop bg:464-485.
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
-                       u64* out, u64* ws, size_t ws_bytes,
-                       void* items_dev, const Stager& sg, const BsgsStreams& ss, const KTimer* tm) {
+                       u64* out, u64* ws, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
+                       const KTimer* tm) {
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
     if (T.N % 128 || G > 64 || R > 512) return hipErrorInvalidValue;
-    if (R > 0 && bsgs_giant_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
-    const int C = (R > 0 && !giant_fused(T) && !T.ks_seal)
-                      ? std::max(1, std::min(ss.chunks, std::min(R, (ss.nev - 2) / 2))) : 1;
-    hipStream_t sm = ss.main, sa = ss.aux;
-    hipEvent_t ev_start = ss.ev[0], ev_end = ss.ev[1];
-    const hipEvent_t* evH = ss.ev + 2;
-    const hipEvent_t* evF = ss.ev + 2 + C;
-    // chunk c covers giant rotations r in [rb(c), rb(c+1)), i.e. giant groups g = r + 1
-    auto rb = [&](int c) { return (int)((long long)c * R / C); };
+    if (R > 0 && bsgs_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
     KsItem items[512];
     const u64* uniq[512];
-    for (int c = 0; c < C; ++c)
-        for (int r = rb(c); r < rb(c + 1); ++r) {
-            const int g = r + 1;
-            const u64* ct = inner + (size_t)g * 2 * S;
-            u64 elt = 1;
-            if (giant_elts) elt = giant_elts[g];
-            else
-                for (int s2 = 0; s2 < g * G; ++s2) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
-            items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)(r - rb(c)),
-                              akeys_host ? akeys_host[g] : nullptr};
-            uniq[r] = ct + S;
-        }
-    // SEAL convention: each giant input is automorphed before its decomposition (serial schedule,
-    // C = 1; the permutations are enqueued after the Hadamard that produces the inputs)
+    for (int r = 0; r < R; ++r) {
+        const int g = r + 1;
+        const u64* ct = inner + (size_t)g * 2 * S;
+        u64 elt = 1;
+        if (giant_elts) elt = giant_elts[g];
+        else
+            for (int s2 = 0; s2 < g * G; ++s2) elt = (elt * 5) & (2 * N - 1);   // 5^(g G) mod 2N
+        items[r] = KsItem{ct + S, ct, nullptr, keys_host[g], nullptr, nullptr, elt, (u64)r,
+                          akeys_host ? akeys_host[g] : nullptr};
+        uniq[r] = ct + S;
+    }
+    // SEAL convention: each giant input is automorphed before its decomposition (the permutations
+    // are enqueued after the Hadamard that produces the inputs)
     std::vector<KsItem> seal_orig;
     u64* seal_perm = ws + ks_core_bytes(T, R, R, l) / 8;
     if (T.ks_seal && R > 0) {
@@ -1919,158 +1429,32 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
         if (e != hipSuccess) return e;
     }
-    // Hadamard chunk c: giant groups [g0(c), g1(c)) (chunk 0 also produces g = 0, which needs no rotation)
-    const bool split = ss.split_hadamard && R > 0 && C > 1;
-    auto hg0 = [&](int c) { return c == 0 ? 0 : rb(c) + 1; };
-    auto hg1 = [&](int c) { return split ? rb(c + 1) + 1 : B; };
-    auto hadamard = [&](int c, hipStream_t st) -> hipError_t {
-        FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-        hipError_t e = launch_inner(T, baby_dev, pts_dev, G, hg0(c), hg1(c), D, l, inner, st);
-        FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
-        hipEventRecord(evH[c], st);
-        return e;
-    };
-    hipError_t he = hipSuccess;
-    if (split) {
-        hipEventRecord(ev_start, sm);
-        hipStreamWaitEvent(sa, ev_start, 0);
-        he = hadamard(0, sa);
-    } else {
-        he = hadamard(0, sm);
-        for (int c = 1; c < C; ++c) hipEventRecord(evH[c], sm);
-    }
+    FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
+    hipError_t he = launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, 0, B, D, l, inner, st);
+    FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
     if (he != hipSuccess) return he;
+    if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
     if (!seal_orig.empty()) {
-        he = seal_permute(T, seal_orig.data(), R, l, seal_perm, sm);
+        he = seal_permute(T, seal_orig.data(), R, l, seal_perm, st);
         if (he != hipSuccess) return he;
-    }
-    hipEventRecord(ev_start, sm);
-    hipStreamWaitEvent(sa, ev_start, 0);
-    if (R <= 0) {
-        hipEventRecord(ev_end, sa);
-        hipStreamWaitEvent(sm, ev_end, 0);
-        return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, sm);
     }
     u64* base = ws + keyswitch_workspace_bytes(T, R, R, l) / 8;
     u64* convsum = base + 2 * S;
-    if (giant_fused(T)) {   // serial: INTT + counts, fused ModUp x key, reduce, ModDown sum
-        FHS_DISPATCH_LOGN(T.logN, {
-            if constexpr (LOGN >= 8 && LOGN <= 14) {
-                const KsBufs b = ks_carve(T, ws, R, R, l);
-                const int E = l + T.P, dn = (l + T.P - 1) / T.P;
-                FHS_TMARK(tm, KID_KS_INTT, 1, sm);
-                if (ks_intt_half<LOGN>(l * R))
-                    hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * R), dim3((1 << LOGN) / 32), 0, sm, T, uq, b.acoef, l,
-                                       R);
-                else
-                    hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * R), dim3((1 << LOGN) / 16), 0, sm, T, uq, b.acoef, l, R);
-                launch_centered(T, b.acoef, b.vcnt, l, R, sm);
-                FHS_TMARK(tm, KID_KS_INTT, 0, sm);
-                FHS_TMARK(tm, KID_KS_FUSED, 1, sm);
-                hipLaunchKernelGGL((k_ks_giant_fused<LOGN>), dim3(xcd_grid(E, R)), dim3((1 << LOGN) / 16), 0, sm, T, it, uq,
-                                   b.acoef, b.vcnt, b.acc, l, R);
-                FHS_TMARK(tm, KID_KS_FUSED, 0, sm);
-                FHS_TMARK(tm, KID_KS_IP, 1, sm);
-                hipLaunchKernelGGL(k_giant_ip_reduce, dim3(eltwise_grid(2 * S)), dim3(256), 0, sm, T, it, b.acc, l, R);
-                FHS_TMARK(tm, KID_KS_IP, 0, sm);
-                FHS_TMARK(tm, KID_SPECIAL_INTT, 1, sm);
-                FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), sm, T, b.acc, b.ycoef, l, R);
-                FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sm);
-                FHS_TMARK(tm, KID_GIANT_SUM, 1, sm);
-                hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0, sm, T, b.acc, b.ycoef, inner, base,
-                                   convsum, l, R, 1, 1);
-                FHS_TMARK(tm, KID_GIANT_SUM, 0, sm);
-                FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-                FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), sm, T, base, convsum, out, l);
-                FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
-            }
-        });
-        return hipGetLastError();
-    }
-    if (C > 1 && !split && bsgs_pipe()) {
-        // Pipelined giant steps (FHESPEAR_BSGS_PIPE=1): INTT + centred counts of all R inputs in one
-        // launch, then ModUp chunk by chunk on `main` while `aux` runs the previous chunk's key inner
-        // products (memory-bound, no LDS: they fit beside the two ModUp workgroups of a CU when
-        // register caps leave room); chunk c's t < l partial sum goes to acc slot c, the special-limb
-        // INTT and the giant sum run once over all R at the end.  Same residues as the serial path.
-        FHS_DISPATCH_LOGN(T.logN, {
-            const KsBufs all = ks_carve(T, ws, R, R, l);
-            const size_t E = l + T.P, dn = (l + T.P - 1) / T.P;
-            hipStreamWaitEvent(sm, evH[0], 0);
-            FHS_TMARK(tm, KID_KS_INTT, 1, sm);
-            if (ks_intt_half<LOGN>(l * R))
-                hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * R), dim3((1 << LOGN) / 32), 0, sm, T, uq, all.acoef, l, R);
-            else
-                hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * R), dim3((1 << LOGN) / 16), 0, sm, T, uq, all.acoef, l, R);
-            launch_centered(T, all.acoef, all.vcnt, l, R, sm);
-            FHS_TMARK(tm, KID_KS_INTT, 0, sm);
-            const int NB = T.N >> 8;
-            for (int c = 0; c < C; ++c) {
-                const int Rc = rb(c + 1) - rb(c);
-                const KsBufs bc = ks_at(T, all, rb(c), rb(c), l);
-                FHS_TMARK(tm, KID_MODUP, 1, sm);
-                launch_modup<LOGN>(T, uq + rb(c), bc.acoef, bc.vcnt, bc.ext, l, Rc, sm);
-                FHS_TMARK(tm, KID_MODUP, 0, sm);
-                hipEventRecord(evF[c], sm);
-                hipStreamWaitEvent(sa, evF[c], 0);
-                FHS_TMARK(tm, KID_KS_IP, 1, sa);
-                hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(T.P, Rc * NB)), dim3(256), 0, sa, T, it + rb(c), uq + rb(c), bc.ext,
-                                   bc.acc, l, Rc, l);
-                hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, sa, T, it + rb(c), uq + rb(c), bc.ext,
-                                   all.acc + (size_t)c * 2 * E * N, l, Rc, 1);
-                FHS_TMARK(tm, KID_KS_IP, 0, sa);
-            }
-            FHS_TMARK(tm, KID_SPECIAL_INTT, 1, sa);
-            FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), sa, T, all.acc, all.ycoef, l, R);
-            FHS_TMARK(tm, KID_SPECIAL_INTT, 0, sa);
-            FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
-            hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0, sa, T, all.acc, all.ycoef, inner, base,
-                               convsum, l, R, 1, C);
-            FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
-            hipEventRecord(ev_end, sa);
-            hipStreamWaitEvent(sm, ev_end, 0);
-            FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-            FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), sm, T, base, convsum, out, l);
-            FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
-        });
-        return hipGetLastError();
-    }
     FHS_DISPATCH_LOGN(T.logN, {
-        const KsBufs all = ks_carve(T, ws, R, R, l);
-        // main: INTT + centred ModUp + NTT per chunk, as soon as its inner products exist
-        for (int c = 0; c < C; ++c) {
-            hipStreamWaitEvent(sm, evH[c], 0);
-            ks_modup_stage<LOGN>(T, uq + rb(c), rb(c + 1) - rb(c), l, ks_at(T, all, rb(c), rb(c), l), sm, tm);
-            hipEventRecord(evF[c], sm);
-        }
-        // aux: Hadamard of chunk c + 1, then key inner product, special-limb INTT and the running
-        // giant sum of chunk c
-        for (int c = 0; c < C; ++c) {
-            if (split && c + 1 < C) {
-                he = hadamard(c + 1, sa);
-                if (he != hipSuccess) return he;
-            }
-            const int Rc = rb(c + 1) - rb(c);
-            const KsBufs bc = ks_at(T, all, rb(c), rb(c), l);
-            hipStreamWaitEvent(sa, evF[c], 0);
-            giant_ip_stage<LOGN>(T, it + rb(c), uq + rb(c), Rc, l, bc, sa, tm);
-            FHS_TMARK(tm, KID_GIANT_SUM, 1, sa);
-            hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0, sa, T, bc.acc, bc.ycoef, inner, base,
-                               convsum, l, Rc, c == 0 ? 1 : 0, (FHS_KSIP_VEC == 2 && T.N >= 512) ? 1 : ksip_parts(Rc));
-            FHS_TMARK(tm, KID_GIANT_SUM, 0, sa);
-        }
-        hipEventRecord(ev_end, sa);
-        hipStreamWaitEvent(sm, ev_end, 0);
-        FHS_TMARK(tm, KID_GIANT_FINAL, 1, sm);
-        FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), sm, T, base, convsum, out, l);
-        FHS_TMARK(tm, KID_GIANT_FINAL, 0, sm);
+        const KsBufs b = ks_carve(T, ws, R, R, l);
+        ks_modup_stage<LOGN>(T, uq, R, l, b, st, tm);
+        giant_ip_stage<LOGN>(T, it, uq, R, l, b, st, tm);
+        FHS_TMARK(tm, KID_GIANT_SUM, 1, st);
+        hipLaunchKernelGGL(k_giant_sum, dim3((T.N + 255) / 256, 2, (l + FHS_GSUM_ICH - 1) / FHS_GSUM_ICH), dim3(256), 0,
+                           st, T, b.acc, b.ycoef, inner, base, convsum, l, R);
+        FHS_TMARK(tm, KID_GIANT_SUM, 0, st);
+        FHS_TMARK(tm, KID_GIANT_FINAL, 1, st);
+        FHS_NTT_LAUNCH(k_giant_final, l * 2, dim3(l, 2), st, T, base, convsum, out, l);
+        FHS_TMARK(tm, KID_GIANT_FINAL, 0, st);
     });
     return hipGetLastError();
 }
 
-size_t bsgs_giant_workspace_bytes(const DevTables& T, int R, int l) {
-    return keyswitch_workspace_bytes(T, R, R, l) + 8 * (size_t)T.N * 4 * l;
-}
 
 
 // ============================================================================ sampling / keys

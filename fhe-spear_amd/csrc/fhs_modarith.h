@@ -90,9 +90,6 @@ __device__ __forceinline__ u64 shoup_lazy(u64 a, u64 w, u64 wp, u64 q) {
 #if FHS_ASM_SHOUP   // a w - qh q = a w + qh (2^64 - q) mod 2^64
     const u64 qh = mulhi64a(a, wp);
     return mullo64a2(a, w, qh, 0 - q);
-#elif defined(FHS_OLD_SHOUP)
-    const u64 qh = __umul64hi(a, wp);
-    return a * w - qh * q;
 #else
     const u64 qh = mulhi64x(a, wp);
     return mullo64x(a, w) - mullo64x(qh, q);
@@ -312,9 +309,7 @@ __device__ __forceinline__ u64 pm_fold64(u64 x, const RedU& R) {
 }
 // Canonical residue of a forward-NTT output: lazy outputs are < (4 + 2 logN) q, Harvey ones < 4q.
 __device__ __forceinline__ u64 fwd_canon(u64 x, const RedU& R) {
-#ifndef FHS_NO_LAZY
     if (R.lazy) return pm_fold64(x, R);
-#endif
     return csub(csub(x, 2 * R.q), R.q);
 }
 __device__ __forceinline__ u64 reduce64(u64 a, const PrimeK& P) { return reduce128(a, 0, P); }

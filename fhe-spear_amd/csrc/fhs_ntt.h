@@ -73,20 +73,10 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
 #pragma unroll 1
     for (int c = 0; c < NG; ++c) {
         const int gid = tid + c * T;
-        #ifdef FHS_NO_SCALAR_TW
-        const int blk = gid / TL, off = gid % TL;
-#else
         const int blk = TL >= 64 ? __builtin_amdgcn_readfirstlane(gid) / TL : gid / TL, off = gid % TL;
-#endif
         const int j0 = blk * 2 * TF + off;
-#ifdef FHS_NO_GRP_PAD
-        const int base = 0;
-#define FHS_GRP_ADDR(k) lds_pad(j0 + (k) * TL)
-#else
         const int base = lds_pad(j0);
 #define FHS_GRP_ADDR(k) grp_pad<TL, GS>(j0, base, (k))
-#endif
-        (void)base;
         u64 x[GS];
 #pragma unroll
         for (int k = 0; k < GS; ++k) x[k] = lds[FHS_GRP_ADDR(k)];
@@ -162,9 +152,6 @@ __device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __rest
                                             int hoff = 0) {
     static_assert(LOGN >= 7 && LOGN <= 14, "LDS-resident NTT supports 128 <= N <= 16384");
     static_assert(EPT >= 16 && (EPT & (EPT - 1)) == 0, "EPT must be a power of two >= 16");
-#ifdef FHS_NO_LAZY
-    lazy = false;
-#endif
     if (lazy)
         fwd_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q, hoff);
     else

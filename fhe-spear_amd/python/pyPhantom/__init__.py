@@ -911,6 +911,9 @@ def galois_keys_from_numpy(ctx, keys):
     SEAL's KSwitchKeys: component 0 = b_j = -a_j s + e_j + P g_j s', component 1 = a_j; the layout
     galois_key.export returns)."""
     elts = sorted(int(e) for e in keys)
+    want = _switch_key_shape(ctx)
+    for e in elts:
+        _check_key_shape(keys[e], want, f"galois_keys_from_numpy: key for element {e}")
     arr = np.ascontiguousarray(np.stack([np.asarray(keys[e], dtype=np.uint64) for e in elts]))
     e_arr = np.array(elts, dtype=np.uint64)
     h = _vp()
@@ -919,7 +922,20 @@ def galois_keys_from_numpy(ctx, keys):
     return galois_key(ctx, h)
 
 
+def _switch_key_shape(ctx):
+    """(dnum, 2, L0+P, N): the layout the C side reads without a length (fhs_*_import)."""
+    return (-(-ctx.L0 // ctx.P), 2, ctx.L0 + ctx.P, ctx.N)
+
+
+def _check_key_shape(arr, want, what):
+    shape = tuple(np.shape(arr))
+    if shape != tuple(want):
+        raise ValueError(f"{what}: shape {shape}, this context needs {tuple(want)}")
+
+
 def relin_key_from_numpy(ctx, key):
+    """[dnum][2][L0+P][N] -> relin_key (the galois_keys_from_numpy layout)."""
+    _check_key_shape(key, _switch_key_shape(ctx), "relin_key_from_numpy")
     a = np.ascontiguousarray(key, dtype=np.uint64)
     h = _vp()
     _check(_lib.fhs_relin_key_import(ctx._h, a.ctypes.data_as(_u64p), C.byref(h)), "relin_key_from_numpy")
@@ -928,6 +944,7 @@ def relin_key_from_numpy(ctx, key):
 
 def secret_key_from_numpy(ctx, s_ntt):
     """[L0+P][N] NTT-form secret -> secret_key (its encryption randomness: a fresh 256-bit key)."""
+    _check_key_shape(s_ntt, (ctx.L0 + ctx.P, ctx.N), "secret_key_from_numpy")
     a = np.ascontiguousarray(s_ntt, dtype=np.uint64)
     sk = secret_key.__new__(secret_key)
     sk._ctx, sk.seed = ctx, None
@@ -955,8 +972,7 @@ class Event:
 
 
 KERNEL_IDS = {"k_bsgs_inner": 0, "k_modup": 1, "k_ks_ip": 2, "k_moddown": 3, "k_ks_intt": 4,
-              "k_ks_special_intt": 5, "k_giant_sum": 6, "k_giant_final": 7, "rescale": 8,
-              "k_ks_giant_fused": 9}
+              "k_ks_special_intt": 5, "k_giant_sum": 6, "k_giant_final": 7, "rescale": 8}
 
 
 def kernel_timer_arm(ctx, names=None):

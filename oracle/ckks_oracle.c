@@ -795,14 +795,16 @@ void ock_encrypt_symmetric(const ock_ctx* c, const uint8_t* key32, uint64_t coun
     }
     free(e); free(et);
 }
-/* the public key's encryption-mask key: 256 PRF bits (w0 of blocks 0..3) of stream ST_PK_RNG */
-void ock_pk_rng_key(const uint8_t* key32, uint8_t* rng32) {
+/* the encryption-mask key of the gen-th public key made from a secret key: 256 PRF bits (w0 of
+   blocks 0..3) of stream ST_PK_RNG with a = gen (each public key object draws its own masks) */
+void ock_pk_rng_key_gen(const uint8_t* key32, uint64_t gen, uint8_t* rng32) {
     prf_key K = prf_key_from_bytes(key32);
     for (int w = 0; w < 4; w++) {
-        uint64_t v = prf_small(&K, stream_id(ST_PK_RNG, 0, 0), (uint64_t)w);
+        uint64_t v = prf_small(&K, stream_id(ST_PK_RNG, gen, 0), (uint64_t)w);
         for (int b = 0; b < 8; b++) rng32[8 * w + b] = (uint8_t)(v >> (8 * b));
     }
 }
+void ock_pk_rng_key(const uint8_t* key32, uint8_t* rng32) { ock_pk_rng_key_gen(key32, 0, rng32); }
 void ock_encrypt_asymmetric(const ock_ctx* c, const uint8_t* rng32, uint64_t counter, const uint64_t* pk,
                             const uint64_t* pt, int l, uint64_t* ct) {
     uint64_t N = c->N; size_t S = (size_t)l * N; int L0 = c->L0;

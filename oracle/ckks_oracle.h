@@ -37,6 +37,7 @@ uint64_t ock_rnd(uint64_t key, uint64_t ctr);   /* test data only (random plaint
 void ock_chacha20_block(const uint32_t key[8], uint32_t counter, const uint32_t nonce[3], uint32_t out[16]);
 /* the public key's encryption-mask key, derived from the secret key's 32 bytes */
 void ock_pk_rng_key(const uint8_t* key32, uint8_t* rng32);
+void ock_pk_rng_key_gen(const uint8_t* key32, uint64_t gen, uint8_t* rng32);
 /* uniform residue mod q from (key, prime index, coefficient) by rejection (switching-key a_j) */
 uint64_t ock_seeded_uniform(uint64_t key, int pi, uint64_t n, uint64_t q);
 

@@ -51,6 +51,7 @@ def lib():
             getattr(L, name).argtypes = [C.c_uint64]
         L.ock_chacha20_block.argtypes = [C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.ock_pk_rng_key.argtypes = [C.c_char_p, C.c_char_p]
+        L.ock_pk_rng_key_gen.argtypes = [C.c_char_p, C.c_uint64, C.c_char_p]
         L.ock_rnd.restype = C.c_uint64
         L.ock_rnd.argtypes = [C.c_uint64, C.c_uint64]
         vp = C.c_void_p
@@ -127,9 +128,10 @@ def _sm64_for_tests(x: int) -> int:
     return int(lib().ock_splitmix64(x))
 
 
-def pk_rng_key(key32: bytes) -> bytes:
+def pk_rng_key(key32: bytes, gen: int = 0) -> bytes:
+    """Mask key of the gen-th public key generated from the secret key `key32` (fhs_gen_public_key)."""
     out = C.create_string_buffer(32)
-    lib().ock_pk_rng_key(key32, out)
+    lib().ock_pk_rng_key_gen(key32, gen, out)
     return out.raw
 
 
@@ -349,12 +351,12 @@ class Oracle:
         lib().ock_encrypt_symmetric(self._h, key_bytes(seed), counter, _p(s), _p(np.ascontiguousarray(pt)), l, _p(ct))
         return ct
 
-    def encrypt_asymmetric(self, seed: int, counter: int, pk, pt):
+    def encrypt_asymmetric(self, seed: int, counter: int, pk, pt, pk_gen: int = 0):
         """`seed`: the SECRET key's seed; the masks come from the public key's own PRF key
-        (pk_rng_key), as in fhs_gen_public_key."""
+        (pk_rng_key of the pk_gen-th public key made from that secret key), as in fhs_gen_public_key."""
         l = pt.shape[0]
         ct = np.empty((2, l, self.N), dtype=np.uint64)
-        lib().ock_encrypt_asymmetric(self._h, pk_rng_key(key_bytes(seed)), counter, _p(np.ascontiguousarray(pk)),
+        lib().ock_encrypt_asymmetric(self._h, pk_rng_key(key_bytes(seed), pk_gen), counter, _p(np.ascontiguousarray(pk)),
                                      _p(np.ascontiguousarray(pt)), l, _p(ct))
         return ct
 

@@ -13,6 +13,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD MI355X (gfx950) GPU; run with -m gpu")
 
 
+# Oracle-comparing (limb-parity) files first, so a `-x` stop later in the GPU suite still leaves the
+# core rows proven; the remaining files keep pytest's order.
+_FIRST = ["test_gpu_parity.py", "test_golden_replay.py", "test_seal_mode.py", "test_full_size.py",
+          "test_fri_ring.py", "test_bootstrap.py", "test_giant_shard.py"]
+
+
+def pytest_collection_modifyitems(session, config, items):
+    rank = {name: i for i, name in enumerate(_FIRST)}
+    items.sort(key=lambda it: rank.get(Path(str(it.fspath)).name, len(_FIRST)))   # stable: in-file order kept
+
+
 def gpu_available():
     try:
         import pyPhantom as ph

@@ -414,3 +414,23 @@ def test_recorded_reference_calls_replay_on_the_oracle(orc, case):
         ct = z[f"c{i}_ct_in"]
         baby = [ct] + [o.rotate(ct, baby_keys[b], b) for b in range(1, G)]
         assert np.array_equal(o.bsgs_loop(baby, pts, giant_keys, G, B, D), z[f"c{i}_out"]), f"call {i}"
+
+
+def test_bench_digest_recomputed_by_the_oracle(orc):
+    """bench.py's parity field compares its output limbs with tests/golden/manifest.json's
+    bench_digests, which only the C oracle writes (tests/golden/make_bench_digest.py): the small
+    configuration's digest is recomputed here from scratch, and the committed full-size records carry
+    the bench's seeds and shapes."""
+    sys.path.insert(0, str(GOLDEN))
+    import make_bench_digest as mbd
+    man = json.loads((GOLDEN / "manifest.json").read_text())["bench_digests"]
+    rec = mbd.digest("small", 2)
+    assert rec["sha256"] == man["small"]["sha256"]
+    import bench
+    for cfg in ("cfg2", "cfg1"):
+        r = man[cfg]
+        N, L0, P, D = mbd.CONFIGS[cfg]
+        assert (r["N"], r["L0"], r["P"], r["D"]) == (bench.CONFIGS[cfg]["N"], bench.CONFIGS[cfg]["L0"],
+                                                     bench.CONFIGS[cfg]["P"], bench.CONFIGS[cfg]["D"])
+        assert (r["sk_seed"], r["input_seed"], r["diag_seed"]) == (bench.SK_SEED, bench.INPUT_SEED, bench.DIAG_SEED)
+        assert r["shape"] == [2, L0 - 1, N] and r["key_switch_mode"] == "exact"

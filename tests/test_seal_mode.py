@@ -183,3 +183,15 @@ def test_gpu_imported_keys_reproduce_rotations(ph, orc, mode):
     with pytest.raises(ValueError):
         bad = {elts[0]: np.full_like(okeys[elts[0]], np.iinfo(np.uint64).max)}
         ph.galois_keys_from_numpy(ctx, bad)
+    # shapes are checked before the C side reads dnum (L0+P) N words from the pointer: a key made for
+    # another dnum / P / N raises instead of being read out of bounds
+    k0 = okeys[elts[0]]
+    for bad_shape in (k0[:-1], k0[:, :, :-1], k0[..., : N // 2], k0[0]):
+        with pytest.raises(ValueError, match="shape"):
+            ph.galois_keys_from_numpy(ctx, {elts[0]: bad_shape})
+        with pytest.raises(ValueError, match="shape"):
+            ph.relin_key_from_numpy(ctx, bad_shape)
+    with pytest.raises(ValueError, match="shape"):
+        ph.secret_key_from_numpy(ctx, s[:-1])
+    with pytest.raises(ValueError, match="shape"):
+        ph.secret_key_from_numpy(ctx, s[:, : N // 2])

@@ -11,5 +11,5 @@ timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 cat "$OUT/smoke.log"
 timeout -k 10 400 python bench.py > "$OUT/bench.log" 2>&1 || { echo "bench failed"; tail -5 "$OUT/bench.log"; exit 1; }
 tail -1 "$OUT/bench.log" > "$OUT/bench.json"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-block > "$OUT/stats.log" 2>&1 || { echo "rocprof failed"; tail -5 "$OUT/stats.log"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-block --no-seal > "$OUT/stats.log" 2>&1 || { echo "rocprof failed"; tail -5 "$OUT/stats.log"; exit 1; }
 echo done
