@@ -13,8 +13,9 @@ an RWKV block, one per GPU at N=8: BASELINE configs[3]) and the output ciphertex
 to rank 0 over RCCL every step -- weak scaling, `value` = matvecs/s summed over ranks.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the kernel with the largest device time inside
-the timed region (HIP events on the library's stream around every launch); `cpu_baseline` times
-the in-repo C oracle (single core) on a bounded sample of the same workload.
+the timed region (HIP events on the library's stream around every launch); `cpu_baseline` times full
+matvecs of the same workload with the in-repo SEAL-class CPU port (oracle/cpu_port.c, OpenMP on the
+host cores this process may use); `parity` checks the output limbs against the C oracle's digest.
 """
 import argparse
 import json
@@ -144,10 +145,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rotations", type=int, default=6)
-    ap.add_argument("--cpu-sample-diagonals", type=int, default=128)
-    ap.add_argument("--cpu-reps", type=int, default=5, help="timed reps per worker (after one warmup rep); "
-                                                              "BASELINE.md plan: median of >= 5")
+    ap.add_argument("--cpu-reps", type=int, default=3, help="timed full CPU matvecs (after one untimed)")
     ap.add_argument("--no-block", action="store_true",
                     help="skip the measured RWKV-block leg (cfg3 on the same ranks) of the default line")
     ap.add_argument("--block-steps", type=int, default=3)
@@ -156,7 +154,6 @@ def main():
     ap.add_argument("--block-dealt", action="store_true",
                     help="block leg over N GPUs: deal each stage's projections only (default at N > 1: latency "
                          "mode, each projection's giant steps sharded over a rank group as with --split)")
-    ap.add_argument("--cpu-workers", type=int, default=16)
     ap.add_argument("--split", action="store_true",
                     help="cfg3 over N GPUs: latency mode, giant steps of each projection sharded over a rank group")
     args = ap.parse_args()
@@ -584,46 +581,30 @@ def bench_block(args, ph, dist, rank, world, local):
 
 
 def cpu_baseline(cfg, primes, args):
-    """The C oracle (oracle/ckks_oracle.c) on a bounded sample of the same matvec, one process per
-    core (W = min(16, cpu_count): the box's CPU share): each worker runs `r` rotations (individual,
-    non-hoisted, as the reference's CPU path issues them) and `d` multiply_plain+add pairs at the
-    same level; the slowest worker's times are extrapolated to one matvec's 89 rotations and 2048
-    products spread over W cores."""
-    import multiprocessing as mp
+    """SURVEY.md §8(d)'s CPU baseline: the build's own CPU restatement with SEAL-class arithmetic
+    (oracle/cpu_port.c: Harvey lazy NTT with Shoup twiddles, Barrett-reduced lazy sums, OpenMP), timed
+    over FULL matvecs of this exact workload -- the G-1 baby rotations and the B-1 giant rotations
+    issued one at a time (non-hoisted, as the reference's CPU path issues them), D multiply_plain+add,
+    the final rescale -- on the host cores this process may use (OMP_NUM_THREADS: 16 on the GPU box,
+    its share of the node).  One untimed matvec, then args.cpu_reps timed; the median is reported.
+    Its output limbs are checked against the oracle digest of the workload (the same one the GPU
+    output is checked against)."""
+    from oracle import cpu_port
     N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
-    W = max(1, min(args.cpu_workers, os.cpu_count() or 1))
-    nr = max(1, min(args.cpu_sample_rotations, (G - 1) + (B - 1)))
-    nd = max(1, min(args.cpu_sample_diagonals, D))
-    ctx = mp.get_context("spawn")
-    barrier = ctx.Barrier(W)
-    out = ctx.Queue()
-    from oracle.cpu_bench import worker
-    procs = [ctx.Process(target=worker, args=(N, [int(q) for q in primes], P, G, nr, nd, w, barrier, out, args.cpu_reps))
-             for w in range(W)]
-    for p in procs:
-        p.start()
-    try:
-        res = [out.get(timeout=900) for _ in procs]
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.terminate()
-    rot = (G - 1) + (B - 1)
-    # per worker: the median of its reps; then the slowest worker (all W run concurrently)
-    t_rot = max(float(np.median(r[0])) for r in res)
-    t_dia = max(float(np.median(r[1])) for r in res)
-    wall = sum(sum(r[0]) + sum(r[1]) for r in res) / len(res)
-    per_matvec = t_rot * rot / (W * nr) + t_dia * D / (W * nd)
-    return {"value": round(1.0 / per_matvec, 5), "unit": "matvec/s", "cores": W, "kind": "port",
-            "cpu_model": cpu_model(),
-            "sample": f"build C oracle (oracle/ckks_oracle.c), not TenSEAL (not importable, SURVEY §8c): {W} "
-                      f"processes x (1 warmup + {args.cpu_reps} timed reps) x ({nr} of {rot} rotations + {nd} of {D} "
-                      f"multiply_plain/add) at L0={L0}, N={N}, non-hoisted rotations as the reference issues "
-                      f"them; median rep per worker, slowest worker extrapolated to one matvec "
-                      f"({wall:.1f} s wall sampled per worker)",
-            "sec_per_matvec": round(per_matvec, 3)}
+    assert [int(q) for q in primes] == [int(q) for q in cpu_port.create_coeff_modulus(N, [59] * (L0 + P))]
+    secs, y, t_setup, threads = cpu_port.baseline(N, L0, P, D, reps=args.cpu_reps, sk_seed=SK_SEED,
+                                                  input_seed=INPUT_SEED, diag_seed=DIAG_SEED)
+    med = float(np.median(secs))
+    return {"value": round(1.0 / med, 5), "unit": "matvec/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"full matvec x {len(secs)}, median (after 1 untimed): oracle/cpu_port.c, SEAL-class CPU "
+                      f"restatement (Harvey NTT + Shoup, Barrett lazy sums, OpenMP over rotations/giant groups), "
+                      f"{(G - 1) + (B - 1)} non-hoisted rotations + {D} multiply_plain/add + rescale at N={N}, "
+                      f"L0={L0}, P={P}; not TenSEAL (not importable, SURVEY §8c)",
+            "sec_per_matvec": round(med, 4), "sec_per_matvec_all": [round(v, 4) for v in secs],
+            "setup_s": round(t_setup, 1),
+            "parity": limb_digest_check(args.config, y)}
 
 
 if __name__ == "__main__":

@@ -434,3 +434,24 @@ def test_bench_digest_recomputed_by_the_oracle(orc):
                                                      bench.CONFIGS[cfg]["P"], bench.CONFIGS[cfg]["D"])
         assert (r["sk_seed"], r["input_seed"], r["diag_seed"]) == (bench.SK_SEED, bench.INPUT_SEED, bench.DIAG_SEED)
         assert r["shape"] == [2, L0 - 1, N] and r["key_switch_mode"] == "exact"
+
+
+def test_cpu_port_matches_oracle(orc):
+    """bench.py's CPU baseline (oracle/cpu_port.c: Harvey NTT, Shoup/Barrett, OpenMP) computes the
+    oracle's limbs: single non-hoisted rotations at two rings, and the whole small bench matvec
+    against the oracle-made digest of tests/golden/manifest.json."""
+    from oracle import cpu_port as cp
+    for N, L0, P in ((2048, 4, 2), (4096, 6, 3)):
+        primes = [int(q) for q in orc.create_coeff_modulus(N, [59] * (L0 + P))]
+        o = orc.Oracle(N, primes, P)
+        s = o.gen_secret(7)
+        ct = o.encrypt_symmetric(7, 0, s, o.random_plaintext(3, 0, L0))
+        port = cp.CpuPort(N, primes, P, 2)
+        for st in (1, 3, -5):
+            k = o.gen_galois_key(7, s, orc.galois_elt(st, N))
+            assert np.array_equal(port.rotate(ct, k, st), o.rotate(ct, k, st)), (N, st)
+    import bench
+    secs, y, _, _ = cp.baseline(4096, 6, 3, 256, reps=1, threads=2, sk_seed=bench.SK_SEED,
+                                input_seed=bench.INPUT_SEED, diag_seed=bench.DIAG_SEED)
+    man = json.loads((GOLDEN / "manifest.json").read_text())["bench_digests"]
+    assert cp.sha256(y) == man["small"]["sha256"]
