@@ -88,7 +88,7 @@ def kernel_source_hash():
     """sha256 of the kernel sources: ties a committed PMC traffic record to the kernels it measured."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("fhs_kernels.hip", "fhs_ntt.h", "fhs_modarith.h"):
+    for f in ("fhs_kernels.hip", "fhs_ntt.h", "fhs_modarith.h", "fhs_buffer.h"):
         h.update((REPO / "fhe-spear_amd" / "csrc" / f).read_bytes())
     return h.hexdigest()[:16]
 

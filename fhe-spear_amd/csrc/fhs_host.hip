@@ -761,6 +761,8 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     };
     DevTables& T = c->T;
     T.N = (int)N; T.logN = c->logN; T.L0 = L0; T.P = P; T.K = K; T.dnum = dnum;
+    T.max_qbits = 0;
+    for (int i = 0; i < K; ++i) T.max_qbits = std::max(T.max_qbits, 64 - __builtin_clzll(c->q[i]));
     HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");
     HIPCHK(up(twf.data(), 8 * twf.size(), (const void**)&T.tw_fwd), "tables");
     HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");
@@ -1713,10 +1715,11 @@ static void crt_compose(const fhs_context* c, const std::vector<uint64_t>& limbs
 
 // Coefficients of a decrypted plaintext are |x| = |m| scale + noise: the centred CRT over the first
 // k limbs (prod q_i >= scale 2^72) is the same integer as over all l, hence the same double, whenever
-// |x| < Q_{k+1} / 2 -- i.e. for every plaintext whose coefficients are below 2^71 scale, the range
-// CKKS decoding is meant for.  k+1 limbs are composed and |x| >= Q_k / 4 falls back to all l limbs,
-// which catches coefficients between Q_k / 4 and Q_{k+1} / 2; a coefficient of |x| >= Q_{k+1} / 2
-// whose residue mod Q_{k+1} happens to be small is NOT detected (it decodes to the aliased value).
+// |x| < Q_k / 2 -- every plaintext whose coefficients are below 2^71 scale, the range CKKS decoding is
+// meant for.  The GPU composes k+1 limbs and checks the result against every other limb (it must equal
+// the coefficient's residue mod each q_e): all agree exactly when the composition IS the coefficient
+// (both lie in (-Q_l/2, Q_l/2) and agree mod Q_l), so any larger coefficient -- which would otherwise
+// decode to an aliased value -- is detected and the decoder composes all l limbs instead.
 // FHESPEAR_DECODE_FULL=1 always composes all l limbs.
 static int decode_limbs(const fhs_context* c, double scale, int l) {
     double bits = 0, need = std::log2(std::max(scale, 1.0)) + 72.0;
@@ -1762,24 +1765,54 @@ static void crt_consts(const fhs_context* c, int l, fhs::CrtConsts& K) {
     }
     for (int w = 0; w < W; ++w) K.halfQ[w] = (K.Q[w] >> 1) | (w + 1 < W ? K.Q[w + 1] << 63 : 0);
 }
-// INTT of the first k limbs and their centred CRT composition on the GPU: N doubles to the host
-static fhs_status decode_coeffs_dev(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<double>& m) {
-    const size_t N = c->N, bytes = 8ull * k * N;
+// INTT of the first lv limbs and the centred CRT composition of the first k on the GPU, checked against
+// limbs k..lv-1 (*exact = every coefficient matched them); N doubles to the host
+static fhs_status decode_coeffs_dev(fhs_context* c, const fhs_plaintext* pt, int k, int lv, std::vector<double>& m,
+                                    bool* exact) {
+    const size_t N = c->N, bytes = 8ull * lv * N;
+    const int nx = lv - k;
     fhs::CrtConsts K;
     crt_consts(c, k, K);
-    uint64_t *tmp = nullptr, *dbl = nullptr;
+    std::vector<uint64_t> vt((size_t)nx * fhs::kCrtVtabWords, 0);
+    for (int e = 0; e < nx; ++e) {
+        uint64_t* v = vt.data() + (size_t)e * fhs::kCrtVtabWords;
+        const uint64_t q = c->q[k + e];
+        const hu128 R = (~(hu128)0) / q;   // floor(2^128 / q) for odd q
+        v[0] = q;
+        v[1] = (uint64_t)R;
+        v[2] = (uint64_t)(R >> 64);
+        const uint64_t t64 = (uint64_t)((((hu128)1) << 64) % q);
+        uint64_t pw = 1 % q;
+        for (int w = 0; w < K.W; ++w) {
+            v[3 + w] = pw;
+            pw = h_mulmod(pw, t64, q);
+        }
+    }
+    const size_t extra_b = 8 * vt.size() + 8;   // vtab, then the mismatch flag
+    uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr;
     HIPCHK(dalloc(c, &tmp, bytes), "decode");
     hipError_t e = dalloc(c, &dbl, 8 * N);
     if (e != hipSuccess) { dfree(c, tmp, bytes); return hip_fail(e, "decode"); }
+    e = dalloc(c, &aux, extra_b);
+    if (e != hipSuccess) { dfree(c, dbl, 8 * N); dfree(c, tmp, bytes); return hip_fail(e, "decode"); }
+    unsigned* flag = reinterpret_cast<unsigned*>(aux + vt.size());
+    unsigned hflag = 0;
     e = hipMemcpyAsync(tmp, pt->d, bytes, hipMemcpyDeviceToDevice, c->st);
-    if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, tmp, k, k, 1, 0, c->st);
-    if (e == hipSuccess) e = fhs::launch_crt_compose(K, tmp, reinterpret_cast<double*>(dbl), (int)N, c->st);
+    if (e == hipSuccess && nx > 0) e = stage_h2d(c, aux, vt.data(), 8 * vt.size());
+    if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4, c->st);
+    if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, tmp, lv, lv, 1, 0, c->st);
+    if (e == hipSuccess)
+        e = fhs::launch_crt_compose(K, tmp, reinterpret_cast<double*>(dbl), (int)N, c->st, tmp + (size_t)k * N, nx, aux,
+                                    flag);
     m.resize(N);
     if (e == hipSuccess) e = hipMemcpyAsync(m.data(), dbl, 8 * N, hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&hflag, flag, 4, hipMemcpyDeviceToHost, c->st);
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    dfree(c, aux, extra_b);
     dfree(c, dbl, 8 * N);
     dfree(c, tmp, bytes);
     if (e != hipSuccess) return hip_fail(e, "decode");
+    *exact = hflag == 0;
     return FHS_OK;
 }
 static fhs_status decode_coeffs(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<uint64_t>& host) {
@@ -1798,7 +1831,8 @@ static fhs_status decode_coeffs(fhs_context* c, const fhs_plaintext* pt, int k, 
 // arithmetic, same doubles as the host composition, which FHESPEAR_DECODE_HOST_CRT=1 forces)
 static fhs_status decode_compose(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<double>& m) {
     static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;   // A/B and test knob
-    if (k <= fhs::kCrtMaxL && !host_crt) return decode_coeffs_dev(c, pt, k, m);
+    bool unused;
+    if (k <= fhs::kCrtMaxL && !host_crt) return decode_coeffs_dev(c, pt, k, k, m, &unused);
     std::vector<uint64_t> host;
     const fhs_status s = decode_coeffs(c, pt, k, host);
     if (s != FHS_OK) return s;
@@ -1814,17 +1848,16 @@ extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double
     const int k = full ? l : decode_limbs(c, pt->scale, l), kk = std::min(l, k + 1);
     HostTrace ht;
     std::vector<double> m;
-    fhs_status s = decode_compose(c, pt, kk, m);
-    if (s != FHS_OK) return s;
-    if (k < kk) {   // |x| < Q_k / 4 (first k limbs) makes the k-limb and kk-limb compositions equal
-        double qk = 1.0;
-        for (int i = 0; i < k; ++i) qk *= (double)c->q[i];
-        double mx = 0;
-        for (size_t i = 0; i < N; ++i) mx = std::max(mx, std::fabs(m[i]));
-        if (!(mx < 0.25 * qk) && kk < l) {   // |x| too large for the shortcut: all l limbs
-            s = decode_compose(c, pt, l, m);
-            if (s != FHS_OK) return s;
-        }
+    static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;   // A/B and test knob
+    bool exact = false;
+    fhs_status s = FHS_OK;
+    if (kk < l && kk <= fhs::kCrtMaxL && !host_crt) {   // kk limbs composed, checked against the other l - kk
+        s = decode_coeffs_dev(c, pt, kk, l, m, &exact);
+        if (s != FHS_OK) return s;
+    }
+    if (!exact) {   // all l limbs (the only composition when kk = l; else an aliased coefficient was caught)
+        s = decode_compose(c, pt, l, m);
+        if (s != FHS_OK) return s;
     }
     ht.mark("decode: intt + crt");
     // slots z_j = m(zeta^(5^j)) = sum_{k < N/2} (m_k + i m_{k+N/2}) zeta^k omega^(s_j k), omega = zeta^4,
@@ -2200,6 +2233,49 @@ extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_cip
         p[k] = pts[k]->d;
     }
     return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out);
+}
+
+// The Hadamard half of the fused BSGS alone: outs[g] = sum_{b < G} baby[b] (.) pts[g G + b], g < B, not
+// rescaled (scale baby * pt).  Used by the baby-step-sharded latency mode (fhespear_dist.bsgs_baby_sharded):
+// a rank holding baby steps b in its share forms every giant group's partial inner product.
+extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_ciphertext* const* baby, int G,
+                                              const fhs_plaintext* const* pts, int B, fhs_ciphertext** outs) {
+    ENTER(c);
+    if (!pts || !outs || !baby) return fail(FHS_ERR_INVALID, "null argument");
+    if (G < 1 || G > 64 || B < 1) return fail(FHS_ERR_INVALID, "bsgs_inner_products: 1 <= G <= 64, B >= 1");
+    const int D = B * G, ci = baby[0]->ci, l = baby[0]->l;
+    if ((size_t)D + G > (size_t)fhs_context::kMaxPtrs) return fail(FHS_ERR_INVALID, "bsgs_inner_products: too many plaintexts");
+    std::vector<const uint64_t*> ptrs(G + D);
+    for (int b = 0; b < G; ++b) {
+        if (!baby[b] || baby[b]->l != l || baby[b]->ncomp != 2 || baby[b]->ci != ci)
+            return fail(FHS_ERR_LEVEL, "bsgs_inner_products: baby steps must share one chain index");
+        ptrs[b] = baby[b]->d;
+    }
+    for (int k = 0; k < D; ++k) {
+        if (!pts[k] || pts[k]->ci != ci) return fail(FHS_ERR_LEVEL, "bsgs_inner_products: plaintext at a different chain index");
+        if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_inner_products: plaintext scales differ");
+        ptrs[G + k] = pts[k]->d;
+    }
+    const size_t S = (size_t)l * c->N;
+    HIPCHK(stage_h2d(c, c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D)), "bsgs_inner_products");
+    const uint64_t* const* dbaby = reinterpret_cast<const uint64_t* const*>(c->ptrs_dev);
+    uint64_t* inner = nullptr;
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * B * 2 * S, &inner), "bsgs_inner_products");
+    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dbaby + G, G, 0, B, D, l, inner, c->st), "bsgs_inner_products");
+    std::vector<fhs_ciphertext*> made;
+    for (int g = 0; g < B; ++g) {
+        fhs_ciphertext* r;
+        fhs_status st = new_ct(c, 2, ci, baby[0]->scale * pts[0]->scale, &r);
+        if (st == FHS_OK && hipMemcpyAsync(r->d, inner + (size_t)g * 2 * S, 16 * S, hipMemcpyDeviceToDevice, c->st) != hipSuccess)
+            st = fail(FHS_ERR_HIP, "bsgs_inner_products: copy");
+        if (st != FHS_OK) {
+            for (fhs_ciphertext* m : made) fhs_ciphertext_destroy(m);
+            return st;
+        }
+        made.push_back(r);
+        outs[g] = r;
+    }
+    return FHS_OK;
 }
 
 extern "C" fhs_status fhs_linear_transform(fhs_context* c, const fhs_ciphertext* const* baby, int G,

@@ -31,6 +31,7 @@ struct DevTables {
     // default); 1 = SEAL's switch_key_inplace (P = 1): per-limb lift without centring, automorphism
     // before the decomposition, ModDown rounded by adding floor(p/2)
     int ks_seal;
+    int max_qbits;            // bits of the largest prime (<= 59: split-30 high halves < 2^29, fewer folds)
 };
 
 // One key-switch of a batch: out = KS_key( galois_elt(a) ) + (galois_elt(add0), add1).
@@ -89,6 +90,10 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                        int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
                        u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
                        const KTimer* tm);
+// inner[g] = sum_{b < G, gG + b < D} baby[b] (.) pts[gG + b] for g in [g0, g1) (k_bsgs_inner), inner laid out
+// [g][2][l][N]
+hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int g0,
+                             int g1, int D, int l, u64* inner, hipStream_t st);
 // CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
 // apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
@@ -119,7 +124,14 @@ struct CrtConsts {
     u64 hat[kCrtMaxL][kCrtMaxL + 1];
     u64 Q[kCrtMaxL + 1], halfQ[kCrtMaxL + 1];
 };
-hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st);
+// verify (optional, nx > 0): the composed integer x (|x| < Q_l / 2 of the first l limbs, centred) must
+// also agree with every further limb -- extra[e][n] (coefficient form) == x mod q_e for e < nx, vtab[e] =
+// {q_e, floor(2^128/q_e) lo, hi, (2^64)^w mod q_e for w < W}; any mismatch (x aliased: the coefficient is
+// too large for l limbs) sets *flag
+hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st,
+                              const u64* extra = nullptr, int nx = 0, const u64* vtab = nullptr,
+                              unsigned* flag = nullptr);
+constexpr int kCrtVtabWords = 3 + kCrtMaxL + 1;   // per extra limb in vtab
 
 // per-limb constants for k_scalar (value mod q_i and its Shoup companion)
 constexpr int kMaxScalarLimbs = 64;

@@ -16,6 +16,7 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_KSIP_UNROLL 2   // digits of the key inner product unrolled together (2: 64 VGPRs, 8 waves/SIMD)
 #endif
 #include "fhs_ntt.h"
+#include "fhs_buffer.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -647,21 +648,66 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     }
 }
 
+// ModUp conversion of a 3-limb digit into target limb `m` (pseudo-Mersenne fold, PrimeK.pm bit 40)
+// for one half-limb workgroup: each thread converts its 16 coefficient pairs (e, e + N/2), does the
+// global first NTT stage on them in registers, writes the lower results to LDS and keeps the upper
+// ones in hi[].  Loads are buffer loads: the digit's three limbs and the centred counts through one
+// descriptor each, the per-lane part (tid) in voffset and every limb / chunk offset in soffset.
+template <int LOGN>
+__device__ __forceinline__ void modup_convert3(const u64* yb, const unsigned char* vb, const u64* hat, int K,
+                                               u64 negQ, const RedU& R, u64 w0, u64 w0p, int tid, u64* lds,
+                                               u64 hi[16]) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32, CH = FHS_MODUPH_CH;
+    const __amdgpu_buffer_rsrc_t ry = brsrc(yb, 3 * N * 8), rv = brsrc(vb, N);
+    const Split30 h0 = split30(hat[0]), h1 = split30(hat[K]), h2 = split30(hat[2 * K]);
+    const u64 m = R.q, q2 = 2 * m;
+    const int vo = tid * 8;
+#pragma unroll
+    for (int ch = 0; ch < 16 / CH; ++ch) {
+        u64 y[3][2 * CH];
+        uint32_t vv[2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) {
+            const int e = (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);   // coefficient index minus tid
+#pragma unroll
+            for (int w = 0; w < 3; ++w)
+                y[w][k] = bload64(ry, vo, (w * N + e) * 8);
+            vv[k] = __builtin_amdgcn_raw_buffer_load_b8(rv, tid, e, 0);
+        }
+        u64 x[2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) {
+            Acc3 a = {0, 0, 0};
+            acc3_mac(a, split30(y[0][k]), h0);
+            acc3_mac(a, split30(y[1][k]), h1);
+            acc3_mac(a, split30(y[2][k]), h2);
+            // - v Q_S folded into L as v (m - Q_S mod m); result in [0, 2m)
+            const uint32_t v = vv[k];
+            const u64 vq = mul32w(v, (uint32_t)negQ) + ((u64)(v * (uint32_t)(negQ >> 32)) << 32);
+            x[k] = acc3_reduce_pm(a.L + vq, a.M, a.H, R.b, R.d);
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {   // global stage 0: (e, e + N/2), twiddle psi^rev(1)
+            const u64 tt = shoup_lazy(x[CH + k], w0, w0p, m);
+            lds[row_pad<TH>(tid, ch * CH + k)] = x[k] + tt;
+            hi[ch * CH + k] = x[k] + (q2 - tt);
+        }
+    }
+}
+
 // (b1') ModUp + NTT with half the limb in LDS (68 KiB at N = 16384): two workgroups share a CU,
 // so one's loads and base conversion overlap the other's NTT.  Stage 0 of the forward NTT pairs
 // coefficient e with e + N/2; each thread converts both, applies that butterfly in registers, keeps
 // the upper half in registers while the lower half is transformed in LDS, then transforms it.
 // Same values as k_modup (same butterflies, same lazy bounds: < q + 2 q log N).
 template <int LOGN>
-__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
-                                                                 const u64* acoef, const unsigned char* vcnt, u64* ext,
-                                                                 int l, int U) {
+constexpr int modup_h_lds_words() { return (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16; }
+// one workgroup's share: target limb t of digit j = mi % dn of input u = mi / dn
+template <int LOGN>
+__device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoef, const unsigned char* vcnt, u64* ext,
+                                             int l, int t, int mi, int tid, u64* lds) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;   // 16 coefficient pairs per thread
-    __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
-    const int tid = threadIdx.x;
     const int P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
-    int t, mi;
-    if (!xcd_tinner(E, dn * U, t, mi)) return;
     const int j = mi % dn, u = mi / dn;
     const int s0 = j * P_, s1 = min(s0 + P_, l), ns = s1 - s0;
     u64* o = ext + (((size_t)u * dn + j) * E + t) * N;
@@ -679,8 +725,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
     u64 w0, w0p;
     ld_tw(tw, 1, w0, w0p);
     const u64 q2 = 2 * m;
-    constexpr int CH = FHS_MODUPH_CH;   // coefficient pairs per conversion chunk
     u64 hi[16];
+    if (ns == 3 && R.cpm) {
+        // the usual digit (P = 3 limbs, pseudo-Mersenne target): compile-time digit size, buffer loads
+        // whose limb / chunk offsets are scalar (no per-load address arithmetic on the VALU)
+        modup_convert3<LOGN>(yb, vb, hat, K, negQ, R, w0, w0p, tid, lds, hi);
+    } else {
+    constexpr int CH = FHS_MODUPH_CH;   // coefficient pairs per conversion chunk
 #pragma unroll
     for (int ch = 0; ch < 16 / CH; ++ch) {
         Acc3 a3[2 * CH];
@@ -728,6 +779,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
             hi[ch * CH + k] = x[k] + (q2 - tt);
         }
     }
+    }
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
         if (h) {   // lower half written out: the upper half moves from registers into LDS
@@ -737,13 +789,21 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
         }
         __syncthreads();
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, m, R.lazy, 1 + h);
-        u64* oh = o + h * NH;
+        // buffer stores: per-lane offset tid, the half / row offset in soffset
+        const __amdgpu_buffer_rsrc_t ro = brsrc(o, N * 8);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            const int e = tid + c * TH;
-            oh[e] = fwd_canon(lds[row_pad<TH>(tid, c)], R);
-        }
+        for (int c = 0; c < 16; ++c) bstore64(fwd_canon(lds[row_pad<TH>(tid, c)], R), ro, tid * 8, (h * NH + c * TH) * 8);
     }
+}
+template <int LOGN>
+__global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
+                                                                 const u64* acoef, const unsigned char* vcnt, u64* ext,
+                                                                 int l, int U) {
+    __shared__ __attribute__((aligned(16))) u64 lds[modup_h_lds_words<LOGN>()];
+    const int E = l + T.P, dn = (l + T.P - 1) / T.P;
+    int t, mi;
+    if (!xcd_tinner(E, dn * U, t, mi)) return;
+    modup_h_body<LOGN>(T, acoef, vcnt, ext, l, t, mi, threadIdx.x, lds);
 }
 
 template <int LOGN>
@@ -765,25 +825,52 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
 // 512-byte region: four whole cache lines, no amplification.
 // Limbs t >= t0 only (the giant-step path sums limbs t < l over rotations in k_ks_ip_sum).  A digit's
 // own limbs were not extended (k_modup skips them): they are read from the input itself.
-__device__ __forceinline__ const u64* ks_src(const u64* ext_tj, const u64* own_t, int t, int j, int P_, int l) {
-    return (t >= j * P_ && t < min(j * P_ + P_, l)) ? own_t : ext_tj;
+// Operands of one (rotation, target limb) key inner product as buffer descriptors built from
+// wave-uniform pointers: the per-lane offsets (gathered source slot sn, key slot n) go in voffset, the
+// digit strides in soffset -- global loads without 64-bit address arithmetic on the VALU, and (unlike
+// the flat loads the generic pointers produced) counted on vmcnt alone, so the digits' loads overlap.
+struct KsOps {
+    __amdgpu_buffer_rsrc_t ext, own, key, akey;
+    int sn8, n8;      // per-lane byte offsets: gathered source slot, key slot
+    int per_r8, kn8;  // digit strides in bytes: ext (E N), key (K N)
+    int jown;         // the digit whose own limb t is (read from the input, not extended); -1 if none
+};
+__device__ __forceinline__ KsOps ks_ops(const DevTables& T, const KsItem& it, const u64* const* uniq, const u64* ext,
+                                        int t, int pt, int l, int n, int sn) {
+    const int N = T.N, P_ = T.P, E = l + P_, dn = (l + P_ - 1) / P_, K = T.K;
+    KsOps o;
+    o.ext = brsrc(ext + ((size_t)it.src * dn * E + t) * N, (uint32_t)((size_t)dn * E * N * 8));
+    o.own = brsrc(uniq[it.src] + (size_t)t * N, (uint32_t)N * 8);
+    o.key = brsrc(it.key + (size_t)pt * N, (uint32_t)((size_t)T.dnum * K * N * 8));
+    o.akey = brsrc(it.akey ? it.akey + (size_t)pt * N : it.key, (uint32_t)((size_t)T.dnum * K * N * 8));
+    o.sn8 = sn * 8;
+    o.n8 = n * 8;
+    o.per_r8 = E * N * 8;
+    o.kn8 = K * N * 8;
+    o.jown = t < l ? t / P_ : -1;
+    return o;
 }
+constexpr int kBufNT = 2;   // buffer aux: non-temporal (streamed once: the switching keys)
 // sum_j ext_j[t][sigma(n)] (b_j, a_j)[t][n] as two lazy 128-bit sums; a_j regenerated from the key's
 // seeds, or read from an imported key's explicit a (akey, a separate instantiation: the choice is
 // per item, so the digit loop carries no branch)
+typedef const __attribute__((address_space(4))) u64* cu64p;   // constant address space: scalar loads
 template <bool EXPLICIT_A>
-__device__ __forceinline__ void ks_digits(const DevTables& T, const u64* ex, const u64* own, const u64* key,
-                                          const u64* akey, const u64* seeds, u64 cx, const RedU& RD, unsigned qb,
-                                          int t, int l, int dn, size_t per_r, u128& c0, u128& c1) {
-    const int P_ = T.P;
-    const size_t KN = (size_t)T.K * T.N;
+__device__ __forceinline__ void ks_digits(const KsOps& o, const u64* seeds_g, u64 cx, const RedU& RD, unsigned qb,
+                                          int dn, u128& c0, u128& c1) {
+    // the seeds are wave-uniform and read-only: scalar loads instead of flat vector loads
+    const cu64p seeds = (cu64p)seeds_g;
     Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
 #pragma unroll FHS_KSIP_UNROLL
     for (int j = 0; j < dn; ++j) {
-        const Split30 v = split30(*ks_src(ex + (size_t)j * per_r, own, t, j, P_, l));
-        acc3_mac(a0, v, split30(__builtin_nontemporal_load(key + (size_t)j * KN)));
+        const bool own = j == o.jown;
+        const u64 x = own ? bload64(o.own, o.sn8, 0) : bload64(o.ext, o.sn8, j * o.per_r8);
+        const Split30 v = split30(x);
+        acc3_mac(a0, v, split30(__builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(o.key, o.n8, j * o.kn8,
+                                                                                             kBufNT))));
         if constexpr (EXPLICIT_A)
-            acc3_mac(a1, v, split30(__builtin_nontemporal_load(akey + (size_t)j * KN)));
+            acc3_mac(a1, v, split30(__builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(o.akey, o.n8,
+                                                                                                 j * o.kn8, kBufNT))));
         else
             acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
         if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
@@ -802,22 +889,19 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     if (!xcd_touter(E - t0, R * NB, t, m)) return;   // rotations of one limb t run together on one XCD
     t += t0;
     const int r = m / NB, n = ((m % NB) << 8) + threadIdx.x;
-    const size_t per_r = (size_t)E * N;
     const int pt = t < l ? t : T.L0 + (t - l);
     const RedU RD = redu(PK(T, pt));
     const KsItem it = items[r];
     const int sn = galois_src(n, it.elt, T.logN);
-    const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
-    const u64* own = uniq[it.src] + (size_t)t * N + sn;
-    const u64* key = it.key + (size_t)pt * N + n;
+    const KsOps o = ks_ops(T, it, uniq, ext, t, pt, l, n, sn);
     const u64* seeds = it.key + (size_t)T.dnum * K * N;
     const u64 cx = seeded_ctr_mix(pt, n);
     const unsigned qb = 64 - __clzll(RD.q);
     u128 c0 = {0, 0}, c1 = {0, 0};
     if (it.akey)
-        ks_digits<true>(T, ex, own, key, it.akey + (size_t)pt * N + n, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
+        ks_digits<true>(o, seeds, cx, RD, qb, dn, c0, c1);
     else
-        ks_digits<false>(T, ex, own, key, nullptr, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
+        ks_digits<false>(o, seeds, cx, RD, qb, dn, c0, c1);
     acc[(((size_t)r * 2 + 0) * E + t) * N + n] = reduce128(c0.lo, c0.hi, RD);
     acc[(((size_t)r * 2 + 1) * E + t) * N + n] = reduce128(c1.lo, c1.hi, RD);
 }
@@ -833,7 +917,6 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
     int t, m;
     if (!xcd_touter(l, NB, t, m)) return;
     const int n = (m << 8) + threadIdx.x;
-    const size_t per_r = (size_t)E * N;
     const RedU RD = redu(PK(T, t));
     const u64 q = RD.q;
     const u64 cx = seeded_ctr_mix(t, n);
@@ -842,18 +925,16 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
     for (int r = 0; r < R; ++r) {
         const KsItem it = items[r];
         const int sn = galois_src(n, it.elt, T.logN);
-        const u64* ex = ext + ((size_t)it.src * dn * E + t) * N + sn;
-        const u64* own = uniq[it.src] + (size_t)t * N + sn;
-        const u64* key = it.key + (size_t)t * N + n;
+        const KsOps o = ks_ops(T, it, uniq, ext, t, t, l, n, sn);
         const u64* seeds = it.key + (size_t)T.dnum * K * N;
         u128 c0 = {0, 0}, c1 = {0, 0};
         if (it.akey)
-            ks_digits<true>(T, ex, own, key, it.akey + (size_t)t * N + n, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
+            ks_digits<true>(o, seeds, cx, RD, qb, dn, c0, c1);
         else
-            ks_digits<false>(T, ex, own, key, nullptr, seeds, cx, RD, qb, t, l, dn, per_r, c0, c1);
+            ks_digits<false>(o, seeds, cx, RD, qb, dn, c0, c1);
         s0 = addmod(s0, reduce128(c0.lo, c0.hi, RD), q);
         s1 = addmod(s1, reduce128(c1.lo, c1.hi, RD), q);
-        sadd = addmod(sadd, it.add0[(size_t)t * N + sn], q);
+        sadd = addmod(sadd, bload64(brsrc(it.add0 + (size_t)t * N, (uint32_t)N * 8), o.sn8, 0), q);
     }
     const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
     acc[((size_t)0 * E + t) * N + n] = addmod(shoup(s0, pinv, pinv_s, q), sadd, q);
@@ -920,6 +1001,44 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
     }
 }
 
+// ModDown conversion of the P = 3 special limbs (coefficient form, already scaled by inv(P/p_k)) into
+// data limb i (pseudo-Mersenne fold), half-limb form as modup_convert3: x = sum_k y_k (P/p_k) mod q_i,
+// global first NTT stage in registers, lower results to LDS, upper ones kept in hi[].
+template <int LOGN>
+__device__ __forceinline__ void moddown_convert3(const u64* y, const u64* hat, int L0, const RedU& R, u64 w0, u64 w0p,
+                                                 int tid, u64* lds, u64 hi[16]) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32, CH = 2;
+    const __amdgpu_buffer_rsrc_t ry = brsrc(y, 3 * N * 8);
+    const Split30 h0 = split30(hat[0]), h1 = split30(hat[L0]), h2 = split30(hat[2 * L0]);
+    const u64 m = R.q, q2 = 2 * m;
+    const int vo = tid * 8;
+#pragma unroll
+    for (int ch = 0; ch < 16 / CH; ++ch) {
+        u64 v[3][2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) {
+            const int e = (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);
+#pragma unroll
+            for (int w = 0; w < 3; ++w) v[w][k] = bload64(ry, vo, (w * N + e) * 8);
+        }
+        u64 x[2 * CH];
+#pragma unroll
+        for (int k = 0; k < 2 * CH; ++k) {
+            Acc3 a = {0, 0, 0};
+            acc3_mac(a, split30(v[0][k]), h0);
+            acc3_mac(a, split30(v[1][k]), h1);
+            acc3_mac(a, split30(v[2][k]), h2);
+            x[k] = acc3_reduce_pm(a.L, a.M, a.H, R.b, R.d);
+        }
+#pragma unroll
+        for (int k = 0; k < CH; ++k) {
+            const u64 tt = shoup_lazy(x[CH + k], w0, w0p, m);
+            lds[row_pad<TH>(tid, ch * CH + k)] = x[k] + tt;
+            hi[ch * CH + k] = x[k] + (q2 - tt);
+        }
+    }
+}
+
 // k_moddown with half the limb in LDS (see k_modup_h): conversion of both coefficients of each
 // (e, e + N/2) pair, global NTT stage 0 in registers, then each half transformed in LDS and finished
 // ((acc - conv) P^-1 + sigma(c0)).  Same values as k_moddown.
@@ -943,6 +1062,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     u64 w0, w0p;
     ld_tw(tw, 1, w0, w0p);
     u64 hi[16];
+    if (P_ == 3 && RU.cpm && !T.ks_seal) {
+        moddown_convert3<LOGN>(y, T.md_hat + i, T.L0, RU, w0, w0p, tid, lds, hi);
+    } else {
 #pragma unroll
     for (int ch = 0; ch < 8; ++ch) {   // 2 pairs per chunk
         Acc3 a3[4];
@@ -980,6 +1102,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             hi[ch * 2 + k] = x[k] + (q2 - tt);
         }
     }
+    }
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
     const u64* add = comp == 0 ? it.add0 : it.add1;
     const u64 aelt = comp == 0 ? it.elt : 1;
@@ -995,22 +1118,32 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
         __syncthreads();
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, q, RU.lazy, 1 + h);
         // outputs in batches of 4 whose accumulator (and rotated c0) loads are issued together, with
-        // the add / no-add choice outside the loop (one latency per batch, not one per coefficient)
+        // the add / no-add choice outside the loop (one latency per batch, not one per coefficient);
+        // buffer loads / stores with the row offsets in soffset
+        const __amdgpu_buffer_rsrc_t rac = brsrc(ac, N * 8), ro = brsrc(o, N * 8);
         if (add) {
-            const u64* ad = add + (size_t)i * N;
+            const __amdgpu_buffer_rsrc_t rad = brsrc(add + (size_t)i * N, N * 8);
+            // galois_src(e) for e = tid + c TH + h NH: rev(e) = rev(tid) + rev(c TH + h NH) (disjoint bits),
+            // so the exponent (2 rev(e) + 1) elt mod 2N is a per-thread base plus a wave-uniform term
+            const unsigned rt = __brev((unsigned)tid) >> (32 - LOGN);
+            const u64 ebase = ((2 * (u64)rt + 1) * aelt) & (2 * (u64)N - 1);
 #pragma unroll
             for (int c0 = 0; c0 < 16; c0 += 4) {
                 u64 av[4], dv[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int e = h * NH + tid + (c0 + k) * TH;
-                    av[k] = ac[e];
-                    dv[k] = ad[galois_src(e, aelt, LOGN)];
+                    const int eo = h * NH + (c0 + k) * TH;
+                    av[k] = bload64(rac, tid * 8, eo * 8);
+                    const u64 ec = (2 * (u64)(__brev((unsigned)eo) >> (32 - LOGN)) * aelt) & (2 * (u64)N - 1);
+                    const u64 e2 = (ebase + ec) & (2 * (u64)N - 1);
+                    const int src = (int)(__brev((unsigned)((e2 - 1) >> 1)) >> (32 - LOGN));
+                    dv[k] = bload64(rad, src * 8, 0);
                 }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const u64 v = fwd_canon(lds[row_pad<TH>(tid, c0 + k)], RU);
-                    o[h * NH + tid + (c0 + k) * TH] = addmod(shoup(submod(av[k], v, q), pinv, pinv_s, q), dv[k], q);
+                    bstore64(addmod(shoup(submod(av[k], v, q), pinv, pinv_s, q), dv[k], q), ro, tid * 8,
+                             (h * NH + (c0 + k) * TH) * 8);
                 }
             }
         } else {
@@ -1018,11 +1151,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             for (int c0 = 0; c0 < 16; c0 += 4) {
                 u64 av[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) av[k] = ac[h * NH + tid + (c0 + k) * TH];
+                for (int k = 0; k < 4; ++k) av[k] = bload64(rac, tid * 8, (h * NH + (c0 + k) * TH) * 8);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const u64 v = fwd_canon(lds[row_pad<TH>(tid, c0 + k)], RU);
-                    o[h * NH + tid + (c0 + k) * TH] = shoup(submod(av[k], v, q), pinv, pinv_s, q);
+                    bstore64(shoup(submod(av[k], v, q), pinv, pinv_s, q), ro, tid * 8, (h * NH + (c0 + k) * TH) * 8);
                 }
             }
         }
@@ -1157,24 +1290,32 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
 // Block = 4 waves sharing one 64-coefficient slice of limb i: the slice of all G baby steps
 // (both components) is staged once in LDS, each wave then streams the diagonals of its giant
 // groups (g = wave, wave+4, ...) from HBM with lazy 128-bit accumulation.
+// diagonal words of plaintext `p` (limb base p + i N) at this lane's coefficients: a non-temporal buffer
+// load (the limb offset and the slice offset n0 are wave-uniform: descriptor base and soffset), so no
+// 64-bit address arithmetic and no flat load (which would also wait on the LDS counter)
 template <int VEC>
-__device__ __forceinline__ void ld_diag(const u64* p, u64* out) {
+__device__ __forceinline__ void ld_diag(const u64* limb, int voff, int soff, u64* out) {
+    const __amdgpu_buffer_rsrc_t r = brsrc(limb, 0x7ffffff0);
     if constexpr (VEC == 2) {
-        const u64x2_t t = __builtin_nontemporal_load(reinterpret_cast<const u64x2_t*>(p));
-        out[0] = t.x;
-        out[1] = t.y;
+        const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kBufNT);
+        out[0] = ((u64)t[1] << 32) | t[0];
+        out[1] = ((u64)t[3] << 32) | t[2];
     } else {
-        out[0] = __builtin_nontemporal_load(p);
+        out[0] = __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kBufNT));
     }
 }
-template <int VEC, int WAVES>
+// FOLD: products per Acc3 before its fold into the 128-bit sums -- 8 for any prime < 2^60, 16 when every
+// prime is < 2^59 (T.max_qbits <= 59): then the split-30 high halves are < 2^29, so L and M gain < 2^60
+// and H < 2^58 per product and 16 products stay below 2^64
+template <int VEC, int WAVES, int FOLD>
 __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
                                                     const u64* const* __restrict__ pts, int G, int g0, int g1, int D,
                                                     int l, u64* __restrict__ inner) {
     extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][W], split-30 packed
     constexpr int W = 64 * VEC;
     const int N = T.N;
-    const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: the diagonal pointers come by scalar loads
     const size_t S = (size_t)l * N;
     const size_t off = (size_t)i * N + n0 + lane * VEC;
     // the first 8 diagonals of this wave's first group are requested before the baby-step slice is
@@ -1184,7 +1325,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     if (g0 + wave < g1 && min(G, D - (g0 + wave) * G) >= 8) {
         const u64* const* pg0 = pts + (size_t)(g0 + wave) * G;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + off, pf[u]);
+        for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, pf[u]);
         have_pf = true;
     }
     for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
@@ -1217,7 +1358,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
             } else
             {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + off, p[u]);
+                for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u)
@@ -1227,15 +1368,17 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
                     acc3_mac(a0[v], unpack30(sb[((b + u) * 2 + 0) * W + lane * VEC + v]), y);
                     acc3_mac(a1[v], unpack30(sb[((b + u) * 2 + 1) * W + lane * VEC + v]), y);
                 }
+            if (FOLD == 8 || (b & 15) == 8) {   // b is the batch's first index: fold after every FOLD products
 #pragma unroll
-            for (int v = 0; v < VEC; ++v) {
-                acc3_fold(c0[v], a0[v]);
-                acc3_fold(c1[v], a1[v]);
+                for (int v = 0; v < VEC; ++v) {
+                    acc3_fold(c0[v], a0[v]);
+                    acc3_fold(c1[v], a1[v]);
+                }
             }
         }
-        for (; b < bmax; ++b) {   // < 8 left: Acc3 capacity holds
+        for (; b < bmax; ++b) {   // < 8 left: at most FOLD - 1 products since the last fold
             u64 p[VEC];
-            ld_diag<VEC>(pg[b] + off, p);
+            ld_diag<VEC>(pg[b] + (size_t)i * N, lane * VEC * 8, n0 * 8, p);
 #pragma unroll
             for (int v = 0; v < VEC; ++v) {
                 const Split30 y = split30(p[v]);
@@ -1380,14 +1523,26 @@ static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, con
     constexpr int W = 64 * VEC;
     static bool attr = false;
     if (!attr) {   // dynamic LDS above 64 KiB must be opted into
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * 2 * W * 8));
-        if (e != hipSuccess) return e;
+        for (const void* k : {reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16>)}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * 2 * W * 8));
+            if (e != hipSuccess) return e;
+        }
         attr = true;
     }
-    hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES>), dim3(T.N / W, l), dim3(64 * WAVES), (size_t)G * 2 * W * 8, st, T,
-                       baby, pts, G, g0, g1, D, l, inner);
+    if (T.max_qbits <= 59)
+        hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16>), dim3(T.N / W, l), dim3(64 * WAVES), (size_t)G * 2 * W * 8, st,
+                           T, baby, pts, G, g0, g1, D, l, inner);
+    else
+        hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 8>), dim3(T.N / W, l), dim3(64 * WAVES), (size_t)G * 2 * W * 8, st,
+                           T, baby, pts, G, g0, g1, D, l, inner);
     return hipGetLastError();
+}
+
+hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int g0,
+                             int g1, int D, int l, u64* inner, hipStream_t st) {
+    if (T.N % 128 || G > 64 || G < 1) return hipErrorInvalidValue;
+    return launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, g0, g1, D, l, inner, st);
 }
 
 // Hadamard (every giant group's inner product), then the giant steps: INTT + centred ModUp + NTT of
@@ -1779,7 +1934,8 @@ hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int coun
 }
 
 // ============================================================================ decode: centred CRT
-__global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double* __restrict__ out, int N) {
+__global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double* __restrict__ out, int N,
+                              const u64* __restrict__ extra, int nx, const u64* __restrict__ vtab, unsigned* flag) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
     const int l = K.l, W = K.W;
@@ -1835,10 +1991,28 @@ __global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double
     double v = 0;   // v 2^64 is exact, so one rounding per step as on the host
     for (int w = W - 1; w >= 0; --w) v = __dadd_rn(__dmul_rn(v, 18446744073709551616.0), (double)x[w]);
     out[n] = neg ? -v : v;
+    // the composition is the true coefficient only if it also matches every limb not composed
+    bool bad = false;
+    for (int e = 0; e < nx; ++e) {
+        const u64* vt = vtab + (size_t)e * kCrtVtabWords;
+        const u64 q = vt[0];
+        u64 lo = 0, hi = 0;   // sum_w x[w] (2^64w mod q) < W 2^123: no overflow
+        for (int w = 0; w < W; ++w) {
+            const u64 p = x[w] * vt[3 + w], ph = __umul64hi(x[w], vt[3 + w]);
+            lo += p;
+            hi += ph + (lo < p);
+        }
+        u64 r = barrett128(lo, hi, q, vt[1], vt[2]);
+        if (neg && r) r = q - r;
+        bad |= r != extra[(size_t)e * N + n];
+    }
+    if (bad) atomicOr(flag, 1u);
 }
-hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st) {
+hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st, const u64* extra,
+                              int nx, const u64* vtab, unsigned* flag) {
     if (K.l < 1 || K.l > kCrtMaxL || K.W != K.l + 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_crt_compose, dim3((N + 255) / 256), dim3(256), 0, st, K, limbs, out, N);
+    if (nx > 0 && (!extra || !vtab || !flag)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_crt_compose, dim3((N + 255) / 256), dim3(256), 0, st, K, limbs, out, N, extra, nx, vtab, flag);
     return hipGetLastError();
 }
 

@@ -206,3 +206,122 @@ def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts,
         return None
     total = from_buffer(ph, ctx, buf, 2, ci, scale)
     return ph.rescale_to_next(ctx, total)
+
+
+# ------------------------------------------------------------------ baby-step sharding (§8e(2))
+def baby_steps_share(G: int, world: int, rank: int) -> list[int]:
+    """Contiguous, balanced share of the baby steps 0..G-1 for `rank` (baby step 0 is the input)."""
+    if world > G:
+        raise ValueError(f"baby_steps_share: {world} ranks for {G} baby steps")
+    base, extra = divmod(G, world)
+    lo = rank * base + min(rank, extra)
+    return list(range(lo, lo + base + (1 if rank < extra else 0)))
+
+
+def baby_sharded_rows(G: int, B: int, D: int, world: int, rank: int) -> list[int]:
+    """Diagonal indices rank `rank` needs in baby-step-sharded mode: its baby steps' column of every
+    giant group."""
+    return [g * G + b for g in range(B) for b in baby_steps_share(G, world, rank) if g * G + b < D]
+
+
+def _reduce_scatter_mod(dist, parts, sizes, moduli_rows, group, host):
+    """parts: [world][kmax][W] int64 (rank r's contribution to every owner's slots); returns this
+    rank's [kmax][W] sums reduced mod q per limb row.  RCCL's integer sum is exact for world (max q - 1)
+    < 2^63 (<= 15 ranks at 59-bit primes); otherwise (or on gloo, which lacks reduce_scatter) the slices
+    are reduced one owner at a time with the modular sum of modular_reduce_sum."""
+    import torch
+    world, kmax, W = parts.shape
+    me = dist.get_rank(group) if group is not None else dist.get_rank()
+    q = torch.as_tensor([int(m) for m in moduli_rows], dtype=torch.int64, device=parts.device).view(-1, 1)
+    if not host and int64_sum_is_exact(world, moduli_rows):
+        out = torch.empty((kmax, W), dtype=torch.int64, device=parts.device)
+        dist.reduce_scatter_tensor(out, parts.reshape(-1), group=group)
+        out.view(kmax, q.shape[0], -1).remainder_(q)
+        return out
+    out = None
+    for owner in range(world):
+        buf = parts[owner].clone()
+        root = owner if group is None else dist.get_global_rank(group, owner)
+        modular_reduce_sum(dist, buf, list(moduli_rows) * kmax, root=root, group=group)
+        if owner == me:
+            out = buf
+    return out
+
+
+_SELECT = {}
+
+
+def _select_plaintexts(ph, ctx, ci):
+    """The plaintexts 0 and 1 (all-ones NTT limbs: the constant polynomial 1) at chain index ci, scale 1."""
+    import numpy as np
+    key = (id(ctx), ci)
+    if key not in _SELECT or _SELECT[key][0] is not ctx:
+        l = ctx.L0 + 1 - ci
+        zero = ph.plaintext_from_numpy(ctx, np.zeros((l, ctx.N), dtype=np.uint64), ci, 1.0)
+        one = ph.plaintext_from_numpy(ctx, np.ones((l, ctx.N), dtype=np.uint64), ci, 1.0)
+        _SELECT[key] = (ctx, zero, one)
+    return _SELECT[key][1], _SELECT[key][2]
+
+
+def bsgs_baby_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, dist, device="cuda",
+                      ranks=None, group=None):
+    """One matvec with its BABY steps split over `ranks` (latency mode without replicated baby
+    rotations).  Rank r rotates the input by its share of b (baby_steps_share; hoisted inside the
+    library), forms the partial inner product of EVERY giant group over those b
+    (ph.bsgs_inner_products), and a reduce-scatter (int64 RCCL sum + one reduction mod q_i, exact)
+    hands each rank the full inner products of its giant groups (giant_groups).  The owner rotates
+    and sums them (ph.linear_transform with identity plaintexts: one giant step per owned group), the
+    partial outputs are summed mod q_i on ranks[0] (modular_reduce_sum), which rescales.  Every term is
+    an exact residue, so the result is limb-identical to ph.bsgs_multiply_accumulate on one GPU.
+    `pts` maps a diagonal index to its plaintext and need only hold baby_sharded_rows of this rank;
+    zero_diag: an encoding of 0 at the diagonals' level and scale (pads the short last group)."""
+    import torch
+    me = dist.get_rank()
+    ranks = list(range(dist.get_world_size())) if ranks is None else list(ranks)
+    R, idx = len(ranks), ranks.index(me)
+    host = dist.get_backend(group) == "gloo"
+    bs = baby_steps_share(G, R, idx)
+    baby = [ct if b == 0 else ph.rotate(ctx, ct, b, gk) for b in bs]
+    flat = [pts[g * G + b] if g * G + b < D else zero_diag for g in range(B) for b in bs]
+    partial = ph.bsgs_inner_products(ctx, baby, flat, len(bs), B)
+    ci, l = partial[0].chain_index(), partial[0].coeff_modulus_size()
+    scale = partial[0].scale()
+    W = 2 * l * ctx.N
+    shares = [giant_groups(B, R, r) for r in range(R)]
+    kmax = max(len(s) for s in shares)
+    parts = torch.zeros((R, kmax, W), dtype=torch.int64, device=device)
+    for r, s in enumerate(shares):
+        for j, g in enumerate(s):
+            to_buffer(ph, ctx, partial[g], parts[r, j])
+    del partial
+    rows = [int(q) for q in ctx.primes[:l]] * 2
+    if host:
+        h = parts.cpu()
+        mine = _reduce_scatter_mod(dist, h, len(shares[idx]), rows, group, True)
+        mine = mine.to(device) if mine is not None else None
+    else:
+        mine = _reduce_scatter_mod(dist, parts, len(shares[idx]), rows, group, False)
+    my_groups = shares[idx]
+    inners = [from_buffer(ph, ctx, mine[j], 2, ci, scale) for j in range(len(my_groups))]
+    # giant steps of the owned groups: identity "diagonals" route inner_j to giant group j
+    zero_pt, one_pt = _select_plaintexts(ph, ctx, ci)
+    k = len(inners)
+    if my_groups[0] == 0:
+        elts = [1] + [ph.get_elt_from_step(g * G, ctx.N) for g in my_groups[1:]]
+        sel = [one_pt if b == j else zero_pt for j in range(k) for b in range(k)]
+    else:
+        elts = [1] + [ph.get_elt_from_step(g * G, ctx.N) for g in my_groups]
+        sel = [zero_pt] * k + [one_pt if b == j else zero_pt for j in range(k) for b in range(k)]
+    part = ph.linear_transform(ctx, inners, sel, k, elts, gk, rescale=False)
+    buf = torch.empty(W, dtype=torch.int64, device=device)
+    to_buffer(ph, ctx, part, buf)
+    if host:
+        h = buf.cpu()
+        modular_reduce_sum(dist, h, rows, root=ranks[0], group=group)
+        buf.copy_(h)
+    else:
+        modular_reduce_sum(dist, buf, rows, root=ranks[0], group=group)
+    if me != ranks[0]:
+        return None
+    total = from_buffer(ph, ctx, buf, 2, ci, part.scale())
+    return ph.rescale_to_next(ctx, total)

@@ -149,6 +149,7 @@ _SIGS = {
     "fhs_upload_plaintexts": (C.c_int, [_vp, _u64p, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
     "fhs_bsgs_from_cpu": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u64p, C.c_int, C.c_int, C.c_int, C.c_double, _vp,
                                     C.POINTER(_vp)]),
+    "fhs_bsgs_inner_products": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp)]),
     "fhs_linear_transform": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.c_int, _u64p, _vp,
                                        C.c_int, C.POINTER(_vp)]),
     "fhs_multiply_const": (C.c_int, [_vp, _vp, C.c_double, C.c_double, C.POINTER(_vp)]),
@@ -768,6 +769,19 @@ def bsgs_multiply_accumulate(ctx, ct_baby, pts, G, B, D, gk):
     bb = (_vp * G)(*[c._h for c in ct_baby[:G]])
     pp = (_vp * D)(*[p._h for p in pts[:D]])
     return _ct(ctx, _lib.fhs_bsgs_multiply_accumulate, bb, G, pp, D, B, gk._h, what="bsgs_multiply_accumulate")
+
+
+def bsgs_inner_products(ctx, ct_baby, pts, G, B):
+    """Extension: the Hadamard half of bsgs_multiply_accumulate alone -- [sum_b baby[b] * pts[g G + b]
+    for g < B], not rotated, not rescaled (fhs_bsgs_inner_products)."""
+    G, B = int(G), int(B)
+    if len(pts) != G * B:
+        raise ValueError(f"bsgs_inner_products: {len(pts)} plaintexts for G={G}, B={B}")
+    bb = (_vp * G)(*[c._h for c in ct_baby[:G]])
+    pp = (_vp * (G * B))(*[p._h for p in pts])
+    hs = (_vp * B)()
+    _check(_lib.fhs_bsgs_inner_products(ctx._h, bb, G, pp, B, hs), "bsgs_inner_products")
+    return [ciphertext(ctx, _vp(hs[g])) for g in range(B)]
 
 
 # ------------------------------------------------------------------ bootstrapping primitives

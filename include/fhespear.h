@@ -193,6 +193,13 @@ fhs_status fhs_host_free(void* ptr);
 fhs_status fhs_linear_transform(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
                                 const fhs_plaintext* const* pts, int D, int B, const uint64_t* giant_elts,
                                 const fhs_galois_keys* gk, int rescale, fhs_ciphertext** out);
+/* Extension (no reference symbol): the Hadamard half of fhs_bsgs_multiply_accumulate on its own --
+ * outs[g] = sum_{b < G} baby[b] (.) pts[g G + b] for g < B (bg:465-476 per giant group), NOT rotated and
+ * NOT rescaled (scale baby * pt).  The baby-step-sharded latency mode (fhespear_dist.bsgs_baby_sharded)
+ * forms every giant group's partial inner product over a rank's share of the baby steps with it.
+ * outs: B new ciphertexts. */
+fhs_status fhs_bsgs_inner_products(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
+                                   const fhs_plaintext* const* pts, int B, fhs_ciphertext** outs);
 /* Extension (no reference symbol): bg:198-203 + bg:361-432 on the device -- the D diagonals of the
  * D x D row-major matrix M1 (complex: M1 + i M2; M2 = NULL for real), group g = k / G rolled by g G,
  * tiled to N/2 slots, encoded at `scale` / `chain_index`.  Limb-identical to encode_*_vector_batch

@@ -55,6 +55,45 @@ def test_giant_sharded_bsgs_bit_exact_two_ranks(require_gpu, D):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,D", [(2, 256), (3, 200), (4, 256)])
+def test_baby_sharded_bsgs_bit_exact(require_gpu, world, D):
+    """Baby-step sharding: each rank rotates its share of the baby steps, forms every
+    giant group's partial inner product, a reduce-scatter hands each rank its groups' inner products,
+    the owners' giant sums are reduced mod q_i on the root -- limb-identical to the one-GPU fused BSGS.
+    `world` ranks share one GPU (gloo, host-staged collectives)."""
+    env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(29601 + world), str(REPO / "tools" / "giant_shard.py"),
+           "--backend", "gloo", "--mode", "baby", "--N", "4096", "--L0", "6", "--P", "3", "--D", str(D), "--reps", "1"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert re.search(r"bit-exact vs one-GPU fused BSGS: True", out.stdout), out.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_baby_sharded_bsgs_over_rccl_world1(require_gpu):
+    """bsgs_baby_sharded through RCCL at world 1 (reduce_scatter_tensor + int64 reduce + event-ordered
+    copies), bit-exact vs the fused BSGS."""
+    env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", "29591", str(REPO / "tools" / "giant_shard.py"),
+           "--backend", "nccl", "--mode", "baby", "--N", "4096", "--L0", "6", "--P", "3", "--D", "256", "--reps", "1"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert re.search(r"bit-exact vs one-GPU fused BSGS: True", out.stdout), out.stdout[-2000:]
+
+
+@pytest.mark.parametrize("G,world", [(46, 1), (46, 2), (46, 8), (16, 3), (5, 5)])
+def test_baby_steps_share_partition(G, world):
+    shares = [fd.baby_steps_share(G, world, r) for r in range(world)]
+    assert sorted(b for s in shares for b in s) == list(range(G))
+    assert max(map(len, shares)) - min(map(len, shares)) <= 1
+    D = 45 * G - 3                          # short last giant group
+    rows = [set(fd.baby_sharded_rows(G, 45, D, world, r)) for r in range(world)]
+    assert sorted(k for r in rows for k in r) == list(range(D))
+
+
+@pytest.mark.gpu
 def test_giant_sharded_bsgs_over_rccl_world1(require_gpu):
     """bsgs_giant_sharded through RCCL (backend nccl) at world 1: the int64 reduce, the event-ordered
     copies between the library stream and torch's stream, and the root's rescale, bit-exact vs the

@@ -134,6 +134,17 @@ def test_block_over_ranks(require_gpu, world, split, babies):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_block_over_ranks_baby_sharded(require_gpu, world):
+    """Latency mode with the baby steps sharded (BlockRunner shard="baby", fhespear_dist.bsgs_baby_sharded:
+    no replicated baby rotations, a reduce-scatter of every giant group's partial inner products):
+    the same decrypted block output as one rank, bit for bit."""
+    err, digest = _run_block_tool(world, extra=["--split", "--shard", "baby"], port=29561 + world)
+    assert err < 1e-4
+    assert digest == _one_rank_digest()
+
+
+@pytest.mark.gpu
 def test_block_exchange_over_rccl_world1(require_gpu):
     """The real transport: backend nccl (RCCL) at world 1 with the process group forced on, so the
     input broadcast, the output gather and the event ordering between the library stream and torch's

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--D", type=int, default=2048)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--mode", default="giant", choices=("giant", "baby"),
+                    help="shard the giant groups (baby steps replicated) or the baby steps (reduce-scatter "
+                         "of every group's partial inner products, fhespear_dist.bsgs_baby_sharded)")
     ap.add_argument("--simulate-world", type=int, nargs="*", default=[],
                     help="also time one rank's share of the compute at these world sizes (on this GPU alone)")
     a = ap.parse_args()
@@ -67,6 +70,8 @@ def main():
     dev = f"cuda:{local}"
 
     def sharded():
+        if a.mode == "baby":
+            return fd.bsgs_baby_sharded(ph, ctx, ct, pts, G, B, D, gk, zero[0], dist, dev)
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         return fd.bsgs_giant_sharded(ph, ctx, baby, pts, G, B, D, gk, zero, dist, dev)
 
@@ -94,7 +99,7 @@ def main():
             ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
         ctx.synchronize()
         t_one = (time.perf_counter() - t0) / a.reps
-        print(f"giant-sharded BSGS N={N} L0={a.L0} D={D} (G={G}, B={B}) over {world} ranks "
+        print(f"{a.mode}-sharded BSGS N={N} L0={a.L0} D={D} (G={G}, B={B}) over {world} ranks "
               f"({a.backend}): bit-exact vs one-GPU fused BSGS: {exact}; "
               f"sharded {1e3 * t_sh:.2f} ms/matvec, one GPU {1e3 * t_one:.2f} ms/matvec", flush=True)
     if rank == 0 and a.simulate_world:
@@ -105,8 +110,20 @@ def main():
             ctx.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.reps):
-                baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
-                ph.rescale_to_next(ctx, fd.bsgs_giant_partial(ph, ctx, baby, pts, G, D, grp, gk, zero))
+                if a.mode == "baby":   # rank 0's baby share, all groups' partial products, its giant groups
+                    bs = fd.baby_steps_share(G, W, 0)
+                    baby = [ct if b == 0 else ph.rotate(ctx, ct, b, gk) for b in bs]
+                    parts = ph.bsgs_inner_products(ctx, baby, [pts[g * G + b] if g * G + b < D else zero[0]
+                                                               for g in range(B) for b in bs], len(bs), B)
+                    zs, os_ = fd._select_plaintexts(ph, ctx, level)
+                    k = len(grp)
+                    sel = [os_ if b == j else zs for j in range(k) for b in range(k)]
+                    elts = [1] + [ph.get_elt_from_step(g * G, N) for g in grp[1:]]
+                    ph.rescale_to_next(ctx, ph.linear_transform(ctx, [parts[g] for g in grp], sel, k, elts, gk,
+                                                                rescale=False))
+                else:
+                    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+                    ph.rescale_to_next(ctx, fd.bsgs_giant_partial(ph, ctx, baby, pts, G, D, grp, gk, zero))
             ctx.synchronize()
             print(f"  per-rank compute at world {W} ({len(grp)} of {B} giant groups): "
                   f"{1e3 * (time.perf_counter() - t0) / a.reps:.2f} ms/matvec", flush=True)

@@ -237,8 +237,14 @@ class BlockRunner:
     steps (fhespear_dist.stage_groups / bsgs_giant_sharded); a stage with more projections than
     ranks is dealt."""
 
-    def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1, split=False, baby_mode="recompute"):
+    def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1, split=False, baby_mode="recompute",
+                 shard="giant"):
         self.srv, self.block, self.pre, self.dist, self.rank, self.world = srv, block, preencoded, dist, rank, world
+        if shard not in ("giant", "baby"):
+            raise ValueError(f"shard {shard!r}: 'giant' (baby steps replicated) or 'baby' (reduce-scatter)")
+        # latency mode's split of one projection over its rank group: its giant groups (every rank
+        # rotates all baby steps) or its baby steps (fhespear_dist.bsgs_baby_sharded)
+        self.shard = shard
         if baby_mode not in ("recompute", "broadcast"):
             raise ValueError(f"baby_mode {baby_mode!r}: 'recompute' or 'broadcast'")
         # baby steps of an input several ranks need: every rank computes them ("recompute"), or the
@@ -263,7 +269,10 @@ class BlockRunner:
                     pg = dist.new_group(ranks) if len(ranks) > 1 else None
                     lay.append((n, ranks, pg))
                     if rank in ranks:
-                        self.share[n] = fhespear_dist.giant_groups(srv.B, len(ranks), ranks.index(rank))
+                        self.share[n] = (fhespear_dist.giant_groups(srv.B, len(ranks), ranks.index(rank))
+                                         if shard == "giant" else
+                                         fhespear_dist.baby_sharded_rows(srv.G, srv.B, srv.D, len(ranks),
+                                                                         ranks.index(rank)))
                 self.layout[i] = lay
                 self.assign[i] = [n for n, ranks, _ in lay if rank in ranks]
             self.zero = srv.encoder.encode_double_vector_batch(srv.ctx, np.zeros((srv.G, srv.slots)), srv.diag_scale,
@@ -290,6 +299,8 @@ class BlockRunner:
         """diagonal indices this rank needs for `name` (its giant groups' share, or all D)"""
         if name not in self.share:
             return None
+        if self.shard == "baby":
+            return self.share[name]
         G, D = self.srv.G, self.srv.D
         return [g * G + b for g in self.share[name] for b in range(G) if g * G + b < D]
 
@@ -398,6 +409,12 @@ class BlockRunner:
         res = {}
         for n, ranks, pg in self.layout[idx]:
             if self.rank not in ranks:
+                continue
+            if self.shard == "baby" and len(ranks) > 1:   # no replicated baby rotations
+                out = fhespear_dist.bsgs_baby_sharded(ph, srv.ctx, cts[inputs[n][1]], self._pts(n), srv.G, srv.B,
+                                                      srv.D, srv.gk, self.zero[0], self.dist, dev, ranks=ranks, group=pg)
+                if out is not None:
+                    res[n] = out
                 continue
             if self.baby_mode == "broadcast" and len(ranks) > 1:
                 baby = self._shared_babies(cts[inputs[n][1]], ranks, pg)
@@ -548,7 +565,8 @@ def run_blocks(ph, args, dist=None, rank=0, world=1, device=0, log=print):
     t0 = time.perf_counter()
     srv = Server(ph, args.N, args.L0, args.P, args.D, device=device)
     runs = [BlockRunner(srv, b, args.preencoded, dist, rank, world, split=getattr(args, "split", False),
-                        baby_mode=getattr(args, "baby_mode", "recompute")) for b in blocks]
+                        baby_mode=getattr(args, "baby_mode", "recompute"), shard=getattr(args, "shard", "giant"))
+            for b in blocks]
     srv.ctx.synchronize()
     if rank == 0:
         log(f"setup (keys{', pre-encoded diagonals' if args.preencoded else ''}): {time.perf_counter() - t0:.2f} s")
@@ -590,6 +608,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--split", action="store_true",
                     help="latency mode: each stage's projections shard their giant steps over rank groups")
+    ap.add_argument("--shard", default="giant", choices=("giant", "baby"),
+                    help="latency mode's split of a projection: giant groups (baby steps replicated) or baby steps "
+                         "(reduce-scatter of every group's partial inner products)")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the process group even at world 1 (runs the exchange code on one GPU)")
     ap.add_argument("--baby-mode", default="recompute", choices=("recompute", "broadcast"),
