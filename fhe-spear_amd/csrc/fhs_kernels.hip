@@ -13,7 +13,7 @@
 #include "fhs_kernels.h"
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #ifndef FHS_KSIP_UNROLL
-#define FHS_KSIP_UNROLL 2   // digits of the key inner product unrolled together (2: 64 VGPRs, 8 waves/SIMD)
+#define FHS_KSIP_UNROLL 4   // digits of the key inner product unrolled together (4 since the buffer loads: profiles/r03/ab/ksip_ch_summary.txt)
 #endif
 #include "fhs_ntt.h"
 #include "fhs_buffer.h"
@@ -31,7 +31,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_MODUP_HALF 1       // k_modup_h: half-limb LDS, two workgroups per CU
 #define FHS_MODDOWN_HALF 1     // k_moddown_h: half-limb LDS
 #define FHS_INTT_HALF 1        // k_ks_intt_h: half-limb LDS inverse NTT
+#ifndef FHS_MODUPH_CH
 #define FHS_MODUPH_CH 2        // k_modup_h: coefficient pairs per conversion chunk
+#endif
 #define FHS_MODUPH_RL 3        // k_modup_h: radix (log2) of the NTT register passes
 #define FHS_MODUP_CH 4         // k_modup (full-limb form): coefficients per conversion chunk
 #define FHS_MODUP_RL 4         // k_modup (full-limb form): radix (log2) of the NTT register passes

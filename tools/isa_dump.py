@@ -13,7 +13,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "fhe-spear_amd", "lib", "libfhespear_hip.so")
+LIB = os.environ.get("FHS_ISA_LIB") or os.path.join(ROOT, "fhe-spear_amd", "lib", "libfhespear_hip.so")
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
