@@ -2278,6 +2278,55 @@ extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_cipherte
     return FHS_OK;
 }
 
+// The giant-step half of the fused BSGS alone: out = sum_j rot_{elts[j]}(inners[j]), every rotation's
+// key switch summed before one ModDown (k_giant_sum / k_giant_final), not rescaled.  elts[0] may be 1
+// (an unrotated term); otherwise a zero term takes group 0's place.  The baby-step-sharded latency mode
+// (fhespear_dist.bsgs_baby_sharded) finishes a rank's giant groups with it.
+extern "C" fhs_status fhs_bsgs_giant_steps(fhs_context* c, const fhs_ciphertext* const* inners, int k,
+                                           const uint64_t* elts, const fhs_galois_keys* gk, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!inners || !elts || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (k < 1 || k > 511) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: 1 <= k <= 511");
+    const int l = inners[0] ? inners[0]->l : 0, ci = inners[0] ? inners[0]->ci : 0;
+    for (int j = 0; j < k; ++j) {
+        if (!inners[j] || inners[j]->ncomp != 2 || inners[j]->l != l || inners[j]->ci != ci)
+            return fail(FHS_ERR_LEVEL, "bsgs_giant_steps: inner products must be 2-component at one chain index");
+        if (!scales_close(inners[j]->scale, inners[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_giant_steps: scales differ");
+        if ((elts[j] & 1) == 0 || elts[j] >= 2 * c->N) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: bad Galois element");
+        if (j > 0 && elts[j] == 1) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: only the first term may be unrotated");
+    }
+    const int pad = elts[0] == 1 ? 0 : 1, B = k + pad;   // group 0 = the unrotated term (or zero)
+    std::vector<uint64_t> ge(B, 1);
+    std::vector<const uint64_t*> keys(B, nullptr), akeys(B, nullptr);
+    for (int g = 1; g < B; ++g) {
+        ge[g] = elts[g - pad];
+        auto it = gk->keys.find(ge[g]);
+        if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "bsgs_giant_steps: galois key missing");
+        keys[g] = it->second;
+        akeys[g] = key_akey(c, it->second);
+    }
+    const size_t S = (size_t)l * c->N;
+    uint64_t *inner = nullptr, *ws = nullptr, *sum = nullptr;
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * B * 2 * S, &inner), "bsgs_giant_steps");
+    if (pad) HIPCHK(hipMemsetAsync(inner, 0, 16 * S, c->st), "bsgs_giant_steps");
+    for (int j = 0; j < k; ++j)
+        HIPCHK(hipMemcpyAsync(inner + (size_t)(j + pad) * 2 * S, inners[j]->d, 16 * S, hipMemcpyDeviceToDevice, c->st),
+               "bsgs_giant_steps");
+    const size_t wsb = std::max<size_t>(8, fhs::bsgs_workspace_bytes(c->T, B - 1, l));
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_WS, wsb, &ws), "bsgs_giant_steps");
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_SUM, 16 * S, &sum), "bsgs_giant_steps");
+    const fhs::KTimer* tm = c->timer_mask ? &c->ktimer : nullptr;
+    HIPCHK(fhs::launch_bsgs(c->T, nullptr, nullptr, 1, B, B, l, keys.data(), akeys.data(), ge.data(), inner, sum, ws, wsb,
+                            c->items_dev, c->stager, c->st, tm),
+           "bsgs_giant_steps");
+    fhs_ciphertext* r;
+    fhs_status s = new_ct(c, 2, ci, inners[0]->scale, &r);
+    if (s != FHS_OK) return s;
+    HIPCHK(hipMemcpyAsync(r->d, sum, 16 * S, hipMemcpyDeviceToDevice, c->st), "bsgs_giant_steps");
+    *out = r;
+    return FHS_OK;
+}
+
 extern "C" fhs_status fhs_linear_transform(fhs_context* c, const fhs_ciphertext* const* baby, int G,
                                            const fhs_plaintext* const* pts, int D, int B, const uint64_t* giant_elts,
                                            const fhs_galois_keys* gk, int rescale, fhs_ciphertext** out) {

@@ -85,7 +85,8 @@ size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l);
 // Hadamard + giant steps of the fused BSGS (fhs_kernels.hip launch_bsgs), enqueued on `st`.
 size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
 // giant_elts (host, B entries, may be null): Galois element of giant group g (g >= 1); null means
-// 5^(g G) mod 2N (the BSGS matvec of bg:464-485).  Group 0 is never rotated.
+// 5^(g G) mod 2N (the BSGS matvec of bg:464-485).  Group 0 is never rotated.  pts_dev null: no Hadamard, `inner`
+// already holds the B inner products ([g][2][l][N]; giant steps only).
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
                        u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,

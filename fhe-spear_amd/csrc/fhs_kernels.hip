@@ -1547,7 +1547,8 @@ hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, con
     return launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, g0, g1, D, l, inner, st);
 }
 
-// Hadamard (every giant group's inner product), then the giant steps: INTT + centred ModUp + NTT of
+// Hadamard (every giant group's inner product; skipped when pts_dev is null and `inner` already holds
+// them), then the giant steps: INTT + centred ModUp + NTT of
 // the B - 1 inner products (one ModUp each), key inner products with the automorphism applied on the
 // fly, special-limb INTT, the giant sum before ModDown (k_giant_sum) and one ModDown NTT per output
 // limb (k_giant_final).  One stream, serial: the limbs are those of the reference loop bg:464-485.
@@ -1586,10 +1587,13 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
         hipError_t e = upload_items(items, R, uniq, R, items_dev, sg, &it, &uq);
         if (e != hipSuccess) return e;
     }
-    FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-    hipError_t he = launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, 0, B, D, l, inner, st);
-    FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
-    if (he != hipSuccess) return he;
+    hipError_t he = hipSuccess;
+    if (pts_dev) {   // null: the B inner products are already in `inner` (giant steps only)
+        FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
+        he = launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, 0, B, D, l, inner, st);
+        FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
+        if (he != hipSuccess) return he;
+    }
     if (R <= 0) return hipMemcpyAsync(out, inner, 8 * 2 * S, hipMemcpyDeviceToDevice, st);
     if (!seal_orig.empty()) {
         he = seal_permute(T, seal_orig.data(), R, l, seal_perm, st);

@@ -248,21 +248,6 @@ def _reduce_scatter_mod(dist, parts, sizes, moduli_rows, group, host):
     return out
 
 
-_SELECT = {}
-
-
-def _select_plaintexts(ph, ctx, ci):
-    """The plaintexts 0 and 1 (all-ones NTT limbs: the constant polynomial 1) at chain index ci, scale 1."""
-    import numpy as np
-    key = (id(ctx), ci)
-    if key not in _SELECT or _SELECT[key][0] is not ctx:
-        l = ctx.L0 + 1 - ci
-        zero = ph.plaintext_from_numpy(ctx, np.zeros((l, ctx.N), dtype=np.uint64), ci, 1.0)
-        one = ph.plaintext_from_numpy(ctx, np.ones((l, ctx.N), dtype=np.uint64), ci, 1.0)
-        _SELECT[key] = (ctx, zero, one)
-    return _SELECT[key][1], _SELECT[key][2]
-
-
 def bsgs_baby_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, dist, device="cuda",
                       ranks=None, group=None):
     """One matvec with its BABY steps split over `ranks` (latency mode without replicated baby
@@ -270,7 +255,7 @@ def bsgs_baby_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, d
     library), forms the partial inner product of EVERY giant group over those b
     (ph.bsgs_inner_products), and a reduce-scatter (int64 RCCL sum + one reduction mod q_i, exact)
     hands each rank the full inner products of its giant groups (giant_groups).  The owner rotates
-    and sums them (ph.linear_transform with identity plaintexts: one giant step per owned group), the
+    and sums them (ph.bsgs_giant_steps: one key switch per owned group, summed before ModDown), the
     partial outputs are summed mod q_i on ranks[0] (modular_reduce_sum), which rescales.  Every term is
     an exact residue, so the result is limb-identical to ph.bsgs_multiply_accumulate on one GPU.
     `pts` maps a diagonal index to its plaintext and need only hold baby_sharded_rows of this rank;
@@ -303,16 +288,9 @@ def bsgs_baby_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, d
         mine = _reduce_scatter_mod(dist, parts, len(shares[idx]), rows, group, False)
     my_groups = shares[idx]
     inners = [from_buffer(ph, ctx, mine[j], 2, ci, scale) for j in range(len(my_groups))]
-    # giant steps of the owned groups: identity "diagonals" route inner_j to giant group j
-    zero_pt, one_pt = _select_plaintexts(ph, ctx, ci)
-    k = len(inners)
-    if my_groups[0] == 0:
-        elts = [1] + [ph.get_elt_from_step(g * G, ctx.N) for g in my_groups[1:]]
-        sel = [one_pt if b == j else zero_pt for j in range(k) for b in range(k)]
-    else:
-        elts = [1] + [ph.get_elt_from_step(g * G, ctx.N) for g in my_groups]
-        sel = [zero_pt] * k + [one_pt if b == j else zero_pt for j in range(k) for b in range(k)]
-    part = ph.linear_transform(ctx, inners, sel, k, elts, gk, rescale=False)
+    # giant steps of the owned groups (group 0 unrotated), summed before one ModDown
+    elts = [ph.get_elt_from_step(g * G, ctx.N) if g else 1 for g in my_groups]
+    part = ph.bsgs_giant_steps(ctx, inners, elts, gk)
     buf = torch.empty(W, dtype=torch.int64, device=device)
     to_buffer(ph, ctx, part, buf)
     if host:

@@ -150,6 +150,7 @@ _SIGS = {
     "fhs_bsgs_from_cpu": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u64p, C.c_int, C.c_int, C.c_int, C.c_double, _vp,
                                     C.POINTER(_vp)]),
     "fhs_bsgs_inner_products": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp)]),
+    "fhs_bsgs_giant_steps": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u64p, _vp, C.POINTER(_vp)]),
     "fhs_linear_transform": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.c_int, _u64p, _vp,
                                        C.c_int, C.POINTER(_vp)]),
     "fhs_multiply_const": (C.c_int, [_vp, _vp, C.c_double, C.c_double, C.POINTER(_vp)]),
@@ -782,6 +783,18 @@ def bsgs_inner_products(ctx, ct_baby, pts, G, B):
     hs = (_vp * B)()
     _check(_lib.fhs_bsgs_inner_products(ctx._h, bb, G, pp, B, hs), "bsgs_inner_products")
     return [ciphertext(ctx, _vp(hs[g])) for g in range(B)]
+
+
+def bsgs_giant_steps(ctx, inners, elts, gk):
+    """Extension: the giant-step half of bsgs_multiply_accumulate alone -- sum_j galois_{elts[j]}(inners[j])
+    with the key switches summed before one ModDown, not rescaled (fhs_bsgs_giant_steps).  Only elts[0]
+    may be 1 (an unrotated term)."""
+    k = len(inners)
+    if k != len(elts) or k < 1:
+        raise ValueError(f"bsgs_giant_steps: {k} inner products for {len(elts)} Galois elements")
+    hh = (_vp * k)(*[c._h for c in inners])
+    e, ep = _u64_arr(elts)
+    return _ct(ctx, _lib.fhs_bsgs_giant_steps, hh, k, ep, gk._h, what="bsgs_giant_steps")
 
 
 # ------------------------------------------------------------------ bootstrapping primitives

@@ -200,6 +200,12 @@ fhs_status fhs_linear_transform(fhs_context* ctx, const fhs_ciphertext* const* b
  * outs: B new ciphertexts. */
 fhs_status fhs_bsgs_inner_products(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
                                    const fhs_plaintext* const* pts, int B, fhs_ciphertext** outs);
+/* Extension (no reference symbol): the giant-step half of fhs_bsgs_multiply_accumulate (bg:478-483):
+ * out = sum_j rot_{elts[j]}(inners[j]) for k 2-component ciphertexts at one chain index and scale, the k
+ * key switches summed before one ModDown, NOT rescaled.  elts[0] may be 1 (unrotated term); no other.
+ * The baby-step-sharded latency mode finishes a rank's giant groups with it.  out: 1 new ciphertext. */
+fhs_status fhs_bsgs_giant_steps(fhs_context* ctx, const fhs_ciphertext* const* inners, int k, const uint64_t* elts,
+                                const fhs_galois_keys* gk, fhs_ciphertext** out);
 /* Extension (no reference symbol): bg:198-203 + bg:361-432 on the device -- the D diagonals of the
  * D x D row-major matrix M1 (complex: M1 + i M2; M2 = NULL for real), group g = k / G rolled by g G,
  * tiled to N/2 slots, encoded at `scale` / `chain_index`.  Limb-identical to encode_*_vector_batch

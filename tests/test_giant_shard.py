@@ -118,3 +118,41 @@ def test_modular_reduce_sum_exact_beyond_int64_bound():
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     assert "reduce exact: True" in out.stdout, out.stdout[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,first_unrotated", [(4096, True), (4096, False), (16384, False)])
+def test_bsgs_giant_steps_matches_oracle(require_gpu, N, first_unrotated):
+    """ph.bsgs_giant_steps (the baby-sharded mode's giant half, fhs_bsgs_giant_steps): the sum of the
+    rotated inner products, key switches summed before one ModDown, equals the oracle's sum of
+    individually key-switched rotations (bg:478-483) limb for limb -- with and without an unrotated
+    first term, and at N = 16384 (half-limb kernel forms)."""
+    import numpy as np
+    import pyPhantom as ph
+    from oracle.oracle import Oracle, galois_elt
+    L0, P, S = 6, 3, 31
+    steps = [0, 8, 16, 24] if first_unrotated else [8, 16, 24]
+    elts = [1 if s == 0 else galois_elt(s, N) for s in steps]
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(P)
+    parms.set_galois_elts(sorted(e for e in elts if e != 1))
+    primes = ph.create_coeff_modulus(N, [59] * (L0 + P))
+    parms.set_coeff_modulus(primes)
+    ctx = ph.context(parms)
+    sk = ph.secret_key(ctx, seed=S)
+    gk = sk.create_galois_keys(ctx)
+    o = Oracle(N, [int(q) for q in primes], P)
+    s = o.gen_secret(S)
+    rng = np.random.default_rng(N + len(steps))
+    cts = [o.encrypt_symmetric(S, j + 1, s, o.encode(rng.standard_normal(N // 2), 2.0 ** 40, L0))
+           for j in range(len(steps))]
+    got = ph.bsgs_giant_steps(ctx, [ph.ciphertext_from_numpy(ctx, c, 1, 2.0 ** 40) for c in cts], elts, gk)
+    want = None
+    for c, e in zip(cts, elts):
+        t = c if e == 1 else o.rotate_elt(c, o.gen_galois_key(S, s, e), e)
+        want = t if want is None else o.add(want, t)
+    assert got.chain_index() == 1 and got.scale() == 2.0 ** 40
+    assert np.array_equal(got.to_numpy(), want)
+    with pytest.raises(ValueError):
+        ph.bsgs_giant_steps(ctx, [ph.ciphertext_from_numpy(ctx, c, 1, 2.0 ** 40) for c in cts[:2]], [elts[-1], 1], gk)

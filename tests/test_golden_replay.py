@@ -121,3 +121,60 @@ def test_fully_encrypted_ffn_chain_bit_exact(ph):
     finally:
         fb.matmul = orig
     assert len(seen) == len(calls)
+
+
+@pytest.mark.gpu
+def test_client_aided_block_server_calls_half_limb_vs_oracle(ph):
+    """The same 8 server calls (bg:545-659 through tools/rwkv_block.py BlockRunner) at N = 16384, where
+    the GPU runs its half-limb NTT workgroup forms (k_ks_intt_h, k_modup_h, k_moddown_h) that the N=256
+    recordings never reach (VERDICT r2 missing #6): every projection's output is compared limb for limb
+    with the oracle's own baby steps (bg:215-220, one rotation at a time) and BSGS loop (bg:464-485) on
+    the same oracle-encrypted input and oracle-encoded diagonals.  L0 = 6 keeps the oracle fast; the
+    kernel forms depend on N only."""
+    import rwkv_block as rb
+    import fhespear_dist
+    from oracle.oracle import Oracle, galois_elt
+    N, L0, P, D, F, S = 16384, 6, 3, 32, 128, 77
+    srv = rb.Server(ph, N, L0, P, D, seed=S)
+    primes = [int(q) for q in ph.create_coeff_modulus(N, [59] * (L0 + P))]
+    o = Oracle(N, primes, P)
+    s = o.gen_secret(S)
+    G, B = srv.G, srv.B
+    baby_keys = {b: o.gen_galois_key(S, s, galois_elt(b, N)) for b in range(1, G)}
+    giant_keys = [None] + [o.gen_galois_key(S, s, galois_elt(g * G, N)) for g in range(1, B)]
+    block = rb.BlockWeights(np.random.default_rng(3), 0, D, F, 2)
+    run = rb.BlockRunner(srv, block, False)
+    run.pre = True
+    run.pts, opts = {}, {}
+    for name, (kind, ms) in run.mats.items():
+        rows = rb._diag_rows(ms[0], D, G, srv.slots)
+        if kind == "complex":
+            rows = rows + 1j * rb._diag_rows(ms[1], D, G, srv.slots)
+        opts[name] = [o.encode(r, srv.diag_scale, L0) for r in rows]
+        run.pts[name] = [ph.plaintext_from_numpy(srv.ctx, p, srv.level, srv.diag_scale) for p in opts[name]]
+    rng = np.random.default_rng(4)
+    inputs, counter = {}, 0
+
+    def enc(key, complex_):
+        nonlocal counter
+        if key not in inputs:
+            z = rng.standard_normal(D) + (1j * rng.standard_normal(D) if complex_ else 0)
+            pt = o.encode(np.tile(z, srv.slots // D), srv.scale, L0)
+            counter += 1
+            inputs[key] = o.encrypt_symmetric(S, counter, s, pt)
+        return ph.ciphertext_from_numpy(srv.ctx, inputs[key], srv.level, srv.scale), key
+    n_pairs = F // D // 2
+    stages = [{n: enc(n, False) for n in ("r", "k", "v")}, {"o": enc("o", False)},
+              {f"ffn_key_{p}": enc("x_k_ffn", False) for p in range(n_pairs)},
+              {f"ffn_val_{p}": enc(f"v{p}", True) for p in range(n_pairs)}]
+    assert [sorted(st) for st in stages] == [sorted(n) for n in fhespear_dist.RWKV_BLOCK_STAGES]
+    checked = 0
+    for idx, ins in enumerate(stages):
+        outs = run.stage(idx, ins)
+        for n, (_, key) in ins.items():
+            ct = inputs[key]
+            baby = [ct] + [o.rotate(ct, baby_keys[b], b) for b in range(1, G)]
+            want = o.bsgs_loop(baby, opts[n], giant_keys, G, B, D)
+            assert np.array_equal(outs[n].to_numpy(), want), f"projection {n}: limbs differ from the oracle"
+            checked += 1
+    assert checked == 8

@@ -115,12 +115,8 @@ def main():
                     baby = [ct if b == 0 else ph.rotate(ctx, ct, b, gk) for b in bs]
                     parts = ph.bsgs_inner_products(ctx, baby, [pts[g * G + b] if g * G + b < D else zero[0]
                                                                for g in range(B) for b in bs], len(bs), B)
-                    zs, os_ = fd._select_plaintexts(ph, ctx, level)
-                    k = len(grp)
-                    sel = [os_ if b == j else zs for j in range(k) for b in range(k)]
-                    elts = [1] + [ph.get_elt_from_step(g * G, N) for g in grp[1:]]
-                    ph.rescale_to_next(ctx, ph.linear_transform(ctx, [parts[g] for g in grp], sel, k, elts, gk,
-                                                                rescale=False))
+                    elts = [ph.get_elt_from_step(g * G, N) if g else 1 for g in grp]
+                    ph.rescale_to_next(ctx, ph.bsgs_giant_steps(ctx, [parts[g] for g in grp], elts, gk))
                 else:
                     baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
                     ph.rescale_to_next(ctx, fd.bsgs_giant_partial(ph, ctx, baby, pts, G, D, grp, gk, zero))
