@@ -2238,10 +2238,9 @@ extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_cip
 // The Hadamard half of the fused BSGS alone: outs[g] = sum_{b < G} baby[b] (.) pts[g G + b], g < B, not
 // rescaled (scale baby * pt).  Used by the baby-step-sharded latency mode (fhespear_dist.bsgs_baby_sharded):
 // a rank holding baby steps b in its share forms every giant group's partial inner product.
-extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_ciphertext* const* baby, int G,
-                                              const fhs_plaintext* const* pts, int B, fhs_ciphertext** outs) {
-    ENTER(c);
-    if (!pts || !outs || !baby) return fail(FHS_ERR_INVALID, "null argument");
+// inner products of the B groups into dst ([g][2][l][N] words, device memory), stream-ordered
+static fhs_status inner_products_core(fhs_context* c, const fhs_ciphertext* const* baby, int G,
+                                      const fhs_plaintext* const* pts, int B, uint64_t* dst) {
     if (G < 1 || G > 64 || B < 1) return fail(FHS_ERR_INVALID, "bsgs_inner_products: 1 <= G <= 64, B >= 1");
     const int D = B * G, ci = baby[0]->ci, l = baby[0]->l;
     if ((size_t)D + G > (size_t)fhs_context::kMaxPtrs) return fail(FHS_ERR_INVALID, "bsgs_inner_products: too many plaintexts");
@@ -2256,12 +2255,21 @@ extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_cipherte
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_inner_products: plaintext scales differ");
         ptrs[G + k] = pts[k]->d;
     }
-    const size_t S = (size_t)l * c->N;
     HIPCHK(stage_h2d(c, c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D)), "bsgs_inner_products");
     const uint64_t* const* dbaby = reinterpret_cast<const uint64_t* const*>(c->ptrs_dev);
+    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dbaby + G, G, 0, B, D, l, dst, c->st), "bsgs_inner_products");
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_ciphertext* const* baby, int G,
+                                              const fhs_plaintext* const* pts, int B, fhs_ciphertext** outs) {
+    ENTER(c);
+    if (!pts || !outs || !baby || !baby[0]) return fail(FHS_ERR_INVALID, "null argument");
+    const int ci = baby[0]->ci;
+    const size_t S = (size_t)baby[0]->l * c->N;
     uint64_t* inner = nullptr;
-    HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * B * 2 * S, &inner), "bsgs_inner_products");
-    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dbaby + G, G, 0, B, D, l, inner, c->st), "bsgs_inner_products");
+    HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * std::max(B, 1) * 2 * S, &inner), "bsgs_inner_products");
+    fhs_status cs = inner_products_core(c, baby, G, pts, B, inner);
+    if (cs != FHS_OK) return cs;
     std::vector<fhs_ciphertext*> made;
     for (int g = 0; g < B; ++g) {
         fhs_ciphertext* r;
@@ -2278,20 +2286,25 @@ extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_cipherte
     return FHS_OK;
 }
 
+// fhs_bsgs_inner_products into caller device memory (e.g. a torch buffer that a reduce-scatter then
+// sums): group g at dst + g 2 l N words, ordered on the context stream (fhs_context_stream).
+extern "C" fhs_status fhs_bsgs_inner_products_device(fhs_context* c, const fhs_ciphertext* const* baby, int G,
+                                                     const fhs_plaintext* const* pts, int B, uint64_t* dst) {
+    ENTER(c);
+    if (!pts || !dst || !baby || !baby[0]) return fail(FHS_ERR_INVALID, "null argument");
+    return inner_products_core(c, baby, G, pts, B, dst);
+}
+
 // The giant-step half of the fused BSGS alone: out = sum_j rot_{elts[j]}(inners[j]), every rotation's
 // key switch summed before one ModDown (k_giant_sum / k_giant_final), not rescaled.  elts[0] may be 1
 // (an unrotated term); otherwise a zero term takes group 0's place.  The baby-step-sharded latency mode
 // (fhespear_dist.bsgs_baby_sharded) finishes a rank's giant groups with it.
-extern "C" fhs_status fhs_bsgs_giant_steps(fhs_context* c, const fhs_ciphertext* const* inners, int k,
-                                           const uint64_t* elts, const fhs_galois_keys* gk, fhs_ciphertext** out) {
-    ENTER(c);
-    if (!inners || !elts || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
-    if (k < 1 || k > 511) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: 1 <= k <= 511");
-    const int l = inners[0] ? inners[0]->l : 0, ci = inners[0] ? inners[0]->ci : 0;
+// src(j): device address of term j's 2 l N words
+template <class Src>
+static fhs_status giant_steps_core(fhs_context* c, Src src, int k, int ci, double scale, const uint64_t* elts,
+                                   const fhs_galois_keys* gk, fhs_ciphertext** out) {
+    const int l = c->L0 + 1 - ci;
     for (int j = 0; j < k; ++j) {
-        if (!inners[j] || inners[j]->ncomp != 2 || inners[j]->l != l || inners[j]->ci != ci)
-            return fail(FHS_ERR_LEVEL, "bsgs_giant_steps: inner products must be 2-component at one chain index");
-        if (!scales_close(inners[j]->scale, inners[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_giant_steps: scales differ");
         if ((elts[j] & 1) == 0 || elts[j] >= 2 * c->N) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: bad Galois element");
         if (j > 0 && elts[j] == 1) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: only the first term may be unrotated");
     }
@@ -2310,7 +2323,7 @@ extern "C" fhs_status fhs_bsgs_giant_steps(fhs_context* c, const fhs_ciphertext*
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_INNER, 8ull * B * 2 * S, &inner), "bsgs_giant_steps");
     if (pad) HIPCHK(hipMemsetAsync(inner, 0, 16 * S, c->st), "bsgs_giant_steps");
     for (int j = 0; j < k; ++j)
-        HIPCHK(hipMemcpyAsync(inner + (size_t)(j + pad) * 2 * S, inners[j]->d, 16 * S, hipMemcpyDeviceToDevice, c->st),
+        HIPCHK(hipMemcpyAsync(inner + (size_t)(j + pad) * 2 * S, src(j), 16 * S, hipMemcpyDeviceToDevice, c->st),
                "bsgs_giant_steps");
     const size_t wsb = std::max<size_t>(8, fhs::bsgs_workspace_bytes(c->T, B - 1, l));
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_WS, wsb, &ws), "bsgs_giant_steps");
@@ -2320,11 +2333,36 @@ extern "C" fhs_status fhs_bsgs_giant_steps(fhs_context* c, const fhs_ciphertext*
                             c->items_dev, c->stager, c->st, tm),
            "bsgs_giant_steps");
     fhs_ciphertext* r;
-    fhs_status s = new_ct(c, 2, ci, inners[0]->scale, &r);
+    fhs_status s = new_ct(c, 2, ci, scale, &r);
     if (s != FHS_OK) return s;
     HIPCHK(hipMemcpyAsync(r->d, sum, 16 * S, hipMemcpyDeviceToDevice, c->st), "bsgs_giant_steps");
     *out = r;
     return FHS_OK;
+}
+extern "C" fhs_status fhs_bsgs_giant_steps(fhs_context* c, const fhs_ciphertext* const* inners, int k,
+                                           const uint64_t* elts, const fhs_galois_keys* gk, fhs_ciphertext** out) {
+    ENTER(c);
+    if (!inners || !elts || !gk || !out || k < 1 || !inners[0]) return fail(FHS_ERR_INVALID, "null argument");
+    if (k > 511) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: 1 <= k <= 511");
+    const int l = inners[0]->l, ci = inners[0]->ci;
+    for (int j = 0; j < k; ++j) {
+        if (!inners[j] || inners[j]->ncomp != 2 || inners[j]->l != l || inners[j]->ci != ci)
+            return fail(FHS_ERR_LEVEL, "bsgs_giant_steps: inner products must be 2-component at one chain index");
+        if (!scales_close(inners[j]->scale, inners[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_giant_steps: scales differ");
+    }
+    return giant_steps_core(c, [&](int j) { return inners[j]->d; }, k, ci, inners[0]->scale, elts, gk, out);
+}
+// the same over k terms laid out contiguously in caller device memory (term j at src + j 2 l N words,
+// l = L0 + 1 - chain_index), e.g. the slice a reduce-scatter handed this rank
+extern "C" fhs_status fhs_bsgs_giant_steps_device(fhs_context* c, const uint64_t* src, int k, int chain_index,
+                                                  double scale, const uint64_t* elts, const fhs_galois_keys* gk,
+                                                  fhs_ciphertext** out) {
+    ENTER(c);
+    if (!src || !elts || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    if (k < 1 || k > 511) return fail(FHS_ERR_INVALID, "bsgs_giant_steps: 1 <= k <= 511");
+    if (chain_index < 1 || chain_index > c->L0) return fail(FHS_ERR_LEVEL, "bsgs_giant_steps: bad chain index");
+    const size_t W = 2 * (size_t)(c->L0 + 1 - chain_index) * c->N;
+    return giant_steps_core(c, [&](int j) { return src + (size_t)j * W; }, k, chain_index, scale, elts, gk, out);
 }
 
 extern "C" fhs_status fhs_linear_transform(fhs_context* c, const fhs_ciphertext* const* baby, int G,

@@ -248,58 +248,151 @@ def _reduce_scatter_mod(dist, parts, sizes, moduli_rows, group, host):
     return out
 
 
-def bsgs_baby_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, dist, device="cuda",
-                      ranks=None, group=None):
-    """One matvec with its BABY steps split over `ranks` (latency mode without replicated baby
-    rotations).  Rank r rotates the input by its share of b (baby_steps_share; hoisted inside the
-    library), forms the partial inner product of EVERY giant group over those b
-    (ph.bsgs_inner_products), and a reduce-scatter (int64 RCCL sum + one reduction mod q_i, exact)
-    hands each rank the full inner products of its giant groups (giant_groups).  The owner rotates
-    and sums them (ph.bsgs_giant_steps: one key switch per owned group, summed before ModDown), the
-    partial outputs are summed mod q_i on ranks[0] (modular_reduce_sum), which rescales.  Every term is
-    an exact residue, so the result is limb-identical to ph.bsgs_multiply_accumulate on one GPU.
-    `pts` maps a diagonal index to its plaintext and need only hold baby_sharded_rows of this rank;
-    zero_diag: an encoding of 0 at the diagonals' level and scale (pads the short last group)."""
+def _rows_tensor(rows, device):
+    import torch
+    return torch.as_tensor([int(q) for q in rows], dtype=torch.int64, device=device).view(-1, 1)
+
+
+def grid_shape(world: int, rb: int):
+    """Rank index idx of a world = rb x rg grid -> (baby share i = idx % rb, giant column j = idx // rb)."""
+    if rb < 1 or world % rb:
+        raise ValueError(f"grid: {world} ranks do not split into {rb} baby shares")
+    return rb, world // rb
+
+
+def grid_rb(R: int) -> int:
+    """Baby shares of the grid for a projection sharded over R ranks (BlockRunner shard="grid").  Per-rank
+    compute measured alone on one MI355X at cfg2 (DESIGN.md §6, profiles/r03/grid_shard_cfg2_projection.log)
+    plus the reduce-scatter's xGMI time at ~64 GB/s per link and direction ((rb - 1)/rb x |column| x 9.4 MB
+    per rank, spread over the rb - 1 peers' direct links): at 2-4 ranks the transfer outweighs the baby
+    rotations it saves (2x1 4.5 + ~3.3 ms vs 1x2 5.0 ms; 2x2 3.0 + ~1.7 vs 1x4 3.5), at 8 ranks sharding
+    all baby steps wins (8x1 1.7 + ~0.8 ms vs 1x8 2.7 ms, 4x2 1.8 + ~0.8)."""
+    return R if R >= 8 else 1
+
+
+def grid_groups(dist, ranks, rb: int):
+    """The process groups of the grid's giant columns (the rb ranks that reduce-scatter one column's
+    partial inner products).  Every process of the default group must call this with the same
+    arguments (torch.distributed.new_group is collective); returns {column: group}."""
+    ranks = list(ranks)
+    rb, rg = grid_shape(len(ranks), rb)
+    return {j: dist.new_group(ranks=ranks[j * rb:(j + 1) * rb]) for j in range(rg)} if rb > 1 else {}
+
+
+def bsgs_grid_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, dist, rb: int, device="cuda",
+                      ranks=None, group=None, col_groups=None, timings=None, sim_grid=None):
+    """One matvec over R = rb x rg ranks (latency mode, SURVEY.md §8e(2)): the B giant groups are split
+    into rg contiguous columns (giant_groups) and the G baby steps into rb shares (baby_steps_share).
+    Rank (i, j) rotates the input by its baby share (hoisted inside the library), forms the partial
+    inner products of column j's groups over that share (ph.bsgs_inner_products), the rb ranks of
+    column j reduce-scatter them (int64 RCCL sum + one reduction mod q_i, exact for rb <= 15) so each
+    holds the full inner products of its slice of the column, and key-switches and sums only those
+    (ph.bsgs_giant_steps: one key switch per group, summed before one ModDown).  The partial outputs
+    are summed mod q_i on ranks[0] (modular_reduce_sum), which rescales.  Every term is an exact
+    residue, so the result is limb-identical to ph.bsgs_multiply_accumulate on one GPU.
+    rb = 1 is giant-step sharding (every rank rotates all G baby steps, no reduce-scatter); rb = R is
+    baby-step sharding (one column); in between trades the replicated baby rotations against the
+    reduce-scatter volume ((rb - 1) / rb x |column| x 2 l N x 8 bytes per rank).
+    `pts` maps a diagonal index to its plaintext and need only hold grid_rows of this rank;
+    zero_diag: an encoding of 0 at the diagonals' level and scale (pads the short last group);
+    col_groups: grid_groups(dist, ranks, rb) (made here when None -- collective over all ranks);
+    timings: optional dict that receives per-phase seconds (device-synchronised; diagnostics);
+    sim_grid = (rb, rg) (diagnostics, one process): run rank (0, 0)'s share of that grid alone, the two
+    collectives replaced by their local part (the mod-q reduction of this rank's slice, no transfer)."""
+    import time
     import torch
     me = dist.get_rank()
     ranks = list(range(dist.get_world_size())) if ranks is None else list(ranks)
     R, idx = len(ranks), ranks.index(me)
-    host = dist.get_backend(group) == "gloo"
-    bs = baby_steps_share(G, R, idx)
-    baby = [ct if b == 0 else ph.rotate(ctx, ct, b, gk) for b in bs]
-    flat = [pts[g * G + b] if g * G + b < D else zero_diag for g in range(B) for b in bs]
-    partial = ph.bsgs_inner_products(ctx, baby, flat, len(bs), B)
-    ci, l = partial[0].chain_index(), partial[0].coeff_modulus_size()
-    scale = partial[0].scale()
-    W = 2 * l * ctx.N
-    shares = [giant_groups(B, R, r) for r in range(R)]
-    kmax = max(len(s) for s in shares)
-    parts = torch.zeros((R, kmax, W), dtype=torch.int64, device=device)
-    for r, s in enumerate(shares):
-        for j, g in enumerate(s):
-            to_buffer(ph, ctx, partial[g], parts[r, j])
-    del partial
-    rows = [int(q) for q in ctx.primes[:l]] * 2
-    if host:
-        h = parts.cpu()
-        mine = _reduce_scatter_mod(dist, h, len(shares[idx]), rows, group, True)
-        mine = mine.to(device) if mine is not None else None
+    if sim_grid is not None:
+        (rb, rg), idx, ranks = sim_grid, 0, [me]
     else:
-        mine = _reduce_scatter_mod(dist, parts, len(shares[idx]), rows, group, False)
-    my_groups = shares[idx]
-    inners = [from_buffer(ph, ctx, mine[j], 2, ci, scale) for j in range(len(my_groups))]
-    # giant steps of the owned groups (group 0 unrotated), summed before one ModDown
+        rb, rg = grid_shape(R, rb)
+    i, j = idx % rb, idx // rb
+    host = dist.get_backend(group) == "gloo"
+    if col_groups is None and sim_grid is None:
+        col_groups = grid_groups(dist, ranks, rb)
+    t0 = [time.perf_counter()]
+
+    def mark(name):
+        if timings is not None:
+            ctx.synchronize()
+            torch.cuda.synchronize(device)
+            t = time.perf_counter()
+            timings[name] = timings.get(name, 0.0) + t - t0[0]
+            t0[0] = t
+    col = giant_groups(B, rg, j)
+    shares = column_shares(len(col), rb)            # positions in col, contiguous: slot = position
+    my_groups = [col[x] for x in shares[i]]
+    bs = baby_steps_share(G, rb, i)
+    baby = [ct if b == 0 else ph.rotate(ctx, ct, b, gk) for b in bs]
+    flat = [pts[g * G + b] if g * G + b < D else zero_diag for g in col for b in bs]
+    ci, l = ct.chain_index(), ct.coeff_modulus_size()
+    scale = ct.scale() * flat[0].scale()
+    W = 2 * l * ctx.N
+    rows = [int(q) for q in ctx.primes[:l]] * 2
     elts = [ph.get_elt_from_step(g * G, ctx.N) if g else 1 for g in my_groups]
-    part = ph.bsgs_giant_steps(ctx, inners, elts, gk)
+    if rb == 1:
+        partial = ph.bsgs_inner_products(ctx, baby, flat, len(bs), len(col))
+        del baby
+        mark("baby+inner")
+        part = ph.bsgs_giant_steps(ctx, partial, elts, gk)
+        del partial
+    else:
+        kmax = len(shares[0])
+        parts = torch.empty((rb * kmax, W), dtype=torch.int64, device=device)
+        if rb * kmax > len(col):
+            parts[len(col):].zero_()
+        cur, lib = torch.cuda.current_stream(parts.device), lib_stream(ph, ctx)
+        _order(cur, lib)                             # the buffer's previous users before the library writes
+        ph.bsgs_inner_products_to_device(ctx, baby, flat, len(bs), len(col), parts.data_ptr())
+        _order(lib, cur)
+        del baby
+        mark("baby+inner")
+        if sim_grid is not None:   # one contribution: only the local mod-q reduction of this rank's slice
+            mine = parts[:kmax]
+            mine.view(kmax, len(rows), -1).remainder_(_rows_tensor(rows, device))
+        elif host:
+            mine = _reduce_scatter_mod(dist, parts.view(rb, kmax, W).cpu(), len(shares[i]), rows, col_groups[j],
+                                       True).to(device)
+        else:
+            mine = _reduce_scatter_mod(dist, parts.view(rb, kmax, W), len(shares[i]), rows, col_groups[j], False)
+        mark("reduce_scatter")
+        _order(cur, lib)
+        part = ph.bsgs_giant_steps_from_device(ctx, mine.data_ptr(), len(my_groups), ci, scale, elts, gk)
+        _order(lib, cur)                             # torch may reuse `mine` only after the library read it
+        del mine, parts
+    mark("giant")
     buf = torch.empty(W, dtype=torch.int64, device=device)
     to_buffer(ph, ctx, part, buf)
-    if host:
+    if sim_grid is not None:
+        buf.view(len(rows), -1).remainder_(_rows_tensor(rows, device))
+    elif host:
         h = buf.cpu()
         modular_reduce_sum(dist, h, rows, root=ranks[0], group=group)
         buf.copy_(h)
     else:
         modular_reduce_sum(dist, buf, rows, root=ranks[0], group=group)
+    mark("reduce")
     if me != ranks[0]:
         return None
     total = from_buffer(ph, ctx, buf, 2, ci, part.scale())
-    return ph.rescale_to_next(ctx, total)
+    out = ph.rescale_to_next(ctx, total)
+    mark("rescale")
+    return out
+
+
+def grid_rows(G: int, B: int, D: int, world: int, rb: int, rank: int) -> list[int]:
+    """Diagonal indices rank index `rank` of an rb x (world / rb) grid needs: its baby share's column of
+    each giant group of its column."""
+    rb, rg = grid_shape(world, rb)
+    return [g * G + b for g in giant_groups(B, rg, rank // rb) for b in baby_steps_share(G, rb, rank % rb)
+            if g * G + b < D]
+
+
+def bsgs_baby_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, dist, device="cuda",
+                      ranks=None, group=None, col_groups=None, timings=None):
+    """Baby-step sharding (VERDICT r2 #7): bsgs_grid_sharded with rb = R (one giant column)."""
+    R = dist.get_world_size() if ranks is None else len(ranks)
+    return bsgs_grid_sharded(ph, ctx, ct, pts, G, B, D, gk, zero_diag, dist, R, device, ranks, group,
+                             col_groups if col_groups is not None else {0: group}, timings)

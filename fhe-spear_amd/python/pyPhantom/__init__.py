@@ -151,6 +151,8 @@ _SIGS = {
                                     C.POINTER(_vp)]),
     "fhs_bsgs_inner_products": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.POINTER(_vp)]),
     "fhs_bsgs_giant_steps": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, _u64p, _vp, C.POINTER(_vp)]),
+    "fhs_bsgs_inner_products_device": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, _vp]),
+    "fhs_bsgs_giant_steps_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_double, _u64p, _vp, C.POINTER(_vp)]),
     "fhs_linear_transform": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.POINTER(_vp), C.c_int, C.c_int, _u64p, _vp,
                                        C.c_int, C.POINTER(_vp)]),
     "fhs_multiply_const": (C.c_int, [_vp, _vp, C.c_double, C.c_double, C.POINTER(_vp)]),
@@ -783,6 +785,27 @@ def bsgs_inner_products(ctx, ct_baby, pts, G, B):
     hs = (_vp * B)()
     _check(_lib.fhs_bsgs_inner_products(ctx._h, bb, G, pp, B, hs), "bsgs_inner_products")
     return [ciphertext(ctx, _vp(hs[g])) for g in range(B)]
+
+
+def bsgs_inner_products_to_device(ctx, ct_baby, pts, G, B, dst_ptr):
+    """Extension: bsgs_inner_products written to caller device memory (group g at dst_ptr + g 2 l N
+    words), ordered on the context stream (fhs_bsgs_inner_products_device)."""
+    G, B = int(G), int(B)
+    if len(pts) != G * B:
+        raise ValueError(f"bsgs_inner_products_to_device: {len(pts)} plaintexts for G={G}, B={B}")
+    bb = (_vp * G)(*[c._h for c in ct_baby[:G]])
+    pp = (_vp * (G * B))(*[p._h for p in pts])
+    _check(_lib.fhs_bsgs_inner_products_device(ctx._h, bb, G, pp, B, _vp(int(dst_ptr))), "bsgs_inner_products_to_device")
+
+
+def bsgs_giant_steps_from_device(ctx, src_ptr, k, chain_index, scale, elts, gk):
+    """Extension: bsgs_giant_steps over k terms in caller device memory (term j at src_ptr + j 2 l N
+    words), ordered on the context stream (fhs_bsgs_giant_steps_device)."""
+    if len(elts) != int(k):
+        raise ValueError(f"bsgs_giant_steps_from_device: {k} terms for {len(elts)} Galois elements")
+    e, ep = _u64_arr(elts)
+    return _ct(ctx, _lib.fhs_bsgs_giant_steps_device, _vp(int(src_ptr)), int(k), int(chain_index), float(scale), ep,
+               gk._h, what="bsgs_giant_steps_from_device")
 
 
 def bsgs_giant_steps(ctx, inners, elts, gk):

@@ -206,6 +206,14 @@ fhs_status fhs_bsgs_inner_products(fhs_context* ctx, const fhs_ciphertext* const
  * The baby-step-sharded latency mode finishes a rank's giant groups with it.  out: 1 new ciphertext. */
 fhs_status fhs_bsgs_giant_steps(fhs_context* ctx, const fhs_ciphertext* const* inners, int k, const uint64_t* elts,
                                 const fhs_galois_keys* gk, fhs_ciphertext** out);
+/* Extensions (no reference symbol): the two halves over caller device memory, for the grid-sharded
+ * latency mode's reduce-scatter buffers -- fhs_bsgs_inner_products writing group g at dst + g 2 l N words,
+ * and fhs_bsgs_giant_steps reading term j at src + j 2 l N words (l = L0 + 1 - chain_index).  Both are
+ * ordered on the context's stream (fhs_context_stream); the caller orders its own streams around them. */
+fhs_status fhs_bsgs_inner_products_device(fhs_context* ctx, const fhs_ciphertext* const* baby, int G,
+                                          const fhs_plaintext* const* pts, int B, uint64_t* dst);
+fhs_status fhs_bsgs_giant_steps_device(fhs_context* ctx, const uint64_t* src, int k, int chain_index, double scale,
+                                       const uint64_t* elts, const fhs_galois_keys* gk, fhs_ciphertext** out);
 /* Extension (no reference symbol): bg:198-203 + bg:361-432 on the device -- the D diagonals of the
  * D x D row-major matrix M1 (complex: M1 + i M2; M2 = NULL for real), group g = k / G rolled by g G,
  * tiled to N/2 slots, encoded at `scale` / `chain_index`.  Limb-identical to encode_*_vector_batch

@@ -71,6 +71,23 @@ def test_baby_sharded_bsgs_bit_exact(require_gpu, world, D):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world,rb,D", [(4, 2, 256), (6, 3, 200), (4, 1, 200)])
+def test_grid_sharded_bsgs_bit_exact(require_gpu, world, rb, D):
+    """Baby x giant grid (fhespear_dist.bsgs_grid_sharded): rb baby shares x world/rb giant columns,
+    reduce-scatter inside each column's process group, giant steps of each rank's slice, modular sum
+    on the root -- limb-identical to the one-GPU fused BSGS (rb = 1: giant-step sharding through the
+    inner-products / giant-steps entries).  `world` ranks share one GPU (gloo)."""
+    env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(29621 + world + 10 * rb), str(REPO / "tools" / "giant_shard.py"),
+           "--backend", "gloo", "--mode", "grid", "--rb", str(rb), "--N", "4096", "--L0", "6", "--P", "3", "--D", str(D),
+           "--reps", "1"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    assert re.search(r"bit-exact vs one-GPU fused BSGS: True", out.stdout), out.stdout[-2000:]
+
+
+@pytest.mark.gpu
 def test_baby_sharded_bsgs_over_rccl_world1(require_gpu):
     """bsgs_baby_sharded through RCCL at world 1 (reduce_scatter_tensor + int64 reduce + event-ordered
     copies), bit-exact vs the fused BSGS."""
@@ -91,6 +108,19 @@ def test_baby_steps_share_partition(G, world):
     D = 45 * G - 3                          # short last giant group
     rows = [set(fd.baby_sharded_rows(G, 45, D, world, r)) for r in range(world)]
     assert sorted(k for r in rows for k in r) == list(range(D))
+
+
+@pytest.mark.parametrize("world,rb", [(8, 2), (8, 4), (6, 3), (4, 1), (3, 3)])
+def test_grid_rows_partition(world, rb):
+    """Every diagonal is needed by exactly one rank of an rb x rg grid, and a rank's rows are its baby
+    share's columns of its giant column's groups."""
+    G, B = 46, 45
+    D = B * G - 3
+    rows = [fd.grid_rows(G, B, D, world, rb, r) for r in range(world)]
+    assert sorted(k for r in rows for k in r) == list(range(D))
+    assert fd.grid_rows(G, B, D, world, world, 1) == fd.baby_sharded_rows(G, B, D, world, 1)
+    with pytest.raises(ValueError):
+        fd.grid_shape(world, world + 1)
 
 
 @pytest.mark.gpu

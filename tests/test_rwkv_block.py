@@ -145,6 +145,17 @@ def test_block_over_ranks_baby_sharded(require_gpu, world):
 
 
 @pytest.mark.gpu
+def test_block_over_ranks_grid_sharded(require_gpu):
+    """Latency mode on a baby x giant grid (BlockRunner shard="grid", rb=2): at world 4 the o projection
+    runs on a 2 x 2 grid (column process groups, reduce-scatter inside each), each FFN pair's 2-rank group
+    as a 2 x 1 grid (baby shares only), the 1-rank groups whole -- the same decrypted block output as one
+    rank, bit for bit."""
+    err, digest = _run_block_tool(4, extra=["--split", "--shard", "grid", "--rb", "2"], port=29581)
+    assert err < 1e-4
+    assert digest == _one_rank_digest()
+
+
+@pytest.mark.gpu
 def test_block_exchange_over_rccl_world1(require_gpu):
     """The real transport: backend nccl (RCCL) at world 1 with the process group forced on, so the
     input broadcast, the output gather and the event ordering between the library stream and torch's

@@ -30,11 +30,16 @@ def main():
     ap.add_argument("--D", type=int, default=2048)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
-    ap.add_argument("--mode", default="giant", choices=("giant", "baby"),
-                    help="shard the giant groups (baby steps replicated) or the baby steps (reduce-scatter "
-                         "of every group's partial inner products, fhespear_dist.bsgs_baby_sharded)")
+    ap.add_argument("--mode", default="giant", choices=("giant", "baby", "grid"),
+                    help="shard the giant groups (baby steps replicated), the baby steps (reduce-scatter "
+                         "of every group's partial inner products, fhespear_dist.bsgs_baby_sharded), or both "
+                         "(an rb x rg grid, fhespear_dist.bsgs_grid_sharded)")
+    ap.add_argument("--rb", type=int, default=1, help="grid mode: baby-step shares (divides the world size)")
     ap.add_argument("--simulate-world", type=int, nargs="*", default=[],
                     help="also time one rank's share of the compute at these world sizes (on this GPU alone)")
+    ap.add_argument("--simulate-grid", nargs="*", default=[],
+                    help="also time one rank's compute on rb x rg grids given as 'rbxrg' (e.g. 2x4), with its "
+                         "phases; the reduce-scatter then runs on a 1-rank group (a copy)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -72,12 +77,16 @@ def main():
     def sharded():
         if a.mode == "baby":
             return fd.bsgs_baby_sharded(ph, ctx, ct, pts, G, B, D, gk, zero[0], dist, dev)
+        if a.mode == "grid":
+            return fd.bsgs_grid_sharded(ph, ctx, ct, pts, G, B, D, gk, zero[0], dist, a.rb, dev, col_groups=cols)
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         return fd.bsgs_giant_sharded(ph, ctx, baby, pts, G, B, D, gk, zero, dist, dev)
 
     def barrier():
         ctx.synchronize()
         dist.barrier()
+
+    cols = fd.grid_groups(dist, range(world), a.rb) if a.mode == "grid" else None
 
     y = sharded()
     exact = None
@@ -123,6 +132,22 @@ def main():
             ctx.synchronize()
             print(f"  per-rank compute at world {W} ({len(grp)} of {B} giant groups): "
                   f"{1e3 * (time.perf_counter() - t0) / a.reps:.2f} ms/matvec", flush=True)
+    if rank == 0 and a.simulate_grid:
+        # rank (0, 0)'s share on an rb x rg grid: its baby share, the partial inner products of its
+        # column, the giant steps of its slice, the final reduce and the root's rescale.  Alone on this
+        # GPU the two collectives keep their local part (the staging copies and the mod-q reduction of
+        # this rank's slice) without the xGMI transfer itself.
+        for spec in a.simulate_grid:
+            rb, rg = (int(v) for v in spec.lower().split("x"))
+            tm = {}
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                fd.bsgs_grid_sharded(ph, ctx, ct, pts, G, B, D, gk, zero[0], dist, rb, dev, timings=tm,
+                                     sim_grid=(rb, rg))
+            ctx.synchronize()
+            dt = (time.perf_counter() - t0) / a.reps
+            print(f"  grid {rb}x{rg} rank (0,0): {1e3 * dt:.2f} ms/matvec; phases (ms) " +
+                  ", ".join(f"{k} {1e3 * v / a.reps:.2f}" for k, v in tm.items()), flush=True)
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0 and not exact:

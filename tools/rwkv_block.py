@@ -238,12 +238,13 @@ class BlockRunner:
     ranks is dealt."""
 
     def __init__(self, srv, block, preencoded, dist=None, rank=0, world=1, split=False, baby_mode="recompute",
-                 shard="giant"):
+                 shard="giant", rb=None):
         self.srv, self.block, self.pre, self.dist, self.rank, self.world = srv, block, preencoded, dist, rank, world
-        if shard not in ("giant", "baby"):
-            raise ValueError(f"shard {shard!r}: 'giant' (baby steps replicated) or 'baby' (reduce-scatter)")
+        if shard not in ("giant", "baby", "grid"):
+            raise ValueError(f"shard {shard!r}: 'giant' (baby steps replicated), 'baby' (reduce-scatter) or 'grid'")
         # latency mode's split of one projection over its rank group: its giant groups (every rank
-        # rotates all baby steps) or its baby steps (fhespear_dist.bsgs_baby_sharded)
+        # rotates all baby steps), its baby steps (fhespear_dist.bsgs_baby_sharded) or both
+        # (fhespear_dist.bsgs_grid_sharded, rb = fhespear_dist.grid_rb(group size) baby shares)
         self.shard = shard
         if baby_mode not in ("recompute", "broadcast"):
             raise ValueError(f"baby_mode {baby_mode!r}: 'recompute' or 'broadcast'")
@@ -259,6 +260,7 @@ class BlockRunner:
         # latency mode: per stage, [(projection, ranks, process group)] or None (dealt)
         self.layout = [None] * len(fhespear_dist.RWKV_BLOCK_STAGES)
         self.share = {}                      # projection -> giant groups this rank computes
+        self.grid = {}                       # projection -> (rb, column process groups) in grid mode
         if split and dist is not None:
             for i, names in enumerate(fhespear_dist.RWKV_BLOCK_STAGES):
                 groups = fhespear_dist.stage_groups(len(names), world)
@@ -268,11 +270,19 @@ class BlockRunner:
                 for n, ranks in zip(names, groups):   # every rank creates every group, same order
                     pg = dist.new_group(ranks) if len(ranks) > 1 else None
                     lay.append((n, ranks, pg))
+                    rb_n = None
+                    if shard == "grid":   # baby shares: the caller's, when it divides the group, else the model's
+                        rb_n = rb if rb and len(ranks) % rb == 0 else fhespear_dist.grid_rb(len(ranks))
+                    if rb_n is not None and len(ranks) > 1:
+                        self.grid[n] = (rb_n, fhespear_dist.grid_groups(dist, ranks, rb_n))
                     if rank in ranks:
-                        self.share[n] = (fhespear_dist.giant_groups(srv.B, len(ranks), ranks.index(rank))
-                                         if shard == "giant" else
-                                         fhespear_dist.baby_sharded_rows(srv.G, srv.B, srv.D, len(ranks),
-                                                                         ranks.index(rank)))
+                        R, me = len(ranks), ranks.index(rank)
+                        if shard == "giant":
+                            self.share[n] = fhespear_dist.giant_groups(srv.B, R, me)
+                        elif shard == "baby":
+                            self.share[n] = fhespear_dist.baby_sharded_rows(srv.G, srv.B, srv.D, R, me)
+                        else:
+                            self.share[n] = fhespear_dist.grid_rows(srv.G, srv.B, srv.D, R, rb_n, me)
                 self.layout[i] = lay
                 self.assign[i] = [n for n, ranks, _ in lay if rank in ranks]
             self.zero = srv.encoder.encode_double_vector_batch(srv.ctx, np.zeros((srv.G, srv.slots)), srv.diag_scale,
@@ -299,7 +309,7 @@ class BlockRunner:
         """diagonal indices this rank needs for `name` (its giant groups' share, or all D)"""
         if name not in self.share:
             return None
-        if self.shard == "baby":
+        if self.shard != "giant":
             return self.share[name]
         G, D = self.srv.G, self.srv.D
         return [g * G + b for g in self.share[name] for b in range(G) if g * G + b < D]
@@ -413,6 +423,14 @@ class BlockRunner:
             if self.shard == "baby" and len(ranks) > 1:   # no replicated baby rotations
                 out = fhespear_dist.bsgs_baby_sharded(ph, srv.ctx, cts[inputs[n][1]], self._pts(n), srv.G, srv.B,
                                                       srv.D, srv.gk, self.zero[0], self.dist, dev, ranks=ranks, group=pg)
+                if out is not None:
+                    res[n] = out
+                continue
+            if self.shard == "grid" and len(ranks) > 1:
+                rb, cols = self.grid[n]
+                out = fhespear_dist.bsgs_grid_sharded(ph, srv.ctx, cts[inputs[n][1]], self._pts(n), srv.G, srv.B,
+                                                      srv.D, srv.gk, self.zero[0], self.dist, rb, dev, ranks=ranks,
+                                                      group=pg, col_groups=cols)
                 if out is not None:
                     res[n] = out
                 continue
@@ -565,7 +583,7 @@ def run_blocks(ph, args, dist=None, rank=0, world=1, device=0, log=print):
     t0 = time.perf_counter()
     srv = Server(ph, args.N, args.L0, args.P, args.D, device=device)
     runs = [BlockRunner(srv, b, args.preencoded, dist, rank, world, split=getattr(args, "split", False),
-                        baby_mode=getattr(args, "baby_mode", "recompute"), shard=getattr(args, "shard", "giant"))
+                        baby_mode=getattr(args, "baby_mode", "recompute"), shard=getattr(args, "shard", "giant"), rb=getattr(args, "rb", None))
             for b in blocks]
     srv.ctx.synchronize()
     if rank == 0:
@@ -608,9 +626,11 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--split", action="store_true",
                     help="latency mode: each stage's projections shard their giant steps over rank groups")
-    ap.add_argument("--shard", default="giant", choices=("giant", "baby"),
-                    help="latency mode's split of a projection: giant groups (baby steps replicated) or baby steps "
-                         "(reduce-scatter of every group's partial inner products)")
+    ap.add_argument("--shard", default="giant", choices=("giant", "baby", "grid"),
+                    help="latency mode's split of a projection: giant groups (baby steps replicated), baby steps "
+                         "(reduce-scatter of every group's partial inner products) or a baby x giant grid")
+    ap.add_argument("--rb", type=int, default=None,
+                    help="grid shard: baby shares per projection group (default fhespear_dist.grid_rb)")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the process group even at world 1 (runs the exchange code on one GPU)")
     ap.add_argument("--baby-mode", default="recompute", choices=("recompute", "broadcast"),
