@@ -332,12 +332,10 @@ def bsgs_grid_sharded(ph, ctx, ct, pts, G: int, B: int, D: int, gk, zero_diag, d
     W = 2 * l * ctx.N
     rows = [int(q) for q in ctx.primes[:l]] * 2
     elts = [ph.get_elt_from_step(g * G, ctx.N) if g else 1 for g in my_groups]
-    if rb == 1:
-        partial = ph.bsgs_inner_products(ctx, baby, flat, len(bs), len(col))
+    if rb == 1:   # giant-step sharding: one fused linear transform over this rank's groups
+        part = bsgs_giant_partial(ph, ctx, baby, pts, G, D, col, gk, [zero_diag] * G)
         del baby
         mark("baby+inner")
-        part = ph.bsgs_giant_steps(ctx, partial, elts, gk)
-        del partial
     else:
         kmax = len(shares[0])
         parts = torch.empty((rb * kmax, W), dtype=torch.int64, device=device)
