@@ -16,6 +16,8 @@ Prints ONE JSON line on rank 0.  `roofline` is for the kernel with the largest d
 the timed region (HIP events on the library's stream around every launch); `cpu_baseline` times full
 matvecs of the same workload with the in-repo SEAL-class CPU port (oracle/cpu_port.c, OpenMP on the
 host cores this process may use); `parity` checks the output limbs against the C oracle's digest.
+The measured RWKV block (`rwkv_block`) carries its own limb check at N=1: the r projection's server call
+of the block, recomputed on the CPU from its recorded input limbs (`rwkv_block.parity`).
 """
 import argparse
 import json
@@ -300,7 +302,8 @@ def main():
             ctx.synchronize()
             del ctx
         try:
-            block = run_block(args, ph, dist, rank, world, local, args.block_steps, 1)
+            block = run_block(args, ph, dist, rank, world, local, args.block_steps, 1,
+                              capture=world == 1 and not args.no_cpu_baseline)
         except Exception as e:   # reported, never hidden: the matvec line stands on its own
             block = {"error": f"{type(e).__name__}: {e}"[:400]}
     if rank == 0:
@@ -403,6 +406,14 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args)
+            cap = block.pop("_capture", None) if isinstance(block, dict) else None
+            if cap is not None:
+                try:
+                    block["parity"] = cpu_check_block_projection(cap)
+                except Exception as e:   # reported, never hidden
+                    block["parity"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+        elif isinstance(block, dict):
+            block.pop("_capture", None)
         print(json.dumps(res))
     if dist is not None:
         dist.barrier()
@@ -450,10 +461,13 @@ def seal_leg(args, ph, cfg):
     return res
 
 
-def run_block(args, ph, dist, rank, world, local, steps, warmup):
+def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False):
     """One client-aided RWKV-7 block (cfg3 shapes, tools/rwkv_block.py = bg:756-899) on these ranks:
     8 BSGS projections in 4 dependent stages, pre-encoded diagonals resident, stage projections
-    dealt over the ranks.  Returns rank 0's {sec_per_block (median), ...} (None elsewhere)."""
+    dealt over the ranks.  Returns rank 0's {sec_per_block (median), ...} (None elsewhere).
+    capture (one rank): after the timed blocks, one more block records the r projection's server
+    call -- input ciphertext, output ciphertext and its 2048 diagonal plaintexts, as limbs -- for the
+    CPU leg's limb check (cpu_check_block_projection), returned under "_capture"."""
     sys.path.insert(0, str(REPO / "tools"))
     import rwkv_block as rb
     cfg = CONFIGS["cfg3"]
@@ -494,6 +508,21 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup):
         tt = torch.tensor([sec], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         sec = float(tt.item())
+    cap = None
+    if capture and rank == 0 and world == 1:
+        orig, rec = run.stage, {}
+
+        def stage(idx, ins):
+            outs = orig(idx, ins)
+            if idx == 0:
+                rec["ct_in"], rec["ct_out"] = ins["r"][0].to_numpy(), outs["r"].to_numpy()
+            return outs
+        run.stage = stage
+        rb.client_aided_block(run, *st)
+        run.stage = orig
+        rec["pts"] = [p.to_numpy() for p in run.pts["r"]]
+        rec.update(N=cfg["N"], L0=cfg["L0"], P=cfg["P"], D=D, sk_seed=srv.seed)
+        cap = rec
     res = None
     if rank == 0:
         ref = rb.plaintext_block(blk, *st)
@@ -507,6 +536,8 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup):
                "workload": cfg["workload"], "n_gpus": world,
                "parallelism": (f"giant-step-split projections x{world}" if split
                                else f"stage-dealt projections x{world}") + (" + RCCL broadcast/gather" if world > 1 else "")}
+        if cap is not None:
+            res["_capture"] = cap
     del run, srv
     return res
 
@@ -605,6 +636,33 @@ def cpu_baseline(cfg, primes, args):
             "sec_per_matvec": round(med, 4), "sec_per_matvec_all": [round(v, 4) for v in secs],
             "setup_s": round(t_setup, 1),
             "parity": limb_digest_check(args.config, y)}
+
+
+def cpu_check_block_projection(cap):
+    """Limb check of the block leg: the r projection's server call recorded in the
+    measured block (its GPU-encoded input ciphertext and diagonals) recomputed by the CPU port with the
+    oracle's Galois keys for the block's secret-key seed -- the reference loop bg:464-485 one rotation at
+    a time -- must give the GPU's output limbs exactly.  (The block's inputs come from the float64 GPU
+    encoder, so no digest can be committed ahead of time as for the matvec leg.)"""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import cpu_port
+    from oracle.oracle import Oracle, galois_elt
+    N, L0, P, D, seed = cap["N"], cap["L0"], cap["P"], cap["D"], cap["sk_seed"]
+    G, B = bsgs_params(D)
+    t0 = time.perf_counter()
+    primes = [int(q) for q in cpu_port.create_coeff_modulus(N, [59] * (L0 + P))]
+    o = Oracle(N, primes, P)
+    s = o.gen_secret(seed)
+    threads = cpu_port.box_threads()
+    with ThreadPoolExecutor(threads) as ex:
+        bk = dict(zip(range(1, G), ex.map(lambda b: o.gen_galois_key(seed, s, galois_elt(b, N)), range(1, G))))
+        gk = dict(zip(range(1, B), ex.map(lambda g: o.gen_galois_key(seed, s, galois_elt(g * G, N)), range(1, B))))
+    y = cpu_port.CpuPort(N, primes, P, threads).matvec(cap["ct_in"], bk, gk, cap["pts"], G, B, D)
+    return {"r_projection_limbs_match_cpu_port": bool(np.array_equal(y, cap["ct_out"])),
+            "sha256": cpu_port.sha256(cap["ct_out"]), "cpu_port_sha256": cpu_port.sha256(y),
+            "check": "r projection's server call (bg:545-659 real D->D) of the measured block, recomputed on "
+                     "the CPU (oracle/cpu_port.c, keys from the C oracle) from the recorded input limbs",
+            "seconds": round(time.perf_counter() - t0, 1)}
 
 
 if __name__ == "__main__":

@@ -443,14 +443,18 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
     if (!plain_tm(l, U, i, u)) return;
     const PrimeK& P = PK(T, i);
     const u64 q = P.q;
-    const u64* src = uniq[u] + (size_t)i * N;
+    // buffer loads / stores: per-lane offset tid in voffset, the half / row offsets in soffset
+    const __amdgpu_buffer_rsrc_t rs = brsrc(uniq[u] + (size_t)i * N, N * 8);
     const u64* tw = T.tw_inv + (size_t)i * N * 2;
     u64 lo[16];
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
         if (h) __syncthreads();
+        u64 v[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = src[h * NH + tid + c * TH];
+        for (int c = 0; c < 16; ++c) v[c] = bload64(rs, tid * 8, (h * NH + c * TH) * 8);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = v[c];
         __syncthreads();
         ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL>(lds, tid, tw, q, 1 + h);
         if (h == 0) {
@@ -460,13 +464,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
     }
     const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
     const u64 s0 = cst[0], s0s = cst[1], s1 = cst[2], s1s = cst[3], q2 = 2 * q;
-    u64* dst = acoef + ((size_t)u * l + i) * N;
+    const __amdgpu_buffer_rsrc_t rd = brsrc(acoef + ((size_t)u * l + i) * N, N * 8);
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
-        const int e = tid + c * TH;
         const u64 X = lo[c], Y = lds[row_pad<TH>(tid, c)];
-        dst[e] = csub(shoup_lazy(X + Y, s0, s0s, q), q);
-        dst[NH + e] = csub(shoup_lazy(X - Y + q2, s1, s1s, q), q);
+        bstore64(csub(shoup_lazy(X + Y, s0, s0s, q), q), rd, tid * 8, c * TH * 8);
+        bstore64(csub(shoup_lazy(X - Y + q2, s1, s1s, q), q), rd, tid * 8, (NH + c * TH) * 8);
     }
 }
 

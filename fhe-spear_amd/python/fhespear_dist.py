@@ -270,6 +270,16 @@ def grid_rb(R: int) -> int:
     return R if R >= 8 else 1
 
 
+def column_shares(n: int, rb: int) -> list[list[int]]:
+    """A giant column of n groups split over its rb ranks in ceil(n / rb)-sized contiguous slices (the
+    last shorter), so slice r sits at slots [r k, r k + len) of a [rb k] reduce-scatter buffer without
+    reordering; every rank gets at least one group when (rb - 1) ceil(n / rb) < n."""
+    k = -(-n // rb)
+    if (rb - 1) * k >= n:
+        raise ValueError(f"grid: a column of {n} giant groups leaves a rank of {rb} without a group")
+    return [list(range(r * k, min((r + 1) * k, n))) for r in range(rb)]
+
+
 def grid_groups(dist, ranks, rb: int):
     """The process groups of the grid's giant columns (the rb ranks that reduce-scatter one column's
     partial inner products).  Every process of the default group must call this with the same

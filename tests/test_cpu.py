@@ -455,3 +455,26 @@ def test_cpu_port_matches_oracle(orc):
                                 input_seed=bench.INPUT_SEED, diag_seed=bench.DIAG_SEED)
     man = json.loads((GOLDEN / "manifest.json").read_text())["bench_digests"]
     assert cp.sha256(y) == man["small"]["sha256"]
+
+
+def test_bench_block_projection_check_on_cpu(orc):
+    """bench.py's block-leg limb check (cpu_check_block_projection) accepts the oracle's own loop
+    output for a recorded call and rejects a one-limb change (small ring, no GPU)."""
+    import bench
+    N, L0, P, D, seed = 4096, 6, 3, 64, 11
+    primes = [int(q) for q in orc.create_coeff_modulus(N, [59] * (L0 + P))]
+    o = orc.Oracle(N, primes, P)
+    s = o.gen_secret(seed)
+    G, B = bench.bsgs_params(D)
+    ct = o.encrypt_symmetric(seed, 1, s, o.random_plaintext(5, 0, L0))
+    pts = [o.random_plaintext(6, k, L0) for k in range(D)]
+    bk = {b: o.gen_galois_key(seed, s, orc.galois_elt(b, N)) for b in range(1, G)}
+    gkeys = [None] + [o.gen_galois_key(seed, s, orc.galois_elt(g * G, N)) for g in range(1, B)]
+    baby = [ct] + [o.rotate(ct, bk[b], b) for b in range(1, G)]
+    want = o.bsgs_loop(baby, pts, gkeys, G, B, D)
+    cap = dict(ct_in=ct, ct_out=want, pts=pts, N=N, L0=L0, P=P, D=D, sk_seed=seed)
+    assert bench.cpu_check_block_projection(cap)["r_projection_limbs_match_cpu_port"]
+    bad = want.copy()
+    bad[1, 0, 0] ^= 1
+    assert not bench.cpu_check_block_projection(dict(cap, ct_out=bad))["r_projection_limbs_match_cpu_port"]
+

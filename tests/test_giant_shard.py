@@ -121,6 +121,14 @@ def test_grid_rows_partition(world, rb):
     assert fd.grid_rows(G, B, D, world, world, 1) == fd.baby_sharded_rows(G, B, D, world, 1)
     with pytest.raises(ValueError):
         fd.grid_shape(world, world + 1)
+    rb_, rg = fd.grid_shape(world, rb)
+    for j in range(rg):                      # each column's slices: contiguous, in slot order, none empty
+        n = len(fd.giant_groups(B, rg, j))
+        sl = fd.column_shares(n, rb_)
+        assert [x for s in sl for x in s] == list(range(n)) and all(sl)
+        assert all(s[0] == r * len(sl[0]) for r, s in enumerate(sl))
+    with pytest.raises(ValueError):
+        fd.column_shares(5, 4)               # ceil(5/4) = 2 per slice leaves the 4th rank empty
 
 
 @pytest.mark.gpu

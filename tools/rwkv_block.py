@@ -142,7 +142,7 @@ class Server:
     non-BSGS fhe_projection and are left out)."""
 
     def __init__(self, ph, N, L0, P, D, seed=11, device=0):
-        self.ph, self.N, self.L0, self.D, self.device = ph, N, L0, D, device
+        self.ph, self.N, self.L0, self.D, self.device, self.seed = ph, N, L0, D, device, seed
         G, B = bsgs_params(D)
         self.G, self.B = G, B
         steps = list(range(1, G)) + [g * G for g in range(1, B)]
