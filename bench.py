@@ -45,6 +45,9 @@ CONFIGS = {
     "cfg3": dict(N=16384, L0=36, P=3, D=2048, F=8192,
                  workload="client-aided RWKV-7 block d=2048 F=8192 N=16384 L0=36 P=3: 8 BSGS projections, "
                           "pre-encoded diagonals resident in HBM"),
+    # the block leg's code path at test size (tests/test_bench_legs.py)
+    "block_small": dict(N=4096, L0=6, P=3, D=64, F=256, workload="client-aided RWKV-7 block d=64 F=256 N=4096 "
+                                                                  "L0=6 P=3 (test size)"),
 }
 SK_SEED, INPUT_SEED, DIAG_SEED = 1000, 10000, 2   # tests/golden/make_bench_digest.py
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
@@ -145,7 +148,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)   # median of 20 after 3 warmups
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="cfg2", choices=sorted(k for k in CONFIGS if k != "block_small"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=3, help="timed full CPU matvecs (after one untimed)")
     ap.add_argument("--no-block", action="store_true",
@@ -461,7 +464,7 @@ def seal_leg(args, ph, cfg):
     return res
 
 
-def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False):
+def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, config="cfg3"):
     """One client-aided RWKV-7 block (cfg3 shapes, tools/rwkv_block.py = bg:756-899) on these ranks:
     8 BSGS projections in 4 dependent stages, pre-encoded diagonals resident, stage projections
     dealt over the ranks.  Returns rank 0's {sec_per_block (median), ...} (None elsewhere).
@@ -470,9 +473,9 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False):
     CPU leg's limb check (cpu_check_block_projection), returned under "_capture"."""
     sys.path.insert(0, str(REPO / "tools"))
     import rwkv_block as rb
-    cfg = CONFIGS["cfg3"]
+    cfg = CONFIGS[config]
     D, F = cfg["D"], cfg["F"]
-    H = D // 64
+    H = max(1, D // 64)
     rng = np.random.default_rng(5)
     blk = rb.BlockWeights(rng, 1, D, F, H)
     srv = rb.Server(ph, cfg["N"], cfg["L0"], cfg["P"], D, device=local)
@@ -512,12 +515,12 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False):
     if capture and rank == 0 and world == 1:
         orig, rec = run.stage, {}
 
-        def stage(idx, ins):
+        def recording_stage(idx, ins):
             outs = orig(idx, ins)
             if idx == 0:
                 rec["ct_in"], rec["ct_out"] = ins["r"][0].to_numpy(), outs["r"].to_numpy()
             return outs
-        run.stage = stage
+        run.stage = recording_stage
         rb.client_aided_block(run, *st)
         run.stage = orig
         rec["pts"] = [p.to_numpy() for p in run.pts["r"]]
