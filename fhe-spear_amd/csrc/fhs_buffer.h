@@ -22,3 +22,8 @@ __device__ __forceinline__ u64 bload64(__amdgpu_buffer_rsrc_t r, int voff, int s
 __device__ __forceinline__ void bstore64(u64 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(fhs_u32x2, v), r, voff, soff, 0);
 }
+// the same with the cache-policy bits (2: non-temporal -- streamed results that L2 need not keep)
+template <int AUX>
+__device__ __forceinline__ void bstore64_aux(u64 v, __amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(fhs_u32x2, v), r, voff, soff, AUX);
+}

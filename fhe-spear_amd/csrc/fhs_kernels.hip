@@ -12,6 +12,10 @@
 // Every integer result is reduced to [0, q): limbs are bit-identical to oracle/ckks_oracle.c.
 #include "fhs_kernels.h"
 typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
+#ifndef FHS_MODUP_STORE_AUX
+#define FHS_MODUP_STORE_AUX 2   // k_modup_h output stores non-temporal: L2 keeps the digits the next
+                                // targets convert (reads 3.14 -> 2.49 GB/step, profiles/r03/ab/*_modup_nt.json)
+#endif
 #ifndef FHS_KSIP_UNROLL
 #define FHS_KSIP_UNROLL 4   // digits of the key inner product unrolled together (4 since the buffer loads: profiles/r03/ab/ksip_ch_summary.txt)
 #endif
@@ -797,7 +801,8 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
         // buffer stores: per-lane offset tid, the half / row offset in soffset
         const __amdgpu_buffer_rsrc_t ro = brsrc(o, N * 8);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) bstore64(fwd_canon(lds[row_pad<TH>(tid, c)], R), ro, tid * 8, (h * NH + c * TH) * 8);
+        for (int c = 0; c < 16; ++c)
+            bstore64_aux<FHS_MODUP_STORE_AUX>(fwd_canon(lds[row_pad<TH>(tid, c)], R), ro, tid * 8, (h * NH + c * TH) * 8);
     }
 }
 template <int LOGN>
