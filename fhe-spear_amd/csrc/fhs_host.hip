@@ -763,6 +763,11 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     T.N = (int)N; T.logN = c->logN; T.L0 = L0; T.P = P; T.K = K; T.dnum = dnum;
     T.max_qbits = 0;
     for (int i = 0; i < K; ++i) T.max_qbits = std::max(T.max_qbits, 64 - __builtin_clzll(c->q[i]));
+    // ModUp's specialised conversion: 3-limb digits with every target on the pseudo-Mersenne fold (the
+    // generic loop is then not compiled into the kernel), one-limb digits, or the generic loop
+    bool all_cpm = true;
+    for (int i = 0; i < K; ++i) all_cpm = all_cpm && ((pk[i].pm >> 40) & 1);
+    T.modup_dp = (P == 3 && L0 % 3 == 0 && all_cpm) ? 3 : (P == 1 ? 1 : 0);
     HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");
     HIPCHK(up(twf.data(), 8 * twf.size(), (const void**)&T.tw_fwd), "tables");
     HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");

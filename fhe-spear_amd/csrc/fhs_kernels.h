@@ -32,6 +32,9 @@ struct DevTables {
     // before the decomposition, ModDown rounded by adding floor(p/2)
     int ks_seal;
     int max_qbits;            // bits of the largest prime (<= 59: split-30 high halves < 2^29, fewer folds)
+    int modup_dp;             // ModUp conversion compiled for this shape: 3 (P = 3, all targets pseudo-
+                              // Mersenne: modup_convert3 only, at levels l % 3 == 0), 1 (P = 1:
+                              // modup_convert1), 0 (generic)
 };
 
 // One key-switch of a batch: out = KS_key( galois_elt(a) ) + (galois_elt(add0), add1).

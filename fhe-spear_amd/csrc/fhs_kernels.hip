@@ -704,6 +704,35 @@ __device__ __forceinline__ void modup_convert3(const u64* yb, const unsigned cha
     }
 }
 
+// ModUp of a one-limb digit (P = 1: SEAL's convention, fhe_rwkv_inference's ring): Q_S = q_u, so the
+// hat factor is 1 and the conversion is y - v q_u mod m = y + v (m - q_u mod m): below q_u + m <= 4 m
+// when q_u <= 3 m (the caller checks), inside the forward NTT's input bound, so no product and no
+// reduction.
+template <int LOGN>
+__device__ __forceinline__ void modup_convert1(const u64* yb, const unsigned char* vb, u64 negQ, u64 m, u64 w0,
+                                               u64 w0p, int tid, u64* lds, u64 hi[16]) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
+    const __amdgpu_buffer_rsrc_t ry = brsrc(yb, N * 8), rv = brsrc(vb, N);
+    const u64 q2 = 2 * m;
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
+        u64 x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int e = (ch * 4 + (k & 3)) * TH + (k >= 4 ? NH : 0);
+            const u64 y = bload64(ry, tid * 8, e * 8);
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b8(rv, tid, e, 0);
+            x[k] = y + (v ? negQ : 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // global stage 0: (e, e + N/2), twiddle psi^rev(1)
+            const u64 tt = shoup_lazy(x[4 + k], w0, w0p, m);
+            lds[row_pad<TH>(tid, ch * 4 + k)] = x[k] + tt;
+            hi[ch * 4 + k] = x[k] + (q2 - tt);
+        }
+    }
+}
+
 // (b1') ModUp + NTT with half the limb in LDS (68 KiB at N = 16384): two workgroups share a CU,
 // so one's loads and base conversion overlap the other's NTT.  Stage 0 of the forward NTT pairs
 // coefficient e with e + N/2; each thread converts both, applies that butterfly in registers, keeps
@@ -712,7 +741,10 @@ __device__ __forceinline__ void modup_convert3(const u64* yb, const unsigned cha
 template <int LOGN>
 constexpr int modup_h_lds_words() { return (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16; }
 // one workgroup's share: target limb t of digit j = mi % dn of input u = mi / dn
-template <int LOGN>
+// DP: the digit size with a specialised conversion compiled in (3: modup_convert3, 1: modup_convert1,
+// 0: the generic loop only) -- one instantiation per context shape, so the rarely used paths cost the
+// usual one no registers
+template <int LOGN, int DP>
 __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoef, const unsigned char* vcnt, u64* ext,
                                              int l, int t, int mi, int tid, u64* lds) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;   // 16 coefficient pairs per thread
@@ -735,10 +767,12 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
     ld_tw(tw, 1, w0, w0p);
     const u64 q2 = 2 * m;
     u64 hi[16];
-    if (ns == 3 && R.cpm) {
+    if constexpr (DP == 3) {   // every digit 3 limbs, every target on the fold (launch_modup checks)
         // the usual digit (P = 3 limbs, pseudo-Mersenne target): compile-time digit size, buffer loads
         // whose limb / chunk offsets are scalar (no per-load address arithmetic on the VALU)
         modup_convert3<LOGN>(yb, vb, hat, K, negQ, R, w0, w0p, tid, lds, hi);
+    } else if (DP == 1 && ns == 1 && PK(T, s0).q <= 3 * m) {   // y + v negQ < q_u + m <= 4 m: the NTT's input bound
+        modup_convert1<LOGN>(yb, vb, negQ, m, w0, w0p, tid, lds, hi);
     } else {
     constexpr int CH = FHS_MODUPH_CH;   // coefficient pairs per conversion chunk
 #pragma unroll
@@ -805,7 +839,7 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
             bstore64_aux<FHS_MODUP_STORE_AUX>(fwd_canon(lds[row_pad<TH>(tid, c)], R), ro, tid * 8, (h * NH + c * TH) * 8);
     }
 }
-template <int LOGN>
+template <int LOGN, int DP>
 __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
                                                                  const u64* acoef, const unsigned char* vcnt, u64* ext,
                                                                  int l, int U) {
@@ -813,7 +847,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     int t, mi;
     if (!xcd_tinner(E, dn * U, t, mi)) return;
-    modup_h_body<LOGN>(T, acoef, vcnt, ext, l, t, mi, threadIdx.x, lds);
+    modup_h_body<LOGN, DP>(T, acoef, vcnt, ext, l, t, mi, threadIdx.x, lds);
 }
 
 template <int LOGN>
@@ -821,10 +855,15 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
                          u64* ext, int l, int U, hipStream_t st) {
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     const int mgrid = xcd_grid(E, dn * U);
-    if ((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>())
-        hipLaunchKernelGGL((k_modup_h<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 32), 0, st, T, uniq, acoef, vcnt, ext, l, U);
-    else
+    const dim3 g(mgrid), b((1 << LOGN) / 32);
+    if (!((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>()))
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    else if (T.modup_dp == 3 && l % 3 == 0)   // every digit of this level full (3 limbs)
+        hipLaunchKernelGGL((k_modup_h<LOGN, 3>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    else if (T.modup_dp == 1)
+        hipLaunchKernelGGL((k_modup_h<LOGN, 1>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    else
+        hipLaunchKernelGGL((k_modup_h<LOGN, 0>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
 }
 
 // (b2) key inner product with the automorphism applied on the fly, lazy 128-bit over digits:
