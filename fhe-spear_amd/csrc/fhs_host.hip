@@ -141,6 +141,68 @@ static bool conv_pm_ok(uint64_t q, int ns) {
     const hu128 rmax = (((hu128)1 << b) - 1) + Sh * d;
     return rmax < 2 * (hu128)q;
 }
+// X form of the centred extension for full 3-limb digits (fhs_modarith.h centered_x_pack /
+// convert3x_value, fhs_kernels.hip k_centered_x): per digit j (primes 3j..3j+2, j < dnum with 3j + 3 <=
+// L0) the exact Q_S / q_u, the rounding thresholds ((2k - 1) Q_S + 1) / 2 and 2^179 - v Q_S (192-bit
+// words, little-endian) into xd[j][32]; per prime m the base-2^60 weights 2^60, 2^120 mod m (split-30
+// packed) and -2^179 mod m into xt[i][4].  |X| < Q_S / 2 < 2^176, so U = X + 2^179 lies in (0, 2^180).
+static void modup_xform_tables(const uint64_t* primes, int K, int L0, int dnum, uint64_t* xd, uint64_t* xt) {
+    auto mul192 = [](const uint64_t a[3], uint64_t m, uint64_t r[3]) {   // r = a m mod 2^192
+        hu128 cy = 0;
+        for (int w = 0; w < 3; ++w) {
+            const hu128 t = (hu128)a[w] * m + cy;
+            r[w] = (uint64_t)t;
+            cy = t >> 64;
+        }
+    };
+    for (int j = 0; j < dnum && 3 * j + 3 <= L0; ++j) {
+        const uint64_t* q3 = &primes[3 * j];
+        uint64_t* d = &xd[(size_t)j * 32];
+        for (int u = 0; u < 3; ++u) {
+            const hu128 h = (hu128)q3[(u + 1) % 3] * q3[(u + 2) % 3];
+            d[2 * u] = (uint64_t)h;
+            d[2 * u + 1] = (uint64_t)(h >> 64);
+        }
+        const uint64_t one[3] = {1, 0, 0};
+        uint64_t Q[3], t[3];
+        mul192(one, q3[0], t);
+        mul192(t, q3[1], Q);
+        mul192(Q, q3[2], t);
+        std::copy(t, t + 3, Q);
+        for (int k = 1; k <= 3; ++k) {   // ((2k - 1) Q + 1) / 2: (2k - 1) Q is odd, so + 1 is carry-free
+            uint64_t m[3];
+            mul192(Q, (uint64_t)(2 * k - 1), m);
+            m[0] += 1;
+            uint64_t* th = d + 6 + 3 * (k - 1);
+            th[0] = (m[0] >> 1) | (m[1] << 63);
+            th[1] = (m[1] >> 1) | (m[2] << 63);
+            th[2] = m[2] >> 1;
+        }
+        for (int v = 0; v <= 3; ++v) {   // 2^179 - v Q
+            uint64_t m[3];
+            mul192(Q, (uint64_t)v, m);
+            uint64_t* c = d + 15 + 3 * v;
+            const uint64_t top[3] = {0, 0, 1ull << (179 - 128)};
+            uint64_t br = 0;
+            for (int w = 0; w < 3; ++w) {
+                const hu128 s = (hu128)top[w] - m[w] - br;
+                c[w] = (uint64_t)s;
+                br = (uint64_t)(s >> 64) ? 1 : 0;
+            }
+        }
+    }
+    for (int i = 0; i < K; ++i) {
+        const uint64_t m = primes[i];
+        uint64_t p60 = 1 % m;
+        for (int e = 0; e < 60; ++e) p60 = h_mulmod(p60, 2, m);
+        const uint64_t p120 = h_mulmod(p60, p60, m);
+        uint64_t p179 = 1 % m;
+        for (int e = 0; e < 179; ++e) p179 = h_mulmod(p179, 2, m);
+        xt[(size_t)i * 4 + 0] = pack30(p60);
+        xt[(size_t)i * 4 + 1] = pack30(p120);
+        xt[(size_t)i * 4 + 2] = p179 ? m - p179 : 0;
+    }
+}
 static bool h_is_prime(uint64_t n) {
     if (n < 2) return false;
     const uint64_t bases[] = {2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37};
@@ -700,6 +762,8 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
             }
         }
     }
+    std::vector<uint64_t> mu_xd((size_t)dnum * 32, 0), mu_xt((size_t)K * 4, 0);
+    if (P == 3) modup_xform_tables(primes, K, L0, dnum, mu_xd.data(), mu_xt.data());
     // ---- ModDown tables
     std::vector<uint64_t> md_intt((size_t)P * 4), md_hat((size_t)P * L0), md_pinv((size_t)4 * L0);
     for (int k = 0; k < P; ++k) {
@@ -775,6 +839,8 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(mu_hat.data(), 8 * mu_hat.size(), (const void**)&T.modup_hat), "tables");
     HIPCHK(up(mu_R.data(), 8 * mu_R.size(), (const void**)&T.modup_R), "tables");
     HIPCHK(up(mu_Q.data(), 8 * mu_Q.size(), (const void**)&T.modup_Q), "tables");
+    HIPCHK(up(mu_xd.data(), 8 * mu_xd.size(), (const void**)&T.modup_xd), "tables");
+    HIPCHK(up(mu_xt.data(), 8 * mu_xt.size(), (const void**)&T.modup_xt), "tables");
     HIPCHK(up(md_intt.data(), 8 * md_intt.size(), (const void**)&T.md_intt), "tables");
     HIPCHK(up(md_hat.data(), 8 * md_hat.size(), (const void**)&T.md_hat), "tables");
     HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
@@ -2834,6 +2900,24 @@ extern "C" fhs_status fhs_context_stream(fhs_context* c, void** stream) {
     return FHS_OK;
 }
 
+// The ModUp X form's arithmetic on the host (the same __host__ __device__ routines the kernels run):
+// y3 (residues of a 3-prime digit q3, after the inverse-hat scaling) -> the centred digit value mod m.
+extern "C" fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* y3, uint64_t m, uint64_t* out) {
+    if (!q3 || !y3 || !out) return FHS_ERR_INVALID;
+    const uint64_t w = pm_word(m, 14);
+    if (!w || !conv_pm_ok(m, 3)) return fail(FHS_ERR_INVALID, "debug_modup_xform: target not on the pseudo-Mersenne fold");
+    const uint64_t pr[4] = {q3[0], q3[1], q3[2], m};
+    uint64_t xd[32] = {0}, xt[16] = {0};
+    modup_xform_tables(pr, 4, 3, 1, xd, xt);
+    uint64_t words[3];
+    centered_x_pack(y3, xd, words);
+    const uint64_t* t = xt + 12;
+    const uint64_t x = convert3x_value(words[0], words[1], words[2], unpack30(t[0]), unpack30(t[1]), t[2],
+                                       (unsigned)(w & 127), (unsigned)(w >> 8));
+    if (x >= 2 * m) return fail(FHS_ERR_INVALID, "debug_modup_xform: result above 2m");
+    *out = x >= m ? x - m : x;
+    return FHS_OK;
+}
 extern "C" fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* out, int* pm_used) {
     if (!out || q < 3) return FHS_ERR_INVALID;
     const uint64_t w = pm_word(q, 14);

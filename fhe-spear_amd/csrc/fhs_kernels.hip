@@ -140,6 +140,46 @@ template <int LOGN, bool H = ntt_half<LOGN>()> constexpr int ntt_lds_words() {
         else                                                                                           \
             hipLaunchKernelGGL((K<LOGN>), grid, dim3(ntt_threads<LOGN>()), 0, st, __VA_ARGS__);        \
     } while (0)
+// Radix-4 first stages: the half-limb forward transforms of ModUp / ModDown do global stages 0 and 1 in
+// registers while converting -- a thread's rows c and c + 8 are N/4 apart, so it converts the quad
+// (e, e + N/4, e + N/2, e + 3N/4) and applies a radix-4 butterfly (stage 0 twiddle psi^rev(1); stage 1
+// psi^rev(2) on the lower half, psi^rev(3) on the upper).  Each half's LDS transform then starts at its
+// local stage 1: 12 stages = four radix-8 passes, no radix-2 pass.  Same butterflies, same values
+// (A/B on the cfg2 bench: k_modup 2.04 -> 1.98 ms, k_moddown 0.46 -> 0.44 ms per step,
+// profiles/r03/ab/r4*.json).
+struct Tw4 {
+    u64 w1, w1p, w2, w2p, w3, w3p;
+};
+__device__ __forceinline__ Tw4 ld_tw4(const u64* __restrict__ tw) {
+    Tw4 t;
+    ld_tw(tw, 1, t.w1, t.w1p);
+    ld_tw(tw, 2, t.w2, t.w2p);
+    ld_tw(tw, 3, t.w3, t.w3p);
+    return t;
+}
+// x = {row c lower, row c + 8 lower, row c upper, row c + 8 upper}, each < 2q: lower-half results to LDS
+// rows c, c + 8, upper-half results to hi[c], hi[c + 8] (values as the LDS passes would leave them)
+template <int TH>
+__device__ __forceinline__ void fwd_quad_first2(u64 x[4], const Tw4& w, u64 q, bool lazy, u64* lds, int tid, int c,
+                                                u64 hi[16]) {
+    const u64 q2 = 2 * q;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {   // global stage 0: (e, e + N/2); outputs < 4q
+        const u64 tt = shoup_lazy(x[2 + k], w.w1, w.w1p, q);
+        const u64 X = x[k];
+        x[k] = X + tt;
+        x[2 + k] = X + (q2 - tt);
+    }
+    if (!lazy) {   // Harvey form: the next butterfly's unmultiplied inputs back below 2q
+        x[0] = x[0] >= q2 ? x[0] - q2 : x[0];
+        x[2] = x[2] >= q2 ? x[2] - q2 : x[2];
+    }
+    const u64 ta = shoup_lazy(x[1], w.w2, w.w2p, q), tb = shoup_lazy(x[3], w.w3, w.w3p, q);   // global stage 1
+    lds[row_pad<TH>(tid, c)] = x[0] + ta;
+    lds[row_pad<TH>(tid, c + 8)] = x[0] + (q2 - ta);
+    hi[c] = x[2] + tb;
+    hi[c + 8] = x[2] + (q2 - tb);
+}
 // forward: load(e) < 2q for every e < N; store(e, v) receives the canonical NTT value
 template <int LOGN, int RL, bool H = ntt_half<LOGN>(), class Load, class Store>
 __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restrict__ tw, const RedU& R, Load load,
@@ -587,9 +627,33 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
         vout[idx] = (unsigned char)v;
     }
 }
-static void launch_centered(const DevTables& T, const u64* acoef, unsigned char* vout, int l, int U, hipStream_t st) {
+// (a2') X form of the centred extension (full 3-limb digits, modup_xform): the exact centred digit value
+// X = S - v Q_S, S = sum_u y_u Q_S/q_u, v = round(S / Q_S) (|X| < Q_S/2; S/Q_S is never a half: Q_S is
+// odd), computed once per coefficient and digit instead of once per target limb, and stored in place of
+// the digit's three residues as U = X + 2^179 in base-2^60 words V0, V1, V2, each split-30 packed.
+// modup_convert3x reduces V0 + V1 (2^60 mod m) + V2 (2^120 mod m) - 2^179 mod m = X mod m: the same
+// residue the count form gives (it is the same integer), with two split-30 products per target instead
+// of three plus the count term, and no count bytes.
+__global__ void k_centered_x(DevTables T, u64* acoef, int l, int U) {
+    const int N = T.N, dn = l / 3;
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y % dn, u = blockIdx.y / dn;
+    if (n >= N || u >= U) return;
+    u64* yb = acoef + ((size_t)u * l + 3 * j) * N + n;
+    const u64 y[3] = {yb[0], yb[N], yb[2 * (size_t)N]};
+    u64 w[3];
+    centered_x_pack(y, T.modup_xd + (size_t)j * 32, w);
+    yb[0] = w[0];
+    yb[N] = w[1];
+    yb[2 * (size_t)N] = w[2];
+}
+
+static void launch_centered(const DevTables& T, u64* acoef, unsigned char* vout, int l, int U, hipStream_t st) {
     const int dn = (l + T.P - 1) / T.P;
-    hipLaunchKernelGGL(k_centered, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, vout, l, U);
+    if (modup_xform(T, l))
+        hipLaunchKernelGGL(k_centered_x, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, l, U);
+    else
+        hipLaunchKernelGGL(k_centered, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, vout, l, U);
 }
 
 // (b1) ModUp + NTT: ext[u][j][t] = NTT_t(centred conv_{digit j -> t}(y_u)) for t outside digit
@@ -657,50 +721,32 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
     }
 }
 
-// ModUp conversion of a 3-limb digit into target limb `m` (pseudo-Mersenne fold, PrimeK.pm bit 40)
-// for one half-limb workgroup: each thread converts its 16 coefficient pairs (e, e + N/2), does the
-// global first NTT stage on them in registers, writes the lower results to LDS and keeps the upper
-// ones in hi[].  Loads are buffer loads: the digit's three limbs and the centred counts through one
-// descriptor each, the per-lane part (tid) in voffset and every limb / chunk offset in soffset.
+// ModUp conversion of a full 3-limb digit from its X form (k_centered_x) into target limb `m`
+// (pseudo-Mersenne fold, PrimeK.pm bit 40), radix-4 first stages (fwd_quad_first2), buffer loads:
+// x = V0 + V1 e1 + V2 e2 + c3 (e1 = 2^60, e2 = 2^120, c3 = -2^179 mod m) as split-30 sums (each within
+// the 3-product bounds conv_pm_ok proves for this prime), folded by acc3_reduce_pm to [0, 2m).
 template <int LOGN>
-__device__ __forceinline__ void modup_convert3(const u64* yb, const unsigned char* vb, const u64* hat, int K,
-                                               u64 negQ, const RedU& R, u64 w0, u64 w0p, int tid, u64* lds,
-                                               u64 hi[16]) {
+__device__ __forceinline__ void modup_convert3x(const u64* yb, const u64* xt, const RedU& R, const u64* tw, int tid,
+                                                u64* lds, u64 hi[16]) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32, CH = FHS_MODUPH_CH;
-    const __amdgpu_buffer_rsrc_t ry = brsrc(yb, 3 * N * 8), rv = brsrc(vb, N);
-    const Split30 h0 = split30(hat[0]), h1 = split30(hat[K]), h2 = split30(hat[2 * K]);
-    const u64 m = R.q, q2 = 2 * m;
+    const __amdgpu_buffer_rsrc_t ry = brsrc(yb, 3 * N * 8);
+    const Split30 e1 = unpack30(xt[0]), e2 = unpack30(xt[1]);
+    const u64 c3 = xt[2], m = R.q, q2 = 2 * m;
     const int vo = tid * 8;
+    const Tw4 w4 = ld_tw4(tw);
 #pragma unroll
-    for (int ch = 0; ch < 16 / CH; ++ch) {
-        u64 y[3][2 * CH];
-        uint32_t vv[2 * CH];
+    for (int ch = 0; ch < 8; ++ch) {
+        u64 V[3][4];   // k: rows ch (k = 0, 2) and ch + 8 (k = 1, 3), lower (k < 2) / upper half
 #pragma unroll
-        for (int k = 0; k < 2 * CH; ++k) {
-            const int e = (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);   // coefficient index minus tid
+        for (int k = 0; k < 4; ++k) {
+            const int e = (ch + 8 * (k & 1)) * TH + (k >= 2 ? NH : 0);   // coefficient index minus tid
 #pragma unroll
-            for (int w = 0; w < 3; ++w)
-                y[w][k] = bload64(ry, vo, (w * N + e) * 8);
-            vv[k] = __builtin_amdgcn_raw_buffer_load_b8(rv, tid, e, 0);
+            for (int w = 0; w < 3; ++w) V[w][k] = bload64(ry, vo, (w * N + e) * 8);
         }
-        u64 x[2 * CH];
+        u64 x[4];
 #pragma unroll
-        for (int k = 0; k < 2 * CH; ++k) {
-            Acc3 a = {0, 0, 0};
-            acc3_mac(a, split30(y[0][k]), h0);
-            acc3_mac(a, split30(y[1][k]), h1);
-            acc3_mac(a, split30(y[2][k]), h2);
-            // - v Q_S folded into L as v (m - Q_S mod m); result in [0, 2m)
-            const uint32_t v = vv[k];
-            const u64 vq = mul32w(v, (uint32_t)negQ) + ((u64)(v * (uint32_t)(negQ >> 32)) << 32);
-            x[k] = acc3_reduce_pm(a.L + vq, a.M, a.H, R.b, R.d);
-        }
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {   // global stage 0: (e, e + N/2), twiddle psi^rev(1)
-            const u64 tt = shoup_lazy(x[CH + k], w0, w0p, m);
-            lds[row_pad<TH>(tid, ch * CH + k)] = x[k] + tt;
-            hi[ch * CH + k] = x[k] + (q2 - tt);
-        }
+        for (int k = 0; k < 4; ++k) x[k] = convert3x_value(V[0][k], V[1][k], V[2][k], e1, e2, c3, R.b, R.d);
+        fwd_quad_first2<TH>(x, w4, m, R.lazy, lds, tid, ch, hi);
     }
 }
 
@@ -741,7 +787,7 @@ __device__ __forceinline__ void modup_convert1(const u64* yb, const unsigned cha
 template <int LOGN>
 constexpr int modup_h_lds_words() { return (1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16; }
 // one workgroup's share: target limb t of digit j = mi % dn of input u = mi / dn
-// DP: the digit size with a specialised conversion compiled in (3: modup_convert3, 1: modup_convert1,
+// DP: the digit size with a specialised conversion compiled in (3: modup_convert3x, 1: modup_convert1,
 // 0: the generic loop only) -- one instantiation per context shape, so the rarely used paths cost the
 // usual one no registers
 template <int LOGN, int DP>
@@ -770,7 +816,7 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
     if constexpr (DP == 3) {   // every digit 3 limbs, every target on the fold (launch_modup checks)
         // the usual digit (P = 3 limbs, pseudo-Mersenne target): compile-time digit size, buffer loads
         // whose limb / chunk offsets are scalar (no per-load address arithmetic on the VALU)
-        modup_convert3<LOGN>(yb, vb, hat, K, negQ, R, w0, w0p, tid, lds, hi);
+        modup_convert3x<LOGN>(yb, T.modup_xt + (size_t)pt * 4, R, tw, tid, lds, hi);
     } else if (DP == 1 && ns == 1 && PK(T, s0).q <= 3 * m) {   // y + v negQ < q_u + m <= 4 m: the NTT's input bound
         modup_convert1<LOGN>(yb, vb, negQ, m, w0, w0p, tid, lds, hi);
     } else {
@@ -831,7 +877,9 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
             for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
         }
         __syncthreads();
-        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, m, R.lazy, 1 + h);
+        // the radix-4 conversion (modup_convert3x, FHS_MODUP_R4) did each half's local stage 0 already
+        constexpr int S0 = DP == 3 ? 1 : 0;
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0>(lds, tid, tw, m, R.lazy, 1 + h);
         // buffer stores: per-lane offset tid, the half / row offset in soffset
         const __amdgpu_buffer_rsrc_t ro = brsrc(o, N * 8);
 #pragma unroll
@@ -1051,40 +1099,36 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const
 }
 
 // ModDown conversion of the P = 3 special limbs (coefficient form, already scaled by inv(P/p_k)) into
-// data limb i (pseudo-Mersenne fold), half-limb form as modup_convert3: x = sum_k y_k (P/p_k) mod q_i,
-// global first NTT stage in registers, lower results to LDS, upper ones kept in hi[].
+// data limb i (pseudo-Mersenne fold), half-limb form as modup_convert3x: x = sum_k y_k (P/p_k) mod q_i,
+// global stages 0 and 1 in registers (fwd_quad_first2), lower results to LDS, upper ones kept in hi[].
 template <int LOGN>
-__device__ __forceinline__ void moddown_convert3(const u64* y, const u64* hat, int L0, const RedU& R, u64 w0, u64 w0p,
+__device__ __forceinline__ void moddown_convert3(const u64* y, const u64* hat, int L0, const RedU& R, const u64* tw,
                                                  int tid, u64* lds, u64 hi[16]) {
-    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32, CH = 2;
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
     const __amdgpu_buffer_rsrc_t ry = brsrc(y, 3 * N * 8);
     const Split30 h0 = split30(hat[0]), h1 = split30(hat[L0]), h2 = split30(hat[2 * L0]);
-    const u64 m = R.q, q2 = 2 * m;
+    const u64 m = R.q;
     const int vo = tid * 8;
+    const Tw4 w4 = ld_tw4(tw);
 #pragma unroll
-    for (int ch = 0; ch < 16 / CH; ++ch) {
-        u64 v[3][2 * CH];
+    for (int ch = 0; ch < 8; ++ch) {
+        u64 v[3][4];   // k: rows ch (k = 0, 2) and ch + 8 (k = 1, 3), lower (k < 2) / upper half
 #pragma unroll
-        for (int k = 0; k < 2 * CH; ++k) {
-            const int e = (ch * CH + (k % CH)) * TH + (k >= CH ? NH : 0);
+        for (int k = 0; k < 4; ++k) {
+            const int e = (ch + 8 * (k & 1)) * TH + (k >= 2 ? NH : 0);
 #pragma unroll
             for (int w = 0; w < 3; ++w) v[w][k] = bload64(ry, vo, (w * N + e) * 8);
         }
-        u64 x[2 * CH];
+        u64 x[4];
 #pragma unroll
-        for (int k = 0; k < 2 * CH; ++k) {
+        for (int k = 0; k < 4; ++k) {
             Acc3 a = {0, 0, 0};
             acc3_mac(a, split30(v[0][k]), h0);
             acc3_mac(a, split30(v[1][k]), h1);
             acc3_mac(a, split30(v[2][k]), h2);
             x[k] = acc3_reduce_pm(a.L, a.M, a.H, R.b, R.d);
         }
-#pragma unroll
-        for (int k = 0; k < CH; ++k) {
-            const u64 tt = shoup_lazy(x[CH + k], w0, w0p, m);
-            lds[row_pad<TH>(tid, ch * CH + k)] = x[k] + tt;
-            hi[ch * CH + k] = x[k] + (q2 - tt);
-        }
+        fwd_quad_first2<TH>(x, w4, m, R.lazy, lds, tid, ch, hi);
     }
 }
 
@@ -1108,14 +1152,13 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     const u64* y = ycoef + ((size_t)r * 2 + comp) * P_ * N;
     const u64* tw = T.tw_fwd + (size_t)i * N * 2;
     const u64 halfq = T.ks_seal ? T.md_pinv[3 * T.L0 + i] : 0;
-    u64 w0, w0p;
-    ld_tw(tw, 1, w0, w0p);
     u64 hi[16];
     if (P_ == 3 && RU.cpm && !T.ks_seal) {
-        moddown_convert3<LOGN>(y, T.md_hat + i, T.L0, RU, w0, w0p, tid, lds, hi);
+        moddown_convert3<LOGN>(y, T.md_hat + i, T.L0, RU, tw, tid, lds, hi);
     } else {
+    const Tw4 w4 = ld_tw4(tw);
 #pragma unroll
-    for (int ch = 0; ch < 8; ++ch) {   // 2 pairs per chunk
+    for (int ch = 0; ch < 8; ++ch) {   // rows ch and ch + 8 of both halves per chunk
         Acc3 a3[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) a3[k] = Acc3{0, 0, 0};
@@ -1124,10 +1167,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             const Split30 hk = split30(T.md_hat[(size_t)k * T.L0 + i]);
             const u64* yk = y + (size_t)k * N + tid;
             u64 v[4];
-            v[0] = yk[(ch * 2) * TH];
-            v[1] = yk[(ch * 2 + 1) * TH];
-            v[2] = yk[(ch * 2) * TH + NH];
-            v[3] = yk[(ch * 2 + 1) * TH + NH];
+            v[0] = yk[ch * TH];
+            v[1] = yk[(ch + 8) * TH];
+            v[2] = yk[ch * TH + NH];
+            v[3] = yk[(ch + 8) * TH + NH];
 #pragma unroll
             for (int z = 0; z < 4; ++z) acc3_mac(a3[z], split30(v[z]), hk);
         }
@@ -1143,13 +1186,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             }
             if (T.ks_seal) x[z] = submod(csub(x[z], q), halfq, q);   // SEAL rounding: - floor(p/2) mod q_i
         }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {   // global stage 0: (e, e + N/2)
-            const int e = tid + (ch * 2 + k) * TH;
-            const u64 tt = shoup_lazy(x[2 + k], w0, w0p, q);
-            lds[row_pad<TH>(tid, ch * 2 + k)] = x[k] + tt;
-            hi[ch * 2 + k] = x[k] + (q2 - tt);
-        }
+        fwd_quad_first2<TH>(x, w4, q, RU.lazy, lds, tid, ch, hi);
     }
     }
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
@@ -1165,7 +1202,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
         }
         __syncthreads();
-        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL>(lds, tid, tw, q, RU.lazy, 1 + h);
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, 1>(lds, tid, tw, q, RU.lazy, 1 + h);
         // outputs in batches of 4 whose accumulator (and rotated c0) loads are issued together, with
         // the add / no-add choice outside the loop (one latency per batch, not one per coefficient);
         // buffer loads / stores with the row offsets in soffset

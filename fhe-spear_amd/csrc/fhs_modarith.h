@@ -159,8 +159,8 @@ struct Split30 {
     uint32_t lo, hi;
 };
 __device__ __forceinline__ Split30 split30(u64 x) { return Split30{(uint32_t)x & 0x3FFFFFFFu, (uint32_t)(x >> 30)}; }
-__device__ __forceinline__ u64 pack30(u64 x) { return (u64)(((uint32_t)x) & 0x3FFFFFFFu) | ((x >> 30) << 32); }
-__device__ __forceinline__ Split30 unpack30(u64 p) { return Split30{(uint32_t)p, (uint32_t)(p >> 32)}; }
+__host__ __device__ __forceinline__ u64 pack30(u64 x) { return (u64)(((uint32_t)x) & 0x3FFFFFFFu) | ((x >> 30) << 32); }
+__host__ __device__ __forceinline__ Split30 unpack30(u64 p) { return Split30{(uint32_t)p, (uint32_t)(p >> 32)}; }
 __device__ __forceinline__ void acc3_mac(Acc3& a, Split30 x, Split30 y) {
     a.L += mul32w(x.lo, y.lo);
     a.M += mul32w(x.lo, y.hi);
@@ -184,6 +184,52 @@ __host__ __device__ __forceinline__ u64 acc3_reduce_pm(u64 L, u64 M, u64 H, unsi
     const u64 Sh = (hi << (64 - b)) | (lo >> b);
     return (lo & ((1ull << b) - 1)) + (u64)(uint32_t)Sh * d;
 }
+// ---- X form of the centred base extension of a full 3-limb digit (DESIGN.md §3 "ModUp X form";
+// k_centered_x / modup_convert3x in fhs_kernels.hip, the host tables in fhs_host.hip
+// modup_xform_tables).  D = the digit's 32-word table: Q_S/q_u (2 words each, u < 3), the rounding
+// thresholds ((2k - 1) Q_S + 1)/2 (k = 1..3) and 2^179 - v Q_S (v = 0..3), 3 words each.
+typedef unsigned __int128 u128x;
+__host__ __device__ __forceinline__ bool ge192(const u64 s[3], const u64* t) {
+    return s[2] != t[2] ? s[2] > t[2] : (s[1] != t[1] ? s[1] > t[1] : s[0] >= t[0]);
+}
+// y[u] (< q_u) -> U = X + 2^179 as split-30 packed base-2^60 words, X = S - v Q_S the centred digit
+// value: S = sum_u y_u Q_S/q_u < 3 Q_S, v = round(S/Q_S) (never a tie: Q_S is odd), |X| < Q_S/2 < 2^176
+__host__ __device__ __forceinline__ void centered_x_pack(const u64 y[3], const u64* D, u64 out[3]) {
+    u128x lo = 0;   // S below 2^128
+    u64 s2 = 0;     // S >> 128
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const u128x a = (u128x)y[k] * D[2 * k], b = (u128x)y[k] * D[2 * k + 1];   // y H = a + b 2^64
+        const u128x t = lo + a;
+        s2 += (u64)(t < a);
+        const u128x bl = b << 64;
+        lo = t + bl;
+        s2 += (u64)(b >> 64) + (u64)(lo < bl);
+    }
+    const u64 s[3] = {(u64)lo, (u64)(lo >> 64), s2};
+    const int v = (int)ge192(s, D + 6) + (int)ge192(s, D + 9) + (int)ge192(s, D + 12);
+    const u64* C = D + 15 + 3 * v;
+    const u128x c01 = (u128x)C[0] | ((u128x)C[1] << 64);
+    const u128x u01 = lo + c01;
+    const u64 u2 = s2 + C[2] + (u64)(u01 < c01);
+    const u64 u0 = (u64)u01, u1 = (u64)(u01 >> 64);
+    constexpr u64 M60 = (1ull << 60) - 1;
+    out[0] = pack30(u0 & M60);
+    out[1] = pack30(((u0 >> 60) | (u1 << 4)) & M60);
+    out[2] = pack30((u1 >> 56) | (u2 << 8));
+}
+// X mod m in [0, 2m) from the packed words: V0 + V1 e1 + V2 e2 + c3 with xt = {pack30(2^60 mod m),
+// pack30(2^120 mod m), -2^179 mod m}; the split-30 sums stay inside the 3-product bounds conv_pm_ok
+// proves for m (L < 2 p30^2 + 2^30 + m, M < 4 p30^2 + 2^30, H < 2 p30^2, p30 = 2^30 - 1)
+__host__ __device__ __forceinline__ u64 convert3x_value(u64 p0, u64 p1, u64 p2, Split30 e1, Split30 e2, u64 c3,
+                                                        unsigned b, unsigned d) {
+    const Split30 a = unpack30(p0), v1 = unpack30(p1), v2 = unpack30(p2);
+    const u64 L = (u64)a.lo + c3 + mul32w(v1.lo, e1.lo) + mul32w(v2.lo, e2.lo);
+    const u64 M = (u64)a.hi + mul32w(v1.lo, e1.hi) + mul32w(v1.hi, e1.lo) + mul32w(v2.lo, e2.hi) + mul32w(v2.hi, e2.lo);
+    const u64 H = mul32w(v1.hi, e1.hi) + mul32w(v2.hi, e2.hi);
+    return acc3_reduce_pm(L, M, H, b, d);
+}
+
 // c += L + M 2^30 + H 2^60 (< 2^123 for 8 products), then clear
 __device__ __forceinline__ void acc3_fold(u128& c, Acc3& a) {
     u64 lo = a.L, hi = 0;

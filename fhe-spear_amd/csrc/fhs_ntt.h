@@ -147,15 +147,16 @@ __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restric
 // Forward transform in LDS.  Entry: input (< 4q) at padded natural positions, after a barrier.
 // Exit: bit-reversed-order output, after a barrier: < 4q (Harvey) or < (4 + 2 LOGN) q when
 // `lazy` (wave-uniform; RedU::lazy); fwd_canon() maps either to [0, q).
-template <int LOGN, int RL = 3, int EPT = 16>
+// S0 > 0: stages [0, S0) were done by the caller (in registers), the passes start at stage S0.
+template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0>
 __device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, bool lazy,
                                             int hoff = 0) {
     static_assert(LOGN >= 7 && LOGN <= 14, "LDS-resident NTT supports 128 <= N <= 16384");
     static_assert(EPT >= 16 && (EPT & (EPT - 1)) == 0, "EPT must be a power of two >= 16");
     if (lazy)
-        fwd_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q, hoff);
+        fwd_from<LOGN, RL, S0, EPT, true>(lds, tid, tw, q, hoff);
     else
-        fwd_from<LOGN, RL, 0, EPT, false>(lds, tid, tw, q, hoff);
+        fwd_from<LOGN, RL, S0, EPT, false>(lds, tid, tw, q, hoff);
 }
 // Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.

@@ -277,6 +277,9 @@ fhs_status fhs_context_stream(fhs_context* ctx, void** stream);
  * the pseudo-Mersenne folds the kernels use when q qualifies (*pm_used = 1), else *pm_used = 0 and
  * *out = (hi:lo) mod q.  Exists so the CPU test suite can check the fold bounds against big ints. */
 fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* out, int* pm_used);
+/* Test hook: ModUp's X form (k_centered_x + modup_convert3x arithmetic, run on the host) of the 3-limb
+ * digit residues y3 over primes q3 into target prime m; *out = the centred digit value mod m. */
+fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* y3, uint64_t m, uint64_t* out);
 
 #ifdef __cplusplus
 }

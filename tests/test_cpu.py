@@ -300,6 +300,39 @@ def test_pseudo_mersenne_reduction_matches_bigint(orc):
     assert n_pm >= 43
 
 
+def test_modup_xform_matches_centred_extension(orc):
+    """ModUp's X form (fhs_modarith.h centered_x_pack + convert3x_value, the routines k_centered_x and
+    modup_convert3x run, here on the host through fhs_debug_modup_xform) against the centred extension
+    in big integers: X = sum_u y_u Q/q_u - round(.) Q, X mod m -- on cfg2's chain (every digit, every
+    target), with extreme residues and sums steered to within a few ulp of k + 1/2."""
+    import ctypes
+    from math import prod
+    lib = _lib()
+    U64 = ctypes.c_uint64
+    lib.fhs_debug_modup_xform.argtypes = [ctypes.POINTER(U64), ctypes.POINTER(U64), U64, ctypes.POINTER(U64)]
+    qs = orc.create_coeff_modulus(16384, [59] * 39)
+    rng = np.random.default_rng(23)
+    out = U64()
+    for j in range(12):
+        q3 = qs[3 * j:3 * j + 3]
+        Q = prod(q3)
+        cases = [[0, 0, 0], [q - 1 for q in q3], [q3[0] - 1, 0, 0], [0, 0, q3[2] - 1]]
+        for trial in range(40):
+            y = [int(rng.integers(0, q)) for q in q3]
+            if trial % 2:   # steer sum_u y_u/q_u next to k + 1/2
+                f = y[0] / q3[0] + y[1] / q3[1]
+                y[2] = (int(((np.floor(f) + 1.5 - f) % 1.0) * q3[2]) + int(rng.integers(-3, 4))) % q3[2]
+            cases.append(y)
+        targets = [t for t in range(39) if t // 3 != j]
+        for y in cases:
+            S = sum(yu * (Q // qu) for yu, qu in zip(y, q3))
+            X = S - ((2 * S + Q) // (2 * Q)) * Q
+            assert 2 * abs(X) < Q
+            for t in targets[:: max(1, len(targets) // 9)] if y not in cases[:4] else targets:
+                assert lib.fhs_debug_modup_xform((U64 * 3)(*q3), (U64 * 3)(*y), qs[t], ctypes.byref(out)) == 0
+                assert out.value == X % qs[t], (j, t, y)
+
+
 def test_device_ntt_passes_emulated_match_direct_evaluation(tmp_path):
     """fhs_ntt.h's forward (Harvey and lazy) and inverse passes, compiled for the host through a
     shim header and run thread-by-thread between barriers, against a direct O(N^2) evaluation
