@@ -180,6 +180,28 @@ __device__ __forceinline__ void fwd_quad_first2(u64 x[4], const Tw4& w, u64 q, b
     hi[c] = x[2] + tb;
     hi[c + 8] = x[2] + (q2 - tb);
 }
+// The inverse counterpart: the last two stages of a half-limb inverse in registers.  x = {half 0 row c,
+// half 0 row c + 8, half 1 row c, half 1 row c + 8} (each < 2q, after the halves' LDS passes from local
+// stage 1 on): the halves' local stage 0 (twiddle psi^-rev(2) / psi^-rev(3)), then the global stage 0
+// with (s0, s1) = N^-1 times any per-limb constant folded in.  Out: {row c, row c + 8} of the lower half,
+// then of the upper half, each < 2q.
+__device__ __forceinline__ void inv_quad_last2(u64 x[4], const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s, u64 s1,
+                                               u64 s1s) {
+    const u64 q2 = 2 * q;
+#pragma unroll
+    for (int k = 0; k < 4; k += 2) {
+        u64 w, wp;
+        ld_tw(tw, 2 + k / 2, w, wp);
+        const u64 X = x[k], Y = x[k + 1], S = X + Y;
+        x[k] = S >= q2 ? S - q2 : S;
+        x[k + 1] = shoup_lazy(X - Y + q2, w, wp, q);
+    }
+    const u64 a = x[0], b = x[1], c = x[2], d = x[3];
+    x[0] = shoup_lazy(a + c, s0, s0s, q);
+    x[1] = shoup_lazy(b + d, s0, s0s, q);
+    x[2] = shoup_lazy(a - c + q2, s1, s1s, q);
+    x[3] = shoup_lazy(b - d + q2, s1, s1s, q);
+}
 // forward: load(e) < 2q for every e < N; store(e, v) receives the canonical NTT value
 template <int LOGN, int RL, bool H = ntt_half<LOGN>(), class Load, class Store>
 __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restrict__ tw, const RedU& R, Load load,
@@ -195,16 +217,13 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
         for (int c = 0; c < 16; ++c) store(tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
     } else {
         constexpr int NH = N / 2, TH = N / 32;
-        const u64 q = R.q, q2 = 2 * q;
-        u64 w0, w0p;
-        ld_tw(tw, 1, w0, w0p);
+        const Tw4 w4 = ld_tw4(tw);
         u64 hi[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
+        for (int c = 0; c < 8; ++c) {   // rows c, c + 8 of both halves: global stages 0-1 in registers
             const int e = tid + c * TH;
-            const u64 xl = load(e), tt = shoup_lazy(load(e + NH), w0, w0p, q);
-            lds[row_pad<TH>(tid, c)] = xl + tt;
-            hi[c] = xl + (q2 - tt);
+            u64 x[4] = {load(e), load(e + 8 * TH), load(e + NH), load(e + NH + 8 * TH)};
+            fwd_quad_first2<TH>(x, w4, R.q, R.lazy, lds, tid, c, hi);
         }
 #pragma unroll 1
         for (int h = 0; h < 2; ++h) {
@@ -214,7 +233,7 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
                 for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
             }
             __syncthreads();
-            ntt_fwd_lds<LOGN - 1, 3>(lds, tid, tw, q, R.lazy, 1 + h);
+            ntt_fwd_lds<LOGN - 1, 3, 16, 1>(lds, tid, tw, R.q, R.lazy, 1 + h);
 #pragma unroll
             for (int c = 0; c < 16; ++c) store(h * NH + tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
         }
@@ -243,19 +262,18 @@ __device__ __forceinline__ void inv_limb(u64* lds, int tid, const u64* __restric
 #pragma unroll
             for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(h * NH + tid + c * TH);
             __syncthreads();
-            ntt_inv_half_lds<LOGN - 1, 3>(lds, tid, tw, q, 1 + h);
+            ntt_inv_half_lds<LOGN - 1, 3, 16, 1>(lds, tid, tw, q, 1 + h);   // local stage 0: inv_quad_last2
             if (h == 0) {
 #pragma unroll
                 for (int c = 0; c < 16; ++c) lo[c] = lds[row_pad<TH>(tid, c)];
             }
         }
-        const u64 q2 = 2 * q;
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-            const int e = tid + c * TH;
-            const u64 X = lo[c], Y = lds[row_pad<TH>(tid, c)];
-            store(e, csub(shoup_lazy(X + Y, s0, s0s, q), q));
-            store(NH + e, csub(shoup_lazy(X - Y + q2, s1, s1s, q), q));
+        for (int c = 0; c < 8; ++c) {
+            u64 x[4] = {lo[c], lo[c + 8], lds[row_pad<TH>(tid, c)], lds[row_pad<TH>(tid, c + 8)]};
+            inv_quad_last2(x, tw, q, s0, s0s, s1, s1s);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) store((k >> 1) * NH + tid + (c + 8 * (k & 1)) * TH, csub(x[k], q));
         }
     }
 }
@@ -475,8 +493,10 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_ks_intt(DevTables T, const
 }
 
 // k_ks_intt with half the limb in LDS (two workgroups per CU, co-resident with the half-limb ModUp
-// and the Hadamard): each half runs every inverse stage but the global last one, whose (e, e+N/2)
-// butterflies (with the N^-1 and ModUp scaling folded in) are done in registers.  Same values.
+// and the Hadamard): each half runs every inverse stage but the last two, which are done in registers
+// as a radix-4 (rows c, c + 8 of both halves: the halves' (e, e + N/4) stage, then the global (e, e + N/2)
+// one with the N^-1 and ModUp scaling folded in) -- four radix-8 LDS passes per half, no radix-2 pass.
+// Same values.
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, const u64* const* uniq, u64* acoef,
                                                                    int l, int U) {
@@ -500,20 +520,23 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
 #pragma unroll
         for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = v[c];
         __syncthreads();
-        ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL>(lds, tid, tw, q, 1 + h);
+        // every stage of the half but its local stage 0 (rows c, c + 8: done below in registers)
+        ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL, 16, 1>(lds, tid, tw, q, 1 + h);
         if (h == 0) {
 #pragma unroll
             for (int c = 0; c < 16; ++c) lo[c] = lds[row_pad<TH>(tid, c)];
         }
     }
     const u64* cst = T.modup_intt + ((size_t)l * T.L0 + i) * 4;
-    const u64 s0 = cst[0], s0s = cst[1], s1 = cst[2], s1s = cst[3], q2 = 2 * q;
+    const u64 s0 = cst[0], s0s = cst[1], s1 = cst[2], s1s = cst[3];
     const __amdgpu_buffer_rsrc_t rd = brsrc(acoef + ((size_t)u * l + i) * N, N * 8);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        const u64 X = lo[c], Y = lds[row_pad<TH>(tid, c)];
-        bstore64(csub(shoup_lazy(X + Y, s0, s0s, q), q), rd, tid * 8, c * TH * 8);
-        bstore64(csub(shoup_lazy(X - Y + q2, s1, s1s, q), q), rd, tid * 8, (NH + c * TH) * 8);
+    for (int c = 0; c < 8; ++c) {
+        u64 x[4] = {lo[c], lo[c + 8], lds[row_pad<TH>(tid, c)], lds[row_pad<TH>(tid, c + 8)]};
+        inv_quad_last2(x, tw, q, s0, s0s, s1, s1s);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            bstore64(csub(x[k], q), rd, tid * 8, ((k >> 1) * NH + (c + 8 * (k & 1)) * TH) * 8);
     }
 }
 
@@ -983,7 +1006,11 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     const int N = T.N, P_ = T.P, K = T.K, E = l + P_, dn = (l + P_ - 1) / P_;
     const int NB = N >> 8;
     int t, m;
-    if (!xcd_touter(E - t0, R * NB, t, m)) return;   // rotations of one limb t run together on one XCD
+    // t0 == 0 (hoisted rotations of one input): the rotations of one limb t run together on one XCD, so
+    // their shared extension stays in its L2.  t0 > 0 (the giant steps' special limbs): every rotation has
+    // its own input, so nothing is shared and a plain map keeps all 8 XCDs busy (an XCD map over P = 3
+    // limbs would leave 5 of them idle)
+    if (!(t0 > 0 ? plain_tm(E - t0, R * NB, t, m) : xcd_touter(E - t0, R * NB, t, m))) return;
     t += t0;
     const int r = m / NB, n = ((m % NB) << 8) + threadIdx.x;
     const int pt = t < l ? t : T.L0 + (t - l);
@@ -1590,7 +1617,7 @@ static void giant_ip_stage(const DevTables& T, const KsItem* it, const u64* cons
                            hipStream_t st, const KTimer* tm) {
     const int NB = T.N >> 8;
     FHS_TMARK(tm, KID_KS_IP, 1, st);
-    hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(T.P, R * NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R, l);
+    hipLaunchKernelGGL(k_ks_ip, dim3(T.P * R * NB), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R, l);
     hipLaunchKernelGGL(k_ks_ip_sum, dim3(xcd_grid(l, NB)), dim3(256), 0, st, T, it, uniq, b.ext, b.acc, l, R);
     FHS_TMARK(tm, KID_KS_IP, 0, st);
     FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);

@@ -162,9 +162,10 @@ __device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __rest
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.
 // Inverse on one half (h = hoff - 1) of a 2^(LOGN+1)-point inverse: all of its stages except the
 // global last one, which the caller applies to the (e, e + 2^LOGN) pairs.  Output in [0, 2q).
-template <int LOGN, int RL = 3, int EPT = 16>
+// S0 > 0: stages [0, S0) are left to the caller (done in registers afterwards).
+template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0>
 __device__ __forceinline__ void ntt_inv_half_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
-    inv_from<LOGN, RL, 0, EPT, true>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
+    inv_from<LOGN, RL, S0, EPT, true>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
 }
 template <int LOGN, int RL = 3, int EPT = 16>
 __device__ __forceinline__ void ntt_inv_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
