@@ -198,7 +198,7 @@ static void modup_xform_tables(const uint64_t* primes, int K, int L0, int dnum, 
         const uint64_t p120 = h_mulmod(p60, p60, m);
         uint64_t p179 = 1 % m;
         for (int e = 0; e < 179; ++e) p179 = h_mulmod(p179, 2, m);
-        xt[(size_t)i * 4 + 0] = pack30(p60);
+        xt[(size_t)i * 4 + 0] = p60;   // convert3x_value takes it as one 32-bit word (< 2^30 checked by the caller)
         xt[(size_t)i * 4 + 1] = pack30(p120);
         xt[(size_t)i * 4 + 2] = p179 ? m - p179 : 0;
     }
@@ -831,7 +831,9 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     // generic loop is then not compiled into the kernel), one-limb digits, or the generic loop
     bool all_cpm = true;
     for (int i = 0; i < K; ++i) all_cpm = all_cpm && ((pk[i].pm >> 40) & 1);
-    T.modup_dp = (P == 3 && L0 % 3 == 0 && all_cpm) ? 3 : (P == 1 ? 1 : 0);
+    bool small_e1 = true;   // the X form's weight 2^60 mod m below 2^30 for every prime (modup_xform_tables)
+    for (int i = 0; i < K && P == 3; ++i) small_e1 = small_e1 && mu_xt[(size_t)i * 4] < (1ull << 30);
+    T.modup_dp = (P == 3 && L0 % 3 == 0 && all_cpm && small_e1) ? 3 : (P == 1 ? 1 : 0);
     HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");
     HIPCHK(up(twf.data(), 8 * twf.size(), (const void**)&T.tw_fwd), "tables");
     HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");
@@ -2912,7 +2914,8 @@ extern "C" fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* 
     uint64_t words[3];
     centered_x_pack(y3, xd, words);
     const uint64_t* t = xt + 12;
-    const uint64_t x = convert3x_value(words[0], words[1], words[2], unpack30(t[0]), unpack30(t[1]), t[2],
+    if (t[0] >= (1ull << 30)) return fail(FHS_ERR_INVALID, "debug_modup_xform: 2^60 mod m >= 2^30 (no X form)");
+    const uint64_t x = convert3x_value(words[0], words[1], words[2], (uint32_t)t[0], unpack30(t[1]), t[2],
                                        (unsigned)(w & 127), (unsigned)(w >> 8));
     if (x >= 2 * m) return fail(FHS_ERR_INVALID, "debug_modup_xform: result above 2m");
     *out = x >= m ? x - m : x;

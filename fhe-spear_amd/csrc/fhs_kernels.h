@@ -21,7 +21,7 @@ struct DevTables {
     const u64* modup_xd;      // [dnum][32]  X form of full 3-limb digits (k_centered_x): Q_S/q_u (2 words
                               // each), rounding thresholds ((2k-1) Q_S + 1)/2 for k = 1..3, 2^179 - v Q_S
                               // for v = 0..3 (3 words each); null unless P = 3
-    const u64* modup_xt;      // [K][4]  per prime m: pack30(2^60 mod m), pack30(2^120 mod m), -2^179 mod m
+    const u64* modup_xt;      // [K][4]  per prime m: 2^60 mod m (< 2^30), pack30(2^120 mod m), -2^179 mod m
     const u64* md_intt;       // [P][4]  INTT constants with inv(P/p_k) folded in
     const u64* md_hat;        // [P][L0]  (P / p_k) mod q_i
     const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup; then [L0] P mod q_i; then [L0] floor(p/2) mod q_i (P = 1)
@@ -37,7 +37,8 @@ struct DevTables {
     int ks_seal;
     int max_qbits;            // bits of the largest prime (<= 59: split-30 high halves < 2^29, fewer folds)
     int modup_dp;             // ModUp conversion compiled for this shape: 3 (P = 3, all targets pseudo-
-                              // Mersenne: modup_convert3x only, at levels l % 3 == 0), 1 (P = 1:
+                              // Mersenne with 2^60 mod m < 2^30: modup_convert3x only, at levels
+                              // l % 3 == 0), 1 (P = 1:
                               // modup_convert1), 0 (generic)
 };
 // ModUp of level l reads the X form (k_centered_x + modup_convert3x) instead of residues + counts

@@ -753,7 +753,8 @@ __device__ __forceinline__ void modup_convert3x(const u64* yb, const u64* xt, co
                                                 u64* lds, u64 hi[16]) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32, CH = FHS_MODUPH_CH;
     const __amdgpu_buffer_rsrc_t ry = brsrc(yb, 3 * N * 8);
-    const Split30 e1 = unpack30(xt[0]), e2 = unpack30(xt[1]);
+    const uint32_t e1 = (uint32_t)xt[0];
+    const Split30 e2 = unpack30(xt[1]);
     const u64 c3 = xt[2], m = R.q, q2 = 2 * m;
     const int vo = tid * 8;
     const Tw4 w4 = ld_tw4(tw);

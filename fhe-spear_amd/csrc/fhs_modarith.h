@@ -218,15 +218,16 @@ __host__ __device__ __forceinline__ void centered_x_pack(const u64 y[3], const u
     out[1] = pack30(((u0 >> 60) | (u1 << 4)) & M60);
     out[2] = pack30((u1 >> 56) | (u2 << 8));
 }
-// X mod m in [0, 2m) from the packed words: V0 + V1 e1 + V2 e2 + c3 with xt = {pack30(2^60 mod m),
-// pack30(2^120 mod m), -2^179 mod m}; the split-30 sums stay inside the 3-product bounds conv_pm_ok
-// proves for m (L < 2 p30^2 + 2^30 + m, M < 4 p30^2 + 2^30, H < 2 p30^2, p30 = 2^30 - 1)
-__host__ __device__ __forceinline__ u64 convert3x_value(u64 p0, u64 p1, u64 p2, Split30 e1, Split30 e2, u64 c3,
+// X mod m in [0, 2m) from the packed words: V0 + V1 e1 + V2 e2 + c3 with xt = {2^60 mod m (< 2^30: the
+// host requires it -- 2d or d for the usual 59/60-bit q = 2^b - d), pack30(2^120 mod m), -2^179 mod m};
+// the split-30 sums stay inside the 3-product bounds conv_pm_ok proves for m (L < 2 p30^2 + 2^30 + m,
+// M < 3 p30^2 + 2^30, H < p30^2, p30 = 2^30 - 1)
+__host__ __device__ __forceinline__ u64 convert3x_value(u64 p0, u64 p1, u64 p2, uint32_t e1, Split30 e2, u64 c3,
                                                         unsigned b, unsigned d) {
     const Split30 a = unpack30(p0), v1 = unpack30(p1), v2 = unpack30(p2);
-    const u64 L = (u64)a.lo + c3 + mul32w(v1.lo, e1.lo) + mul32w(v2.lo, e2.lo);
-    const u64 M = (u64)a.hi + mul32w(v1.lo, e1.hi) + mul32w(v1.hi, e1.lo) + mul32w(v2.lo, e2.hi) + mul32w(v2.hi, e2.lo);
-    const u64 H = mul32w(v1.hi, e1.hi) + mul32w(v2.hi, e2.hi);
+    const u64 L = (u64)a.lo + c3 + mul32w(v1.lo, e1) + mul32w(v2.lo, e2.lo);
+    const u64 M = (u64)a.hi + mul32w(v1.hi, e1) + mul32w(v2.lo, e2.hi) + mul32w(v2.hi, e2.lo);
+    const u64 H = mul32w(v2.hi, e2.hi);
     return acc3_reduce_pm(L, M, H, b, d);
 }
 

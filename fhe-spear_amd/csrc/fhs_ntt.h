@@ -32,12 +32,17 @@ __device__ __forceinline__ int row_pad(int tid, int c) {
     else
         return lds_pad(tid + c * TH);
 }
+// When TL divides 16 and a group's span TL GS is a multiple of 16, the group's start j0 = blk TL GS + off
+// has j0 % 16 = off < TL, so (j0 + k TL) >> 4 = (j0 >> 4) + (k TL) / 16: again base plus a compile-time
+// offset (the radix-8 pass with TL = 8 of the half-limb transforms that start at stage 1).
 template <int TL, int GS>
 __device__ __forceinline__ int grp_pad(int j0, int base, int k) {
     if constexpr (TL % 16 == 0)
         return base + k * (TL + TL / 16);
     else if constexpr (16 % (TL * GS) == 0)
         return base + k * TL;
+    else if constexpr (16 % TL == 0 && (TL * GS) % 16 == 0)
+        return base + k * TL + (k * TL) / 16;
     else
         return lds_pad(j0 + k * TL);
 }
