@@ -1432,15 +1432,20 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: the diagonal pointers come by scalar loads
     const size_t S = (size_t)l * N;
     const size_t off = (size_t)i * N + n0 + lane * VEC;
-    // the first 8 diagonals of this wave's first group are requested before the baby-step slice is
-    // staged, so the staging and its barrier overlap the diagonal stream instead of stalling it
-    u64 pf[8][VEC];
-    bool have_pf = false;
-    if (g0 + wave < g1 && min(G, D - (g0 + wave) * G) >= 8) {
-        const u64* const* pg0 = pts + (size_t)(g0 + wave) * G;
+    // Rolling refill: within a giant group a wave keeps 8 diagonal loads in flight at every moment --
+    // slot u is reloaded with the next batch's diagonal u as soon as its product is formed, so the loads
+    // do not drain while the wave computes (they drain once per group, at its tail and stores).  The first
+    // batch is requested before the baby-step slice is staged, so the staging and its barrier overlap the
+    // stream too.
+    auto full_batches = [&](int g) { return g < g1 ? max(0, min(G, D - g * G)) / 8 : 0; };
+    u64 p[8][VEC];
+    const int gcur = g0 + wave;
+    int gf = gcur;   // the wave's first group with a full batch
+    while (gf < g1 && full_batches(gf) == 0) gf += WAVES;
+    if (gf < g1) {
+        const u64* const* pg0 = pts + (size_t)gf * G;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, pf[u]);
-        have_pf = true;
+        for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
     }
     for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
         const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
@@ -1448,7 +1453,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     }
     __syncthreads();
     const RedU R = redu(PK(T, i));
-    for (int g = g0 + wave; g < g1; g += WAVES) {
+    for (int g = gcur; g < g1; g += WAVES) {
         const int bmax = min(G, D - g * G);
         if (bmax <= 0) continue;
         u128 c0[VEC], c1[VEC];
@@ -1459,43 +1464,51 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
             a0[v] = a1[v] = Acc3{0, 0, 0};
         }
         const u64* const* pg = pts + (size_t)g * G;
+        const int nb = bmax / 8;
+        // the wave's next group with a full batch (its first batch is what the last batch here refills)
+        int gn = g + WAVES;
+        while (gn < g1 && full_batches(gn) == 0) gn += WAVES;
         int b = 0;
-        // 8 diagonal loads in flight per wave-iteration, folded into the 128-bit sums every 8
-        for (; b + 8 <= bmax; b += 8) {
-            u64 p[8][VEC];
-            if (have_pf) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) p[u][v] = pf[u][v];
-                have_pf = false;
-            } else
-            {
+        for (int bi = 0; bi < nb; ++bi, b += 8) {
+            // slot u's refill: this group's next batch (none after the last: the tail, folds and stores
+            // below run with the slots dead, and the next group's first batch is requested after them).
+            // FOLD == 8 (a prime >= 2^59) keeps batch-at-a-time loads: its extra folds leave no registers
+            // for live refills (spills)
+            constexpr bool ROLL = FOLD == 16;
+            if (!ROLL && bi > 0) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
             }
+            const u64* const* nxt = ROLL && bi + 1 < nb ? pg + b + 8 : nullptr;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
+            for (int h = 0; h < 8; h += 4) {   // half a batch at a time: products, then that half's refill
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) {
-                    const Split30 y = split30(p[u][v]);
-                    acc3_mac(a0[v], unpack30(sb[((b + u) * 2 + 0) * W + lane * VEC + v]), y);
-                    acc3_mac(a1[v], unpack30(sb[((b + u) * 2 + 1) * W + lane * VEC + v]), y);
+                for (int u = h; u < h + 4; ++u)
+#pragma unroll
+                    for (int v = 0; v < VEC; ++v) {
+                        const Split30 y = split30(p[u][v]);
+                        acc3_mac(a0[v], unpack30(sb[((b + u) * 2 + 0) * W + lane * VEC + v]), y);
+                        acc3_mac(a1[v], unpack30(sb[((b + u) * 2 + 1) * W + lane * VEC + v]), y);
+                    }
+                if (h == 4 && (FOLD == 8 || (b & 15) == 8)) {   // fold after every FOLD products (b is the
+#pragma unroll                                                       // batch's first index), before the refill
+                    for (int v = 0; v < VEC; ++v) {
+                        acc3_fold(c0[v], a0[v]);
+                        acc3_fold(c1[v], a1[v]);
+                    }
                 }
-            if (FOLD == 8 || (b & 15) == 8) {   // b is the batch's first index: fold after every FOLD products
+                if (nxt) {
 #pragma unroll
-                for (int v = 0; v < VEC; ++v) {
-                    acc3_fold(c0[v], a0[v]);
-                    acc3_fold(c1[v], a1[v]);
+                    for (int u = h; u < h + 4; ++u) ld_diag<VEC>(nxt[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
                 }
             }
         }
         for (; b < bmax; ++b) {   // < 8 left: at most FOLD - 1 products since the last fold
-            u64 p[VEC];
-            ld_diag<VEC>(pg[b] + (size_t)i * N, lane * VEC * 8, n0 * 8, p);
+            u64 q1[VEC];
+            ld_diag<VEC>(pg[b] + (size_t)i * N, lane * VEC * 8, n0 * 8, q1);
 #pragma unroll
             for (int v = 0; v < VEC; ++v) {
-                const Split30 y = split30(p[v]);
+                const Split30 y = split30(q1[v]);
                 acc3_mac(a0[v], unpack30(sb[(b * 2 + 0) * W + lane * VEC + v]), y);
                 acc3_mac(a1[v], unpack30(sb[(b * 2 + 1) * W + lane * VEC + v]), y);
             }
@@ -1509,6 +1522,11 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
         for (int v = 0; v < VEC; ++v) {
             inner[(size_t)g * 2 * S + off + v] = reduce128(c0[v].lo, c0[v].hi, R);
             inner[(size_t)g * 2 * S + S + off + v] = reduce128(c1[v].lo, c1[v].hi, R);
+        }
+        if (gn < g1) {
+            const u64* const* pgn = pts + (size_t)gn * G;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) ld_diag<VEC>(pgn[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
         }
     }
 }
