@@ -516,6 +516,37 @@ def test_bsgs_matches_oracle_on_cfg2_ring(ph):
     assert np.array_equal(y.to_numpy(), want)
 
 
+@pytest.mark.parametrize("bits", [59, 60])
+def test_bsgs_full_batches_match_oracle(ph, bits):
+    """Shapes the small oracle tests above miss: G = 23 (two full 8-diagonal batches plus a tail per giant
+    group, the Hadamard's rolling refill) and B = 23 (waves with two giant groups, the next group's
+    first batch requested after a group's stores), with 59-bit primes (16 products per fold, lazy NTT)
+    and 60-bit ones (8 per fold and batch-at-a-time loads, Harvey NTT, the X form at b = 60) -- the
+    hoisted baby steps and the fused BSGS bit-identical to the oracle's loop (bg:215-220, bg:464-485)."""
+    N, L0, P, D, seed = 1024, 6, 3, 512, 41
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    assert (G, B) == (23, 23)
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, bits=bits, seed=seed)
+    gk = sk.create_galois_keys(ctx)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(seed)
+    rng = np.random.default_rng(bits)
+    a = rand_ct(o, rng, 2, L0)
+    ct = ph.ciphertext_from_numpy(ctx, a, 1, 2.0 ** 40)
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    bkeys = {b: o.gen_galois_key(seed, s, ph.get_elt_from_step(b, N)) for b in range(1, G)}
+    want_baby = [a] + [o.rotate_elt(a, bkeys[b], ph.get_elt_from_step(b, N)) for b in range(1, G)]
+    for b in range(G):
+        assert np.array_equal(baby[b].to_numpy(), want_baby[b]), f"baby step {b}"
+    pts = ph.random_plaintexts(ctx, 17, D, 1, 2.0 ** 40)
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    gkeys = [None] + [o.gen_galois_key(seed, s, ph.get_elt_from_step(g * G, N)) for g in range(1, B)]
+    want = o.bsgs_loop(want_baby, [p.to_numpy() for p in pts], gkeys, G, B, D)
+    assert np.array_equal(y.to_numpy(), want)
+
+
 def test_n32768_encode_bsgs_and_fused_equals_loop(ph):
     """cfg5's ring size (N = 32768, BASELINE configs[4]): every NTT runs in its half-limb form and
     the encoder FFT in its split form; decode accuracy, fused BSGS == op-by-op loop, and the
