@@ -765,6 +765,20 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     std::vector<uint64_t> mu_xd((size_t)dnum * 32, 0), mu_xt((size_t)K * 4, 0);
     if (P == 3) modup_xform_tables(primes, K, L0, dnum, mu_xd.data(), mu_xt.data());
     // ---- ModDown tables
+    // X form of the special digit (fhs_kernels.hip k_special_x): Y = sum_k y_k (P/p_k) < 3P stored as
+    // base-2^60 words -- no centring (thresholds all ones), no offset (C_0 = 0); needs 3P < 2^180, so
+    // special primes below 2^59
+    std::vector<uint64_t> md_xd(32, 0);
+    bool md_x_ok = P == 3;
+    for (int k = 0; k < P && md_x_ok; ++k) md_x_ok = primes[L0 + k] < (1ull << 59);
+    if (md_x_ok) {
+        for (int u = 0; u < 3; ++u) {
+            const hu128 h = (hu128)primes[L0 + (u + 1) % 3] * primes[L0 + (u + 2) % 3];
+            md_xd[2 * u] = (uint64_t)h;
+            md_xd[2 * u + 1] = (uint64_t)(h >> 64);
+        }
+        for (int w = 6; w < 15; ++w) md_xd[w] = ~0ull;
+    }
     std::vector<uint64_t> md_intt((size_t)P * 4), md_hat((size_t)P * L0), md_pinv((size_t)4 * L0);
     for (int k = 0; k < P; ++k) {
         const int pi = L0 + k;
@@ -834,6 +848,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     bool small_e1 = true;   // the X form's weight 2^60 mod m below 2^30 for every prime (modup_xform_tables)
     for (int i = 0; i < K && P == 3; ++i) small_e1 = small_e1 && mu_xt[(size_t)i * 4] < (1ull << 30);
     T.modup_dp = (P == 3 && L0 % 3 == 0 && all_cpm && small_e1) ? 3 : (P == 1 ? 1 : 0);
+    T.md_xform = T.modup_dp == 3 && md_x_ok;
     HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");
     HIPCHK(up(twf.data(), 8 * twf.size(), (const void**)&T.tw_fwd), "tables");
     HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");
@@ -843,6 +858,7 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(mu_Q.data(), 8 * mu_Q.size(), (const void**)&T.modup_Q), "tables");
     HIPCHK(up(mu_xd.data(), 8 * mu_xd.size(), (const void**)&T.modup_xd), "tables");
     HIPCHK(up(mu_xt.data(), 8 * mu_xt.size(), (const void**)&T.modup_xt), "tables");
+    HIPCHK(up(md_xd.data(), 8 * md_xd.size(), (const void**)&T.md_xd), "tables");
     HIPCHK(up(md_intt.data(), 8 * md_intt.size(), (const void**)&T.md_intt), "tables");
     HIPCHK(up(md_hat.data(), 8 * md_hat.size(), (const void**)&T.md_hat), "tables");
     HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
@@ -2919,6 +2935,31 @@ extern "C" fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* 
                                        (unsigned)(w & 127), (unsigned)(w >> 8));
     if (x >= 2 * m) return fail(FHS_ERR_INVALID, "debug_modup_xform: result above 2m");
     *out = x >= m ? x - m : x;
+    return FHS_OK;
+}
+// ModDown's X form on the host (k_special_x + moddown_convert3x arithmetic): y3 (special residues < p_k,
+// already scaled by inv(P/p_k)) -> (sum_k y_k P/p_k) mod q, the fast base conversion's value.
+extern "C" fhs_status fhs_debug_moddown_xform(const uint64_t* p3, const uint64_t* y3, uint64_t q, uint64_t* out) {
+    if (!p3 || !y3 || !out) return FHS_ERR_INVALID;
+    const uint64_t w = pm_word(q, 14);
+    if (!w || !conv_pm_ok(q, 3)) return fail(FHS_ERR_INVALID, "debug_moddown_xform: target not on the pseudo-Mersenne fold");
+    for (int k = 0; k < 3; ++k)
+        if (p3[k] >= (1ull << 59)) return fail(FHS_ERR_INVALID, "debug_moddown_xform: special primes must be < 2^59");
+    uint64_t xd[32] = {0}, xt[4] = {0};
+    for (int u = 0; u < 3; ++u) {   // as fhs_context_create's md_xd
+        const hu128 h = (hu128)p3[(u + 1) % 3] * p3[(u + 2) % 3];
+        xd[2 * u] = (uint64_t)h;
+        xd[2 * u + 1] = (uint64_t)(h >> 64);
+    }
+    for (int i = 6; i < 15; ++i) xd[i] = ~0ull;
+    modup_xform_tables(&q, 1, 0, 0, xd, xt);   // the target's weights only (no digit rows: L0 = 0)
+    if (xt[0] >= (1ull << 30)) return fail(FHS_ERR_INVALID, "debug_moddown_xform: 2^60 mod q >= 2^30");
+    uint64_t words[3];
+    centered_x_pack(y3, xd, words);
+    const uint64_t x = convert3x_value(words[0], words[1], words[2], (uint32_t)xt[0], unpack30(xt[1]), 0,
+                                       (unsigned)(w & 127), (unsigned)(w >> 8));
+    if (x >= 2 * q) return fail(FHS_ERR_INVALID, "debug_moddown_xform: result above 2q");
+    *out = x >= q ? x - q : x;
     return FHS_OK;
 }
 extern "C" fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* out, int* pm_used) {

@@ -22,6 +22,8 @@ struct DevTables {
                               // each), rounding thresholds ((2k-1) Q_S + 1)/2 for k = 1..3, 2^179 - v Q_S
                               // for v = 0..3 (3 words each); null unless P = 3
     const u64* modup_xt;      // [K][4]  per prime m: 2^60 mod m (< 2^30), pack30(2^120 mod m), -2^179 mod m
+    const u64* md_xd;         // [32]  X form of ModDown's special digit (k_special_x): P/p_k (2 words each),
+                              // thresholds never reached (no centring), 0 offset; null unless md_xform
     const u64* md_intt;       // [P][4]  INTT constants with inv(P/p_k) folded in
     const u64* md_hat;        // [P][L0]  (P / p_k) mod q_i
     const u64* md_pinv;       // [L0][2]  P^-1 mod q_i, Shoup; then [L0] P mod q_i; then [L0] floor(p/2) mod q_i (P = 1)
@@ -36,6 +38,7 @@ struct DevTables {
     // before the decomposition, ModDown rounded by adding floor(p/2)
     int ks_seal;
     int max_qbits;            // bits of the largest prime (<= 59: split-30 high halves < 2^29, fewer folds)
+    int md_xform;             // ModDown converts from the X form (P = 3 special primes < 2^59, modup_dp == 3)
     int modup_dp;             // ModUp conversion compiled for this shape: 3 (P = 3, all targets pseudo-
                               // Mersenne with 2^60 mod m < 2^30: modup_convert3x only, at levels
                               // l % 3 == 0), 1 (P = 1:

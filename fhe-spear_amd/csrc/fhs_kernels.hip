@@ -1083,6 +1083,22 @@ __global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_ks_special_intt(De
                                [&](int e) { return src[e]; }, [&](int e, u64 v) { dst[e] = csub(csub(v, p) + half, p); });
 }
 
+// (c') ModDown's special digit in X form (T.md_xform): Y = sum_k y_k (P/p_k) (< 3P < 2^179, the fast
+// base conversion's integer, no centring) once per coefficient, stored in place of the three special
+// residues as base-2^60 words (centered_x_pack with md_xd) -- each of the l targets then reduces it with
+// two split-30 products (moddown_convert3x) instead of three: the same integer, the same residues
+__global__ void k_special_x(DevTables T, u64* ycoef, int R2) {
+    const int N = T.N, n = blockIdx.x * blockDim.x + threadIdx.x, rc = blockIdx.y;
+    if (n >= N || rc >= R2) return;
+    u64* yb = ycoef + (size_t)rc * 3 * N + n;
+    const u64 y[3] = {yb[0], yb[N], yb[2 * (size_t)N]};
+    u64 w[3];
+    centered_x_pack(y, T.md_xd, w);
+    yb[0] = w[0];
+    yb[N] = w[1];
+    yb[2 * (size_t)N] = w[2];
+}
+
 // (d) ModDown: out_c[i] = (acc_c[i] - NTT(conv_P->q_i(y_c))) * P^-1 (+ add_c)
 template <int LOGN>
 __global__ void __launch_bounds__((1 << LOGN) / 16) k_moddown(DevTables T, const KsItem* items, const u64* acc,
@@ -1160,10 +1176,36 @@ __device__ __forceinline__ void moddown_convert3(const u64* y, const u64* hat, i
     }
 }
 
+// moddown_convert3 from the X form (k_special_x): x = V0 + V1 (2^60 mod q_i) + V2 (2^120 mod q_i)
+template <int LOGN>
+__device__ __forceinline__ void moddown_convert3x(const u64* y, const u64* xt, const RedU& R, const u64* tw, int tid,
+                                                  u64* lds, u64 hi[16]) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
+    const __amdgpu_buffer_rsrc_t ry = brsrc(y, 3 * N * 8);
+    const uint32_t e1 = (uint32_t)xt[0];
+    const Split30 e2 = unpack30(xt[1]);
+    const int vo = tid * 8;
+    const Tw4 w4 = ld_tw4(tw);
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {
+        u64 v[3][4];   // k: rows ch (k = 0, 2) and ch + 8 (k = 1, 3), lower (k < 2) / upper half
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = (ch + 8 * (k & 1)) * TH + (k >= 2 ? NH : 0);
+#pragma unroll
+            for (int w = 0; w < 3; ++w) v[w][k] = bload64(ry, vo, (w * N + e) * 8);
+        }
+        u64 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = convert3x_value(v[0][k], v[1][k], v[2][k], e1, e2, 0, R.b, R.d);
+        fwd_quad_first2<TH>(x, w4, R.q, R.lazy, lds, tid, ch, hi);
+    }
+}
+
 // k_moddown with half the limb in LDS (see k_modup_h): conversion of both coefficients of each
 // (e, e + N/2) pair, global NTT stage 0 in registers, then each half transformed in LDS and finished
 // ((acc - conv) P^-1 + sigma(c0)).  Same values as k_moddown.
-template <int LOGN>
+template <int LOGN, bool MX>
 __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, const KsItem* items, const u64* acc,
                                                                    const u64* ycoef, int l, int R) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
@@ -1181,7 +1223,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     const u64* tw = T.tw_fwd + (size_t)i * N * 2;
     const u64 halfq = T.ks_seal ? T.md_pinv[3 * T.L0 + i] : 0;
     u64 hi[16];
-    if (P_ == 3 && RU.cpm && !T.ks_seal) {
+    if constexpr (MX) {   // T.md_xform: y holds the special digit's X form
+        moddown_convert3x<LOGN>(y, T.modup_xt + (size_t)i * 4, RU, tw, tid, lds, hi);
+    } else if (P_ == 3 && RU.cpm && !T.ks_seal) {
         moddown_convert3<LOGN>(y, T.md_hat + i, T.L0, RU, tw, tid, lds, hi);
     } else {
     const Tw4 w4 = ld_tw4(tw);
@@ -1390,9 +1434,16 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
         u64 *acc, *ycoef;
         ks_front<LOGN>(T, it, uq, R, U, l, ws, st, tm, &acc, &ycoef);
         FHS_TMARK(tm, KID_MODDOWN, 1, st);
-        if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>())
-            hipLaunchKernelGGL((k_moddown_h<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc, ycoef, l, R);
-        else
+        if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
+            if (T.md_xform) {   // the special digit to its X form, then the two-product conversion
+                hipLaunchKernelGGL(k_special_x, dim3((T.N + 255) / 256, 2 * R), dim3(256), 0, st, T, ycoef, 2 * R);
+                hipLaunchKernelGGL((k_moddown_h<LOGN, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc,
+                                   ycoef, l, R);
+            } else {
+                hipLaunchKernelGGL((k_moddown_h<LOGN, false>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it,
+                                   acc, ycoef, l, R);
+            }
+        } else
         hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
         FHS_TMARK(tm, KID_MODDOWN, 0, st);
     });

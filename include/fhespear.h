@@ -280,6 +280,9 @@ fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* o
 /* Test hook: ModUp's X form (k_centered_x + modup_convert3x arithmetic, run on the host) of the 3-limb
  * digit residues y3 over primes q3 into target prime m; *out = the centred digit value mod m. */
 fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* y3, uint64_t m, uint64_t* out);
+/* Test hook: ModDown's X form (k_special_x + moddown_convert3x arithmetic, on the host): special residues y3
+ * over primes p3 (< 2^59) into target prime q; *out = (sum_k y3[k] P/p3[k]) mod q. */
+fhs_status fhs_debug_moddown_xform(const uint64_t* p3, const uint64_t* y3, uint64_t q, uint64_t* out);
 
 #ifdef __cplusplus
 }

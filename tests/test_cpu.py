@@ -333,6 +333,28 @@ def test_modup_xform_matches_centred_extension(orc):
                 assert out.value == X % qs[t], (j, t, y)
 
 
+def test_moddown_xform_matches_fast_base_conversion(orc):
+    """ModDown's X form (k_special_x + moddown_convert3x, the same __host__ __device__ routines through
+    fhs_debug_moddown_xform) against big integers: (sum_k y_k P/p_k) mod q_i, the fast base conversion's
+    value, on cfg2's 3 special primes into every data prime, with extreme residues."""
+    import ctypes
+    from math import prod
+    lib = _lib()
+    U64 = ctypes.c_uint64
+    lib.fhs_debug_moddown_xform.argtypes = [ctypes.POINTER(U64), ctypes.POINTER(U64), U64, ctypes.POINTER(U64)]
+    qs = orc.create_coeff_modulus(16384, [59] * 39)
+    p3, data = qs[36:], qs[:36]
+    P = prod(p3)
+    rng = np.random.default_rng(29)
+    out = U64()
+    cases = [[0, 0, 0], [p - 1 for p in p3]] + [[int(rng.integers(0, p)) for p in p3] for _ in range(60)]
+    for y in cases:
+        Y = sum(yk * (P // pk) for yk, pk in zip(y, p3))
+        for q in data:
+            assert lib.fhs_debug_moddown_xform((U64 * 3)(*p3), (U64 * 3)(*y), q, ctypes.byref(out)) == 0
+            assert out.value == Y % q, (q, y)
+
+
 def test_device_ntt_passes_emulated_match_direct_evaluation(tmp_path):
     """fhs_ntt.h's forward (Harvey and lazy) and inverse passes, compiled for the host through a
     shim header and run thread-by-thread between barriers, against a direct O(N^2) evaluation
