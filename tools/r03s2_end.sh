@@ -2,7 +2,7 @@
 # GPU box: end-of-session confirmation -- GPU suite and smoke, then the profile round (bench line,
 # rocprofv3 stats, FETCH/WRITE and VALU PMC passes for the hash-matched traffic record).
 set -o pipefail
-OUT=gpurun_out/r03s2_end
+OUT=gpurun_out/${1:-r03s2_end}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest.log" 2>&1 || { echo "pytest failed"; tail -5 "$OUT/pytest.log"; exit 1; }
