@@ -246,7 +246,10 @@ def main():
         step()
     ctx.synchronize()
     kprof = ph.kernel_timer_read(ctx, reset=True)
-    dom = max(kprof, key=lambda k: kprof[k][0])
+    # the dominant kernel among those with algorithmic bytes (the roofline needs them): a host stall
+    # inside one instrumented bracket must not hand the line to an unpriced kernel and a null roofline
+    priced = [k for k in kprof if kprof[k][1] and algorithmic_bytes_per_matvec(k, cfg, L0 + 1 - level)]
+    dom = max(priced or list(kprof), key=lambda k: kprof[k][0])
     # timed region: only the dominant kernel and the Hadamard kernel carry events (each event pair
     # costs ~10 us of queue time), measured live on the context stream they launch on
     ph.kernel_timer_arm(ctx, sorted({dom, "k_bsgs_inner"}))
@@ -342,7 +345,7 @@ def main():
                     "bytes_per_launch": ab // max(launches, 1), "ms_per_launch": round(ms / n, 4)}
 
         roof = roofline_of(dom)
-        if dom == "k_modup":
+        if roof and dom == "k_modup":
             roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (SQ counters: VALU issue ~75-85% of SIMD cycles, "
                             "profiles/r01), so its HBM fraction is low by construction; ntt_valu_roofline "
                             "prices it against the register-only butterfly ceiling")
