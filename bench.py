@@ -8,12 +8,17 @@ bsgs_multiply_accumulate (bg:459: 2048 ct x pt products, 44 giant-step rotations
 rescale), on a fresh encryption of a replicated input and D = 2048 pre-encoded diagonals
 resident in HBM (SURVEY.md §8d throughput workload: limbs i.i.d. uniform mod q_i).
 
-Multi-GPU (torchrun, one process per GPU): every rank runs its own projection (8 projections of
-an RWKV block, one per GPU at N=8: BASELINE configs[3]) and the output ciphertexts are gathered
-to rank 0 over RCCL every step -- weak scaling, `value` = matvecs/s summed over ranks.
+Multi-GPU (one process per GPU): every rank runs its own projection (8 projections of an RWKV block,
+one per GPU at N=8: BASELINE configs[3]) and the output ciphertexts are gathered to rank 0 over RCCL
+every step -- weak scaling, `value` = matvecs/s summed over ranks.  `--gpus N` without WORLD_SIZE in the
+environment starts the N ranks itself (torch.distributed.run as a child process, before anything
+touches the GPU); under torchrun WORLD_SIZE must equal --gpus.  Rank 0 limb-checks every rank's
+gathered output of the last timed step against the oracle digest of that rank's workload.
 
-Prints ONE JSON line on rank 0.  `roofline` is for the kernel with the largest device time inside
-the timed region (HIP events on the library's stream around every launch); `cpu_baseline` times full
+Prints ONE JSON line on rank 0.  `roofline` is for the kernel that the newest hash-matched rocprofv3
+record of this workload (profiles/r*/rocprof_summary_<config>.json, tools/rocprof_summary.py) shows
+with the longest steady-state device time per step, measured live in the timed region with HIP events
+on the library stream around its launches; `cpu_baseline` times full
 matvecs of the same workload with the in-repo SEAL-class CPU port (oracle/cpu_port.c, OpenMP on the
 host cores this process may use); `parity` checks the output limbs against the C oracle's digest.
 The measured RWKV block (`rwkv_block`) carries its own limb check at N=1: the r projection's server call
@@ -35,6 +40,11 @@ import numpy as np  # noqa: E402
 CONFIGS = {
     # BASELINE configs[1]: single BSGS matvec d=2048, N=16384, L0=36 (P=3: tf default, README.md:53)
     "cfg2": dict(N=16384, L0=36, P=3, D=2048, workload="BSGS matvec d=2048 N=16384 L0=36 P=3 (89 rotations)"),
+    # the same matvec in SEAL's switch_key_inplace convention (north_star's bit-exact claim): P = 1, one
+    # ModUp per rotation (the default line runs it as its seal_mode leg; --config cfg2seal profiles it)
+    "cfg2seal": dict(N=16384, L0=36, P=1, D=2048, mode="seal", digest="cfg2_seal",
+                     workload="BSGS matvec d=2048 N=16384 L0=36 P=1, SEAL switch_key_inplace convention "
+                              "(89 non-hoisted rotations)"),
     # BASELINE configs[0] shape (CPU-runnable case in the reference)
     "cfg1": dict(N=8192, L0=24, P=3, D=1024, workload="BSGS matvec d=1024 N=8192 L0=24 P=3 (62 rotations)"),
     "small": dict(N=4096, L0=6, P=3, D=256, workload="BSGS matvec d=256 N=4096 L0=6 P=3 (smoke size)"),
@@ -60,15 +70,16 @@ def bsgs_params(D):
 
 
 def algorithmic_bytes_per_matvec(name, cfg, l):
-    """Unique HBM bytes kernel `name` must move for one matvec (DESIGN.md §4).  Rotations of one
+    """Unique HBM bytes kernel `name` must move for one matvec (DESIGN.md §5).  Rotations of one
     input share one ModUp (hoisting): the G-1 baby rotations have one input, each of the B-1
-    giant rotations its own, so a matvec runs B ModUps for its G-1 + B-1 key-switches."""
+    giant rotations its own, so a matvec runs B ModUps for its G-1 + B-1 key-switches.  In SEAL's
+    convention (cfg mode "seal") nothing is hoisted: one ModUp per rotation."""
     N, P, D = cfg["N"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
     E, dn = l + P, (l + P - 1) // P
     w = 8 * N
     rot = (G - 1) + (B - 1)
-    modups = 1 + (B - 1)
+    modups = rot if cfg.get("mode") == "seal" else 1 + (B - 1)
     if name == "k_bsgs_inner":   # diagonals + baby steps in, B inner products out
         return w * (D * l + 2 * G * l + 2 * B * l)
     if name == "k_modup":        # digit limbs (coefficient form) in, extended limbs out
@@ -99,16 +110,71 @@ def kernel_source_hash():
 
 
 def latest_traffic_record(config):
-    """The newest profiles/r*/pmc_traffic_<config>.json whose kernel-source hash matches these
-    sources (tools/pmc_traffic.py); None when none matches (then roofline.traffic is null)."""
+    """The newest hash-matched profiles/r*/pmc_traffic_<config>.json (tools/pmc_traffic.py); (None, None)
+    when none matches (then roofline.traffic is null)."""
+    return latest_record("pmc_traffic", config)
+
+
+def latest_record(kind, config):
+    """The newest profiles/r*/<kind>_<config>.json whose kernel-source hash matches these sources
+    (tools/rocprof_summary.py, tools/pmc_valu.py write it); (None, None) when none matches."""
     want = kernel_source_hash()
     for d in sorted((REPO / "profiles").glob("r*"), reverse=True):
-        f = d / f"pmc_traffic_{config}.json"
+        f = d / f"{kind}_{config}.json"
         if f.exists():
             rec = json.loads(f.read_text())
             if rec.get("kernel_source_sha256_16") == want:
                 return rec, str(f.relative_to(REPO))
     return None, None
+
+
+def kernel_roofline(name, ktimes, steps, cfg, l, traffic_rec, valu_rec, rrec):
+    """HBM roofline of kernel family `name` from its live HIP-event time over `steps` timed steps
+    (ktimes: name -> (ms, launches)): algorithmic bytes per launch (algorithmic_bytes_per_matvec /
+    launches) over the average launch duration.  traffic: HBM-side bytes per launch from the hash-matched
+    rocprofv3 PMC passes of this workload (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py), null when
+    absent; valu_busy from the VALU pass (tools/pmc_valu.py); rocprof_*: the same kernel's steady-state
+    time in the hash-matched rocprofv3 trace record (tools/rocprof_summary.py)."""
+    traffic, tsrc = traffic_rec
+    valu_k, vsrc = valu_rec
+    ms, n = ktimes.get(name, (0.0, 0))
+    ab = algorithmic_bytes_per_matvec(name, cfg, l)
+    if not ab or not n:
+        return None
+    launches = max(n // steps, 1)
+    ach = ab / (ms / steps * 1e-3) / 1e9
+    tr = traffic.get(name) or traffic.get(name + "_h")   # half-limb variant names
+    tr_step = tr["traffic_bytes_per_step"] if tr else None
+    vb = valu_k.get(name) or valu_k.get(name + "_h")
+    out = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": int(tr_step / launches) if tr else None,
+           "traffic_source": tsrc if tr else None,
+           "traffic_over_algorithmic": round(tr_step / ab, 3) if tr else None,
+           "bytes_per_launch": ab // launches, "launches_per_step": launches,
+           "ms_per_step": round(ms / steps, 4), "ms_per_launch": round(ms / n, 4),
+           "valu_busy": vb["valu_busy"] if vb else None, "valu_source": vsrc if vb else None}
+    if rrec and name in rrec.get("kernels", {}):
+        rk = rrec["kernels"][name]
+        out["rocprof_ms_per_step"] = rk["ms_per_step"]
+        out["rocprof_frac"] = round(ab / (rk["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    return out
+
+
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` run directly: start the N ranks (one process per GPU) with
+    torch.distributed.run as a child process and exit with its status.  Nothing here has touched the
+    GPU (torch is not even imported), so no process that initialised HIP is replaced."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
 
 
 def limb_digest_check(config, limbs, suffix=""):
@@ -163,6 +229,13 @@ def main():
                     help="cfg3 over N GPUs: latency mode, giant steps of each projection sharded over a rank group")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:     # the driver's plain `bench.py --gpus N`: start N ranks
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (launch with --nproc-per-node "
+              f"{args.gpus}, or run without torchrun and let --gpus start the ranks)", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -195,6 +268,8 @@ def main():
     parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(steps, N))))
     parms.set_coeff_modulus(primes)
     ctx = ph.context(parms, device=local)
+    if cfg.get("mode") == "seal":
+        ctx.set_key_switch_mode("seal")
     sk = ph.secret_key(ctx, seed=SK_SEED + rank)
     gk = sk.create_galois_keys(ctx)
     scale = 2.0 ** 59
@@ -214,6 +289,8 @@ def main():
         gather_buf = torch.empty(out_words, dtype=torch.int64, device=f"cuda:{local}")
         import fhespear_dist
 
+    gathered = [None]
+
     def step():
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
@@ -223,9 +300,9 @@ def main():
             torch.cuda.current_stream().synchronize()
             ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
             if dist.get_backend() == "gloo":
-                fhespear_dist.gather_to_root(dist, gather_buf.cpu(), world, rank)
+                gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf.cpu(), world, rank)
             else:
-                fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
+                gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
         return y
 
     for _ in range(args.warmup):
@@ -246,13 +323,20 @@ def main():
         step()
     ctx.synchronize()
     kprof = ph.kernel_timer_read(ctx, reset=True)
-    # the dominant kernel among those with algorithmic bytes (the roofline needs them): a host stall
-    # inside one instrumented bracket must not hand the line to an unpriced kernel and a null roofline
+    # the roofline kernel, by a fixed rule: the priced kernel (one with algorithmic bytes) with the
+    # longest steady-state device time per step in the newest rocprofv3 record of this workload whose
+    # kernel-source hash matches these sources (tools/rocprof_summary.py); without such a record, the
+    # longest priced kernel of the instrumented pass above
+    rrec, rsrc = latest_record("rocprof_summary", args.config)
     priced = [k for k in kprof if kprof[k][1] and algorithmic_bytes_per_matvec(k, cfg, L0 + 1 - level)]
-    dom = max(priced or list(kprof), key=lambda k: kprof[k][0])
-    # timed region: only the dominant kernel and the Hadamard kernel carry events (each event pair
-    # costs ~10 us of queue time), measured live on the context stream they launch on
-    ph.kernel_timer_arm(ctx, sorted({dom, "k_bsgs_inner"}))
+    if rrec and rrec.get("longest_matvec_kernel") in priced:
+        dom, dom_rule = rrec["longest_matvec_kernel"], f"longest priced kernel per step in {rsrc} (rocprofv3)"
+    else:
+        dom = max(priced or list(kprof), key=lambda k: kprof[k][0])
+        dom_rule = "longest priced kernel of this run's instrumented pass (no hash-matched rocprof record)"
+    # timed region: the ModUp and Hadamard kernels (and the dominant one) carry events, measured live on
+    # the context stream they launch on (each event pair costs ~10 us of queue time)
+    ph.kernel_timer_arm(ctx, sorted({dom, "k_modup", "k_bsgs_inner"}))
     barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -281,7 +365,20 @@ def main():
     # correctness guard on the timed output: the level, and on rank 0 the SHA-256 of its limbs against
     # the digest the C oracle computed for this exact workload (tests/golden/manifest.json)
     assert y.chain_index() == level + 1
-    parity = limb_digest_check(args.config, y.to_numpy()) if rank == 0 else None
+    dkey = cfg.get("digest", args.config)
+    parity = limb_digest_check(dkey, y.to_numpy()) if rank == 0 else None
+    if dist is not None and rank == 0:
+        # every rank's output of the last timed step, as gathered over RCCL (gloo in rehearsals), against
+        # the oracle digest of that rank's workload (seeds + rank, tests/golden/make_bench_digest.py --rank)
+        shape = (2, L0 - 1, N)
+        ranks = {}
+        for r, t in enumerate(gathered[0]):
+            limbs = t.cpu().numpy().view(np.uint64).reshape(shape)
+            ranks[r] = limb_digest_check(dkey, limbs, f"_rank{r}" if r else "")
+        keys = [next(k for k in v if k.endswith("_match")) for v in ranks.values()]
+        parity["gathered_outputs"] = {"ranks_checked": len(ranks),
+                                      "all_match": all(v[k] is True for v, k in zip(ranks.values(), keys)),
+                                      "per_rank": {r: v[k] for (r, v), k in zip(ranks.items(), keys)}}
 
     if dist is not None:
         import torch
@@ -328,27 +425,20 @@ def main():
 
         trec, tsrc = latest_traffic_record(args.config)
         traffic = trec["kernels"] if trec else {}
+        vrec, vsrc = latest_record("pmc_valu", args.config)
+        valu_k = vrec["kernels"] if vrec else {}
 
         def roofline_of(name):
-            ms, n = ktimes[name]
-            ab = algorithmic_bytes_per_matvec(name, cfg, l)
-            if not ab or not n:
-                return None
-            launches = n // args.steps
-            ach = ab / (ms / args.steps * 1e-3) / 1e9
-            # traffic: HBM-side bytes per launch from the committed rocprofv3 PMC passes of this
-            # workload (FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py); null when absent
-            tr = traffic.get(name) or traffic.get(name + "_h")   # half-limb variant names
-            tr_b = int(tr["traffic_bytes_per_step"] / max(tr["launches_per_step"], 1)) if tr else None
-            return {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr_b, "traffic_source": tsrc if tr_b else None,
-                    "bytes_per_launch": ab // max(launches, 1), "ms_per_launch": round(ms / n, 4)}
+            return kernel_roofline(name, ktimes, args.steps, cfg, l, (traffic, tsrc), (valu_k, vsrc), rrec)
 
         roof = roofline_of(dom)
-        if roof and dom == "k_modup":
-            roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (SQ counters: VALU issue ~75-85% of SIMD cycles, "
-                            "profiles/r01), so its HBM fraction is low by construction; ntt_valu_roofline "
-                            "prices it against the register-only butterfly ceiling")
+        if roof is not None:
+            roof["selection"] = dom_rule
+        mu_roof = roofline_of("k_modup")
+        if mu_roof is not None:
+            mu_roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (valu_busy: SQ_ACTIVE_INST_VALU x 4 over SIMD "
+                               "cycles), so its HBM fraction is low by construction; ntt_valu_roofline prices it "
+                               "against the register-only butterfly ceiling")
         had_roof = roofline_of("k_bsgs_inner")
         mu_ms = (ktimes["k_modup"][0] / args.steps if ktimes["k_modup"][1]
                  else kprof["k_modup"][0] / prof_steps)
@@ -404,6 +494,7 @@ def main():
             "seal_mode_value": seal.get("value") if seal else None,
             "seal_mode": seal,
             "roofline": roof,
+            "modup_roofline": mu_roof,
             "hadamard_roofline": had_roof,
             "ntt_valu_roofline": valu,
             "matvec_roofline": matvec_roof,
@@ -411,7 +502,14 @@ def main():
             "parity": parity,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args)
+            res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args, cfg.get("mode", "exact"))
+            if seal is not None and "error" not in seal:
+                # the SEAL-convention leg's own CPU baseline: the same matvec in the same convention
+                try:
+                    seal["cpu_baseline"] = cpu_baseline(CONFIGS["cfg2seal"], seal.pop("_primes"), args, "seal")
+                    seal["gpu_over_cpu"] = round(seal["value"] / seal["cpu_baseline"]["value"], 1)
+                except Exception as e:   # reported, never hidden
+                    seal["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"[:400]}
             cap = block.pop("_capture", None) if isinstance(block, dict) else None
             if cap is not None:
                 try:
@@ -420,6 +518,8 @@ def main():
                     block["parity"] = {"error": f"{type(e).__name__}: {e}"[:400]}
         elif isinstance(block, dict):
             block.pop("_capture", None)
+        if isinstance(seal, dict):
+            seal.pop("_primes", None)
         print(json.dumps(res))
     if dist is not None:
         dist.barrier()
@@ -429,28 +529,49 @@ def main():
 def seal_leg(args, ph, cfg):
     """cfg2's matvec with context.set_key_switch_mode('seal'): primes [59] x (L0 + 1), one special
     prime, SEAL's switch_key_inplace per rotation (DESIGN.md §3 SEAL convention).  Same seeds as the
-    main leg; output limbs checked against the oracle's digest of this mode (bench_digests cfg2_seal)."""
-    N, L0, D = cfg["N"], cfg["L0"], cfg["D"]
+    main leg; output limbs checked against the oracle's digest of this mode (bench_digests cfg2_seal).
+    One instrumented step gives the per-kernel breakdown; the roofline kernel is chosen as for the main
+    leg (hash-matched rocprof_summary_cfg2seal record, else the instrumented step) and timed live with
+    HIP events in the timed steps; `matvec_roofline` prices the whole matvec at SURVEY §8(d)'s bytes for
+    P = 1 (diagonals + 89 keys of 36 digits x 2 x 37 limbs + ct in/out: 40.8 GB)."""
+    scfg = CONFIGS["cfg2seal"]
+    N, L0, D = scfg["N"], scfg["L0"], scfg["D"]
     G, B = bsgs_params(D)
     steps = list(range(1, G)) + [g * G for g in range(1, B)]
     parms = ph.params(ph.scheme_type.ckks)
     parms.set_poly_modulus_degree(N)
     parms.set_special_modulus_size(1)
     parms.set_galois_elts(sorted(set(ph.get_elts_from_steps(steps, N))))
-    parms.set_coeff_modulus(ph.create_coeff_modulus(N, [59] * (L0 + 1)))
+    primes = ph.create_coeff_modulus(N, [59] * (L0 + 1))
+    parms.set_coeff_modulus(primes)
     ctx = ph.context(parms)
     ctx.set_key_switch_mode("seal")
     sk = ph.secret_key(ctx, seed=SK_SEED)
     gk = sk.create_galois_keys(ctx)
     scale = 2.0 ** 59
     ct = sk.encrypt_symmetric(ctx, ph.random_plaintexts(ctx, INPUT_SEED, 1, 1, scale)[0])
-    pts = ph.random_plaintexts(ctx, DIAG_SEED, D, ct.chain_index(), scale)
+    level = ct.chain_index()
+    pts = ph.random_plaintexts(ctx, DIAG_SEED, D, level, scale)
 
     def step():
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         return ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
     step()
     ctx.synchronize()
+    ph.kernel_timer_read(ctx, reset=True)
+    ph.kernel_timer_arm(ctx, None)
+    step()
+    ctx.synchronize()
+    kprof = ph.kernel_timer_read(ctx, reset=True)
+    l = L0 + 1 - level
+    rrec, rsrc = latest_record("rocprof_summary", "cfg2seal")
+    priced = [k for k in kprof if kprof[k][1] and algorithmic_bytes_per_matvec(k, scfg, l)]
+    if rrec and rrec.get("longest_matvec_kernel") in priced:
+        dom, rule = rrec["longest_matvec_kernel"], f"longest priced kernel per step in {rsrc} (rocprofv3)"
+    else:
+        dom = max(priced or list(kprof), key=lambda k: kprof[k][0])
+        rule = "longest priced kernel of the leg's instrumented step (no hash-matched rocprof record)"
+    ph.kernel_timer_arm(ctx, [dom])
     evs = []
     for _ in range(args.seal_steps):
         e0 = ph.Event(ctx)
@@ -458,10 +579,26 @@ def seal_leg(args, ph, cfg):
         evs.append((e0, ph.Event(ctx)))
     ctx.synchronize()
     med = float(np.median([a.elapsed_ms(b) for a, b in evs]))
-    res = {"value": round(1000.0 / med, 3), "unit": "matvec/s", "median_ms_per_step": round(med, 3),
-           "steps": args.seal_steps, "P": 1, "dnum": L0, "hoisting": False,
-           "workload": f"BSGS matvec d={D} N={N} L0={L0} P=1, SEAL switch_key_inplace convention",
-           "parity": limb_digest_check("cfg2", y.to_numpy(), "_seal")}
+    ktimes = ph.kernel_timer_read(ctx, reset=True)
+    ph.kernel_timer_arm(ctx, [])
+    trec, tsrc = latest_traffic_record("cfg2seal")
+    vrec, vsrc = latest_record("pmc_valu", "cfg2seal")
+    roof = kernel_roofline(dom, ktimes, args.seal_steps, scfg, l, (trec["kernels"] if trec else {}, tsrc),
+                           (vrec["kernels"] if vrec else {}, vsrc), rrec)
+    if roof is not None:
+        roof["selection"] = rule
+    mvb = matvec_bytes(scfg, l)
+    value = 1000.0 / med
+    res = {"value": round(value, 3), "unit": "matvec/s", "median_ms_per_step": round(med, 3),
+           "steps": args.seal_steps, "P": 1, "dnum": L0, "hoisting": False, "workload": scfg["workload"],
+           "parity": limb_digest_check("cfg2", y.to_numpy(), "_seal"),
+           "roofline": roof,
+           "matvec_roofline": {"bound": "hbm", "bytes_per_matvec": mvb, "achieved": round(mvb * value / 1e9, 1),
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(mvb * value / 1e9 / HBM_PEAK_GBS, 4),
+                               "floor_matvec_per_s": round(HBM_PEAK_GBS * 1e9 / mvb, 1)},
+           "kernels": {k: {"ms_per_step": round(v[0], 3), "launches_per_step": v[1]} for k, v in kprof.items() if v[1]},
+           "_primes": [int(q) for q in primes]}
     del y, pts, ct, gk, sk
     ctx.synchronize()
     return res
@@ -617,31 +754,68 @@ def bench_block(args, ph, dist, rank, world, local):
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, primes, args):
+def cpu_baseline(cfg, primes, args, mode="exact"):
     """SURVEY.md §8(d)'s CPU baseline: the build's own CPU restatement with SEAL-class arithmetic
     (oracle/cpu_port.c: Harvey lazy NTT with Shoup twiddles, Barrett-reduced lazy sums, OpenMP), timed
     over FULL matvecs of this exact workload -- the G-1 baby rotations and the B-1 giant rotations
     issued one at a time (non-hoisted, as the reference's CPU path issues them), D multiply_plain+add,
-    the final rescale -- on the host cores this process may use (OMP_NUM_THREADS: 16 on the GPU box,
-    its share of the node).  One untimed matvec, then args.cpu_reps timed; the median is reported.
-    Its output limbs are checked against the oracle digest of the workload (the same one the GPU
-    output is checked against)."""
+    the final rescale -- on the host cores this process may use.  One untimed matvec, then
+    args.cpu_reps timed; the median is reported.  Its output limbs are checked against the oracle
+    digest of the workload (the same one the GPU output is checked against).
+    Cores: `cores` = the OpenMP threads used = the box's CPU share (OMP_NUM_THREADS, 16 on the GPU box:
+    the pool gives each GPU 16 of the node's cores, so that is what this process may use); `cores_usable`
+    records the affinity mask, the cgroup quota and that share.  The same matvec is also timed on half
+    the threads, and `whole_host_extrapolated` scales the per-core rate linearly to every physical core
+    of the node -- an upper bound on the node's CPU throughput (memory bandwidth does not scale that way),
+    so the GPU/CPU ratio against it is a lower bound.
+    mode="seal": the SEAL-convention matvec (P = 1, 37 one-limb digits, SEAL's switch_key_inplace
+    rounding), checked against the oracle's digest of that mode."""
     from oracle import cpu_port
     N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
+    if mode == "seal":
+        P = 1
     G, B = bsgs_params(D)
     assert [int(q) for q in primes] == [int(q) for q in cpu_port.create_coeff_modulus(N, [59] * (L0 + P))]
-    secs, y, t_setup, threads = cpu_port.baseline(N, L0, P, D, reps=args.cpu_reps, sk_seed=SK_SEED,
-                                                  input_seed=INPUT_SEED, diag_seed=DIAG_SEED)
+    threads = cpu_port.box_threads()
+    secs, y, t_setup, threads = cpu_port.baseline(N, L0, P, D, reps=args.cpu_reps, threads=threads, sk_seed=SK_SEED,
+                                                  input_seed=INPUT_SEED, diag_seed=DIAG_SEED, mode=mode)
     med = float(np.median(secs))
-    return {"value": round(1.0 / med, 5), "unit": "matvec/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
-            "sample": f"full matvec x {len(secs)}, median (after 1 untimed): oracle/cpu_port.c, SEAL-class CPU "
-                      f"restatement (Harvey NTT + Shoup, Barrett lazy sums, OpenMP over rotations/giant groups), "
-                      f"{(G - 1) + (B - 1)} non-hoisted rotations + {D} multiply_plain/add + rescale at N={N}, "
-                      f"L0={L0}, P={P}; not TenSEAL (not importable, SURVEY §8c)",
-            "sec_per_matvec": round(med, 4), "sec_per_matvec_all": [round(v, 4) for v in secs],
-            "setup_s": round(t_setup, 1),
-            "parity": limb_digest_check(args.config, y)}
+    half = None
+    if threads >= 2:
+        hs, _, _, _ = cpu_port.baseline(N, L0, P, D, reps=1, threads=threads // 2, sk_seed=SK_SEED,
+                                        input_seed=INPUT_SEED, diag_seed=DIAG_SEED, mode=mode)
+        half = {"threads": threads // 2, "sec_per_matvec": round(float(np.median(hs)), 4)}
+    phys = physical_cores()
+    res = {"value": round(1.0 / med, 5), "unit": "matvec/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "cores_usable": cpu_port.usable_cores(),
+           "sample": f"full matvec x {len(secs)}, median (after 1 untimed): oracle/cpu_port.c, SEAL-class CPU "
+                     f"restatement (Harvey NTT + Shoup, Barrett lazy sums, OpenMP over rotations/giant groups), "
+                     f"{(G - 1) + (B - 1)} non-hoisted rotations + {D} multiply_plain/add + rescale at N={N}, "
+                     f"L0={L0}, P={P}" + (", SEAL switch_key_inplace convention" if mode == "seal" else "")
+                     + "; not TenSEAL (not importable, SURVEY §8c)",
+           "sec_per_matvec": round(med, 4), "sec_per_matvec_all": [round(v, 4) for v in secs],
+           "half_threads": half, "setup_s": round(t_setup, 1),
+           "parity": limb_digest_check("cfg2" if args.config == "cfg2" else args.config, y,
+                                       "_seal" if mode == "seal" else "")}
+    if phys:
+        res["whole_host_extrapolated"] = {
+            "physical_cores": phys, "value": round(phys / threads / med, 4), "unit": "matvec/s",
+            "basis": f"{threads}-thread rate x {phys}/{threads} (linear per-core scaling: an upper bound)"}
+    return res
+
+
+def physical_cores():
+    """Physical cores of the host (/proc/cpuinfo: distinct (physical id, core id) pairs), None if unknown."""
+    try:
+        pairs, pid = set(), None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                pid = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                pairs.add((pid, line.split(":")[1].strip()))
+        return len(pairs) or None
+    except OSError:
+        return None
 
 
 def cpu_check_block_projection(cap):

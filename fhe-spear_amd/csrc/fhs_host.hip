@@ -332,10 +332,16 @@ struct fhs_context {
     std::vector<hipEvent_t> timer_open;                              // begin event per id
     std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> timer_pairs;
     fhs::KTimer ktimer{};
-    // pinned staging ring for launch descriptors (stage_h2d); wraps after a stream sync
+    // pinned staging ring for launch descriptors (stage_h2d): kRingSegs segments; leaving a segment
+    // records an event, re-entering it waits for that event (recorded a whole ring earlier)
     unsigned char* ring = nullptr;
-    size_t ring_head = 0;
+    size_t ring_head = 0;          // next free byte; always inside segment ring_seg (or at its end)
+    int ring_seg = 0;
     static constexpr size_t kRingBytes = 16u << 20;
+    static constexpr int kRingSegs = 8;
+    static constexpr size_t kSegBytes = kRingBytes / kRingSegs;
+    hipEvent_t ring_ev[kRingSegs] = {};
+    uint64_t ring_waits = 0, ring_blocked = 0;   // segment re-entries; of those, the ones that had to wait
     fhs::Stager stager{};
     // grow-only scratch buffers reused across calls (stream order makes reuse safe): a large
     // allocation costs host time per GB
@@ -551,6 +557,60 @@ static fhs_status new_pt(fhs_context* c, int ci, double scale, fhs_plaintext** o
 static size_t ct_bytes(const fhs_ciphertext* ct) { return 8ull * ct->ncomp * ct->l * ct->ctx->N; }
 static size_t pt_bytes(const fhs_plaintext* pt) { return 8ull * pt->l * pt->ctx->N; }
 
+// ---------------------------------------------------------------- timing events
+// A pool of timing events per device: hipEventCreate can take milliseconds now and then (it may
+// allocate a signal through the driver), so the timing hooks -- the bench's per-step events
+// (fhs_event_record) and the per-kernel brackets (timer_rec) -- take pre-created events instead of
+// creating them between enqueued launches, where a slow creation leaves the GPU idle inside an open
+// bracket.  fhs_kernel_timer_arm tops the pool up before a timed region.
+static std::mutex g_ev_mu;
+static std::map<int, std::vector<hipEvent_t>> g_ev_free;
+static std::unordered_map<hipEvent_t, int> g_ev_dev;
+static hipEvent_t ev_get(int dev) {
+    {
+        std::lock_guard<std::mutex> lk(g_ev_mu);
+        auto& v = g_ev_free[dev];
+        if (!v.empty()) {
+            hipEvent_t e = v.back();
+            v.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ev_mu);
+    g_ev_dev[e] = dev;
+    return e;
+}
+static void ev_put(hipEvent_t e) {
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(g_ev_mu);
+    auto it = g_ev_dev.find(e);
+    if (it == g_ev_dev.end()) {
+        hipEventDestroy(e);
+        return;
+    }
+    g_ev_free[it->second].push_back(e);
+}
+static void ev_reserve(int dev, size_t n) {
+    std::vector<hipEvent_t> made;
+    {
+        std::lock_guard<std::mutex> lk(g_ev_mu);
+        if (g_ev_free[dev].size() >= n) return;
+        n -= g_ev_free[dev].size();
+    }
+    for (size_t k = 0; k < n; ++k) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) break;
+        made.push_back(e);
+    }
+    std::lock_guard<std::mutex> lk(g_ev_mu);
+    for (hipEvent_t e : made) {
+        g_ev_dev[e] = dev;
+        g_ev_free[dev].push_back(e);
+    }
+}
+
 // ---------------------------------------------------------------- host-side latency trace
 // FHESPEAR_HOST_TRACE=1 prints the host time of each section of the BSGS entry point (stderr); used
 // to check that no call blocks on the GPU queue (tools/debug/host_timing.py).
@@ -570,17 +630,36 @@ struct HostTrace {
 // Small host->device copies on the context stream.  A pageable-source hipMemcpyAsync returns only
 // once the copy has run, i.e. once the stream has drained up to it, which would serialise the host
 // with the GPU on every launch; staging through a pinned ring keeps the host ahead of the queue.
-// The ring is reused after one stream synchronisation per wrap (every few hundred BSGS steps).
+// The ring is cut into kRingSegs segments and a copy never straddles two.  Leaving segment k records
+// an event on the stream after k's last copy; before k is written again -- a whole ring (16 MB of
+// descriptors, hundreds of BSGS steps) later -- the host waits for that event, which has long
+// completed.  Round 1-3 synchronised the whole stream on every wrap instead: the queue drained to
+// empty, and any host delay right after it (e.g. an event creation, see timer_rec) left the GPU idle
+// inside whatever kernel bracket was open.
 static hipError_t stage_h2d(void* user, void* dst, const void* src, size_t bytes) {
     fhs_context* c = static_cast<fhs_context*>(user);
-    if (!c->ring || bytes > fhs_context::kRingBytes / 4) {
+    constexpr size_t SEG = fhs_context::kSegBytes;
+    if (!c->ring || bytes > SEG) {
         hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->st);
         return e == hipSuccess ? hipStreamSynchronize(c->st) : e;
     }
-    if (c->ring_head + bytes > fhs_context::kRingBytes) {
-        hipError_t e = hipStreamSynchronize(c->st);
+    const int seg = c->ring_seg;
+    if (c->ring_head + bytes > (size_t)(seg + 1) * SEG) {   // leave segment `seg` for the next one
+        hipEvent_t& out = c->ring_ev[seg];
+        if (!out && hipEventCreateWithFlags(&out, hipEventDisableTiming) != hipSuccess) out = nullptr;
+        hipError_t e = out ? hipEventRecord(out, c->st) : hipStreamSynchronize(c->st);
         if (e != hipSuccess) return e;
-        c->ring_head = 0;
+        const int next = (seg + 1) % fhs_context::kRingSegs;
+        if (hipEvent_t in = c->ring_ev[next]) {
+            ++c->ring_waits;
+            if (hipEventQuery(in) == hipErrorNotReady) {
+                ++c->ring_blocked;
+                e = hipEventSynchronize(in);
+                if (e != hipSuccess) return e;
+            }
+        }
+        c->ring_seg = next;
+        c->ring_head = (size_t)next * SEG;
     }
     unsigned char* p = c->ring + c->ring_head;
     memcpy(p, src, bytes);
@@ -934,8 +1013,12 @@ static void ctx_free(fhs_context* c) {
             for (void* p : kv.second) hipFree(p);
         c->free_blocks.clear();
         if (c->ring) hipHostFree(c->ring);
+        for (hipEvent_t e : c->ring_ev)
+            if (e) hipEventDestroy(e);
         for (auto& v : c->timer_pairs)
-            for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+            for (auto& pr : v) { ev_put(pr.first); ev_put(pr.second); }
+        for (hipEvent_t e : c->timer_open)
+            if (e) ev_put(e);
         hipStreamDestroy(c->st);
     }
     delete c;
@@ -2804,8 +2887,8 @@ extern "C" fhs_status fhs_random_plaintexts(fhs_context* c, uint64_t seed, int c
 }
 extern "C" fhs_status fhs_event_record(fhs_context* c, void** ev) {
     ENTER(c);
-    hipEvent_t e;
-    HIPCHK(hipEventCreate(&e), "event");
+    hipEvent_t e = ev_get(c->device);
+    if (!e) return fail(FHS_ERR_HIP, "event: hipEventCreate failed");
     HIPCHK(hipEventRecord(e, c->st), "event");
     *ev = (void*)e;
     return FHS_OK;
@@ -2816,22 +2899,23 @@ extern "C" fhs_status fhs_event_elapsed(void* a, void* b, float* ms) {
     return FHS_OK;
 }
 extern "C" fhs_status fhs_event_destroy(void* e) {
-    if (e) hipEventDestroy((hipEvent_t)e);
+    ev_put((hipEvent_t)e);   // back to the pool (events are reused, not destroyed)
     return FHS_OK;
 }
 static void timer_rec(void* vc, int id, int begin, hipStream_t st) {
     auto* c = static_cast<fhs_context*>(vc);
     if (!(c->timer_mask & (1u << id))) return;
-    hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return;
+    hipEvent_t e = ev_get(c->device);
+    if (!e) return;
     hipEventRecord(e, st);
     if (begin) {
+        if (c->timer_open[id]) ev_put(c->timer_open[id]);
         c->timer_open[id] = e;
     } else if (c->timer_open[id]) {
         c->timer_pairs[id].push_back({c->timer_open[id], e});
         c->timer_open[id] = nullptr;
     } else {
-        hipEventDestroy(e);
+        ev_put(e);
     }
 }
 // Arms the timer for the kernels in `mask` (bit i = fhs::KernelId i) after reporting, for kernel
@@ -2855,7 +2939,7 @@ extern "C" fhs_status fhs_kernel_timer(fhs_context* c, int kernel_id, float* ms,
     if (launches) *launches = n;
     if (reset) {
         for (auto& v : c->timer_pairs) {
-            for (auto& pr : v) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+            for (auto& pr : v) { ev_put(pr.first); ev_put(pr.second); }
             v.clear();
         }
     }
@@ -2869,6 +2953,14 @@ extern "C" fhs_status fhs_kernel_timer_arm(fhs_context* c, uint32_t mask) {
         c->ktimer = fhs::KTimer{c, timer_rec};
     }
     c->timer_mask = mask;
+    if (mask) ev_reserve(c->device, 2048);   // created here, not between the timed launches
+    return FHS_OK;
+}
+// staging-ring statistics (tests / diagnostics): segment re-entries, and how many had to wait
+extern "C" fhs_status fhs_staging_stats(fhs_context* c, uint64_t* reentries, uint64_t* blocked) {
+    ENTER(c);
+    if (reentries) *reentries = c->ring_waits;
+    if (blocked) *blocked = c->ring_blocked;
     return FHS_OK;
 }
 // device-to-device copy of a ciphertext's limbs into caller memory (RCCL interop); synchronises

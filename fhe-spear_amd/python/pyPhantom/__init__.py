@@ -176,6 +176,7 @@ _SIGS = {
     "fhs_ciphertext_copy_to_device_async": (C.c_int, [_vp, _vp, _vp]),
     "fhs_ciphertext_from_device_async": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
     "fhs_context_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
+    "fhs_staging_stats": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 # Fork-only symbols the reference probes with try/except AttributeError (bg:449-461, 382-391): if
 # the library lacks one (an older build, or FHESPEAR_DISABLE_SYMBOLS for tests), the Python names
@@ -1044,6 +1045,13 @@ def kernel_timer_read(ctx, reset=False):
     if reset:
         _check(_lib.fhs_kernel_timer(ctx._h, -1, None, None, 1), "kernel_timer")
     return out
+
+
+def staging_stats(ctx):
+    """(segment re-entries, re-entries that waited for the GPU) of the context's descriptor ring."""
+    a, b = C.c_uint64(), C.c_uint64()
+    _check(_lib.fhs_staging_stats(ctx._h, C.byref(a), C.byref(b)), "staging_stats")
+    return int(a.value), int(b.value)
 
 
 def ciphertext_copy_to_device(ctx, ct, dst_ptr, sync=True):

@@ -273,6 +273,9 @@ fhs_status fhs_ciphertext_from_device_async(fhs_context* ctx, const void* src, i
                                             double scale, fhs_ciphertext** out);
 /* the context's HIP stream (hipStream_t), on which every library call is ordered */
 fhs_status fhs_context_stream(fhs_context* ctx, void** stream);
+/* staging-ring statistics: how often the pinned descriptor ring re-entered a segment, and how many of
+ * those re-entries had to wait for the GPU (should stay 0: the host never drains the queue) */
+fhs_status fhs_staging_stats(fhs_context* ctx, uint64_t* reentries, uint64_t* blocked);
 /* Host-side diagnostic of the device reduction arithmetic (no GPU needed): reduces hi:lo mod q with
  * the pseudo-Mersenne folds the kernels use when q qualifies (*pm_used = 1), else *pm_used = 0 and
  * *out = (hi:lo) mod q.  Exists so the CPU test suite can check the fold bounds against big ints. */

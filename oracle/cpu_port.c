@@ -10,7 +10,11 @@
  *     exact centred ModUp (the same count as oracle/ckks_oracle.c ock_centered_count), key inner
  *     product, ModDown by P;
  *   - OpenMP over the independent rotations / giant groups of the matvec, and over limbs in the
- *     final sum and rescale.
+ *     final sum and rescale;
+ *   - cpx_set_ks_mode(c, 1): SEAL's switch_key_inplace convention (P = 1, the oracle's
+ *     ock_ctx_set_ks_mode(c, 1), ckks_oracle.c:459,486,496): every limb lifted as its residue in
+ *     [0, q) (no centring), ModDown rounded by adding floor(p/2) to the special limb and subtracting
+ *     floor(p/2) mod q_i after the conversion -- bench.py's seal_mode.cpu_baseline.
  * TEST INFRASTRUCTURE (bench.py's cpu_baseline leg and tests/ only, never the product path).  Its
  * limbs equal the oracle's (tests/test_cpu.py::test_cpu_port_matches_oracle), so the baseline runs
  * the same arithmetic as the GPU path, not an approximation of it.
@@ -32,6 +36,7 @@ typedef struct {
     u64 *ninv, *ninvs;       /* K */
     u64 *w1ninv, *w1ninvs;   /* K: psi^-rev(1) N^-1 (last inverse stage) */
     u64 *br0, *br1;          /* K: floor(2^128 / q) (Barrett) */
+    int ks_seal;             /* 0 exact centred (default), 1 SEAL's switch_key_inplace rounding (P = 1) */
 } cpx_ctx;
 
 static inline u64 mulmod(u64 a, u64 b, u64 q) { return (u64)(((u128)a * b) % q); }
@@ -263,7 +268,7 @@ static void keyswitch(const cpx_ctx* c, const u64* a, const u64* key, int l, u64
         for (u64 n = 0; n < N; n++) {
             u64 yy[8];
             for (int u = 0; u < ns; u++) yy[u] = ys[(size_t)(b0 + u) * N + n];
-            vc[(size_t)j * N + n] = (unsigned char)centered_count(yy, c->q + b0, R0 + b0, R1 + b0, ns);
+            vc[(size_t)j * N + n] = c->ks_seal ? 0 : (unsigned char)centered_count(yy, c->q + b0, R0 + b0, R1 + b0, ns);
         }
     }
     for (int t = 0; t < E; t++) {
@@ -322,6 +327,7 @@ static void keyswitch(const cpx_ctx* c, const u64* a, const u64* key, int l, u64
             memcpy(d, acc + ((size_t)comp * E + l + k) * N, 8 * N);
             ntt_inv(c, d, pi);
             for (u64 n = 0; n < N; n++) d[n] = shoup(d[n], ih, ihs, p);
+            if (c->ks_seal) for (u64 n = 0; n < N; n++) d[n] = addmod(d[n], p >> 1, p);
         }
         for (int i = 0; i < l; i++) {
             const u64 q = c->q[i];
@@ -332,10 +338,11 @@ static void keyswitch(const cpx_ctx* c, const u64* a, const u64* key, int l, u64
                 hm[k] = h; Pm = mulmod(Pm, c->q[L0 + k] % q, q);
             }
             const u64 Pinv = invmod(Pm, q), Pinvs = shoup_pre(Pinv, q);
+            const u64 halfq = c->ks_seal ? (c->q[L0] >> 1) % q : 0;
             for (u64 n = 0; n < N; n++) {
                 u128 s = 0;
                 for (int k = 0; k < P; k++) s += (u128)yp[(size_t)k * N + n] * hm[k];
-                ext[n] = barrett(s, q, c->br0[i], c->br1[i]);
+                ext[n] = submod(barrett(s, q, c->br0[i], c->br1[i]), halfq, q);
             }
             ntt_fwd(c, ext, i);
             const u64* ap = acc + ((size_t)comp * E + i) * N;
@@ -471,6 +478,11 @@ int cpx_matvec(const cpx_ctx* c, const u64* ct, int l, const u64* const* baby_ke
 }
 
 int cpx_threads(void) { return omp_get_max_threads(); }
+int cpx_set_ks_mode(cpx_ctx* c, int mode) {
+    if (mode && c->P != 1) return -1;   /* SEAL's convention has one special prime */
+    c->ks_seal = mode != 0;
+    return 0;
+}
 void cpx_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }
 
 /* exported single transforms (tests and timing) */

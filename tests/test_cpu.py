@@ -512,6 +512,32 @@ def test_cpu_port_matches_oracle(orc):
     assert cp.sha256(y) == man["small"]["sha256"]
 
 
+def test_cpu_port_seal_mode_matches_oracle(orc):
+    """The SEAL-convention CPU baseline (bench.py seal_mode.cpu_baseline: cpu_port in SEAL mode, P = 1)
+    computes the oracle's SEAL-mode limbs: single rotations and a whole small BSGS matvec (bg:464-485,
+    every rotation non-hoisted) against the oracle's own loop."""
+    from oracle import cpu_port as cp
+    N, L0, P, D, seed = 2048, 5, 1, 36, 9
+    primes = [int(q) for q in orc.create_coeff_modulus(N, [59] * (L0 + P))]
+    o = orc.Oracle(N, primes, P)
+    o.set_key_switch_mode("seal")
+    s = o.gen_secret(seed)
+    ct = o.encrypt_symmetric(seed, 0, s, o.random_plaintext(3, 0, L0))
+    port = cp.CpuPort(N, primes, P, 2, mode="seal")
+    for st in (1, 6, -3):
+        k = o.gen_galois_key(seed, s, orc.galois_elt(st, N))
+        assert np.array_equal(port.rotate(ct, k, st), o.rotate(ct, k, st)), st
+    G, B = 6, 6
+    pts = [o.random_plaintext(4, k, L0) for k in range(D)]
+    bk = {b: o.gen_galois_key(seed, s, orc.galois_elt(b, N)) for b in range(1, G)}
+    gk = {g: o.gen_galois_key(seed, s, orc.galois_elt(g * G, N)) for g in range(1, B)}
+    baby = [ct] + [o.rotate(ct, bk[b], b) for b in range(1, G)]
+    want = o.bsgs_loop(baby, pts, [None] + [gk[g] for g in range(1, B)], G, B, D)
+    assert np.array_equal(port.matvec(ct, bk, gk, pts, G, B, D), want)
+    with pytest.raises(ValueError):
+        cp.CpuPort(N, [int(q) for q in orc.create_coeff_modulus(N, [59] * 6)], 2, 2, mode="seal")
+
+
 def test_bench_block_projection_check_on_cpu(orc):
     """bench.py's block-leg limb check (cpu_check_block_projection) accepts the oracle's own loop
     output for a recorded call and rejects a one-limb change (small ring, no GPU)."""

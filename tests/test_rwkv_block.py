@@ -99,7 +99,7 @@ def _run_block_tool(world, backend="gloo", extra=(), port=29541):
            str(REPO / "tools" / "rwkv_block.py"),
            "--backend", backend, "--N", "2048", "--L0", "4", "--P", "2", "--D", "64", "--F", "256",
            "--head-size", "16", "--blocks", "2", "--reps", "1", "--preencoded"] + list(extra)
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100)
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=100 if world <= 4 else 280)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     m = re.search(rf"world {world}.*: .* final max_err ([0-9.e+-]+) x_sha256 ([0-9a-f]+)", out.stdout)
     assert m, out.stdout[-2000:]
@@ -151,6 +151,23 @@ def test_block_over_ranks_grid_sharded(require_gpu):
     as a 2 x 1 grid (baby shares only), the 1-rank groups whole -- the same decrypted block output as one
     rank, bit for bit."""
     err, digest = _run_block_tool(4, extra=["--split", "--shard", "grid", "--rb", "2"], port=29581)
+    assert err < 1e-4
+    assert digest == _one_rank_digest()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["dealt", "dealt-broadcast", "giant", "baby", "grid"])
+def test_block_over_eight_ranks(require_gpu, mode):
+    """cfg4's world size: 8 ranks (gloo, all sharing cuda:0) in every shard mode of BlockRunner.  dealt:
+    each stage's projections round-robin (r, k, v on ranks 0-2, o on 0, the FFN pairs on 0-1), with
+    "broadcast" the FFN key pair's baby steps computed once and broadcast; giant / baby / grid: latency
+    mode, the stages' rank groups 3+3+2 (r, k, v), 8 (o), 4+4, 4+4 (FFN pairs) shard each projection by
+    giant groups, by baby steps (reduce-scatter) or on a grid with fhespear_dist.grid_rb(group size)
+    baby shares (8x1 for o).  Every mode must give the one-rank block's output bit for bit."""
+    extra = {"dealt": [], "dealt-broadcast": ["--baby-mode", "broadcast"], "giant": ["--split"],
+             "baby": ["--split", "--shard", "baby"], "grid": ["--split", "--shard", "grid"]}[mode]
+    port = 29600 + ["dealt", "dealt-broadcast", "giant", "baby", "grid"].index(mode)
+    err, digest = _run_block_tool(8, extra=extra, port=port)
     assert err < 1e-4
     assert digest == _one_rank_digest()
 

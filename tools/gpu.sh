@@ -1,0 +1,85 @@
+#!/bin/bash
+# GPU box: one parametrised script for every gpurun call (replaces the per-round one-offs).
+#   tools/gpu.sh OUT STEP [STEP ...]      (OUT is a directory under gpurun_out/)
+# Steps, run in order, each under its own time limit; the script stops at the first failure:
+#   tests[=pytest args]     GPU suite (default: all of tests/ -m gpu)           -> OUT/pytest.log
+#   smoke                   __graft_entry__.smoke()                              -> OUT/smoke.log
+#   bench[=bench args]      one bench line (default: the driver's default line)  -> OUT/bench.json
+#   ab=NAME[:ENV=v,ENV=v]   cfg2 matvec-only bench under extra environment       -> OUT/ab_NAME.json
+#   trace[=bench args]      rocprofv3 --kernel-trace --stats of a matvec-only bench -> OUT/trace/,
+#                           OUT/rocprof_summary_<config>.json (tools/rocprof_summary.py: per-dispatch
+#                           steady state of the timed steps)
+#   pmc[=config]            FETCH_SIZE, WRITE_SIZE and VALU counter passes (one rocprofv3 run each)
+#                           -> OUT/pmc_traffic_<config>.json, OUT/pmc_valu_<config>.json
+#   rehearse=N[:bench args] N ranks sharing this one GPU (gloo, host-staged exchange; timings
+#                           meaningless): bench.py --gpus N self-launches them -> OUT/rehearse_nN.json
+#   py=SCRIPT[:args]        python SCRIPT args                                  -> OUT/py_<name>.log
+set -o pipefail
+OUT=gpurun_out/$1
+shift
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+MV="--no-cpu-baseline --no-block --no-seal"
+fail() { echo "step $1 failed"; tail -20 "$2"; exit 1; }
+for step in "$@"; do
+    name=${step%%=*}
+    arg=""
+    [ "$name" != "$step" ] && arg=${step#*=}
+    case "$name" in
+    tests)
+        timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 300 --timeout-method thread $arg \
+            > "$OUT/pytest.log" 2>&1 || fail tests "$OUT/pytest.log"
+        tail -1 "$OUT/pytest.log" ;;
+    smoke)
+        timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || fail smoke "$OUT/smoke.log"
+        tail -1 "$OUT/smoke.log" ;;
+    bench)
+        timeout -k 10 600 python bench.py $arg > "$OUT/bench.log" 2>&1 || fail bench "$OUT/bench.log"
+        grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"
+        python3 tools/show_bench.py "$OUT/bench.json" ;;
+    ab)
+        v=${arg%%:*}
+        envs=""
+        [ "$v" != "$arg" ] && envs=$(echo "${arg#*:}" | tr ',' ' ')
+        env $envs timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 $MV > "$OUT/ab_$v.log" 2>&1 || fail "ab $v" "$OUT/ab_$v.log"
+        grep '^{' "$OUT/ab_$v.log" | tail -1 > "$OUT/ab_$v.json"
+        python3 tools/show_bench.py "$OUT/ab_$v.json" "$v" ;;
+    trace)
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+            -- python3 bench.py --steps 20 --warmup 3 $MV $arg > "$OUT/trace.log" 2>&1 || fail trace "$OUT/trace.log"
+        cfg=$(echo "$arg" | sed -n 's/.*--config \([a-z0-9_]*\).*/\1/p')
+        cfg=${cfg:-cfg2}
+        grep '^{' "$OUT/trace.log" | tail -1 > "$OUT/trace_bench_$cfg.json"
+        python3 tools/rocprof_summary.py "$OUT/trace" "$OUT/trace_bench_$cfg.json" "$OUT/rocprof_summary_$cfg.json" ;;
+    pmc)
+        cfg=${arg:-cfg2}
+        K="k_modup|k_ks_ip|k_bsgs_inner|k_moddown|k_ks_intt|k_giant_sum|k_centered"
+        for c in "fetch FETCH_SIZE" "write WRITE_SIZE" "valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
+            d=${c%% *}
+            timeout -s KILL 240 rocprofv3 --kernel-include-regex "$K" --pmc ${c#* } -d "$OUT/pmc_$d" -o run \
+                --output-format csv -- python3 bench.py --config "$cfg" --steps 3 --warmup 1 $MV > "$OUT/pmc_$d.log" 2>&1 \
+                || fail "pmc $d" "$OUT/pmc_$d.log"
+        done
+        python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" \
+            "$OUT/pmc_write/run_counter_collection.csv" 7 "$OUT/pmc_traffic_$cfg.json" || exit 1
+        python3 tools/pmc_valu.py "$OUT/pmc_valu/run_counter_collection.csv" 7 "$OUT/pmc_valu_$cfg.json" || exit 1 ;;
+    rehearse)
+        n=${arg%%:*}
+        a=""
+        [ "$n" != "$arg" ] && a=${arg#*:}
+        FHESPEAR_DIST_BACKEND=gloo FHESPEAR_DEVICE=0 timeout -k 10 900 python bench.py --gpus "$n" $a \
+            > "$OUT/rehearse_n$n.log" 2>&1 || fail "rehearse $n" "$OUT/rehearse_n$n.log"
+        grep '^{' "$OUT/rehearse_n$n.log" | tail -1 > "$OUT/rehearse_n$n.json"
+        python3 tools/show_bench.py "$OUT/rehearse_n$n.json" ;;
+    py)
+        s=${arg%%:*}
+        a=""
+        [ "$s" != "$arg" ] && a=${arg#*:}
+        b=$(basename "$s" .py)
+        timeout -k 10 900 python -u "$s" $a > "$OUT/py_$b.log" 2>&1 || fail "py $s" "$OUT/py_$b.log"
+        tail -3 "$OUT/py_$b.log" ;;
+    *)
+        echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "done $OUT"

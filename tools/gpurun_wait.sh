@@ -1,0 +1,19 @@
+#!/bin/bash
+# Local helper (this container, not the GPU box): run one gpurun call, and when the pool had no free box
+# (status "transient": nothing ran, nothing charged) try again after a pause, at most 12 times.  A call
+# that ran -- passed, failed or timed out -- is never repeated.
+#   tools/gpurun_wait.sh LOG TIMEOUT 'command'
+log=$1
+lim=$2
+shift 2
+for i in $(seq 1 12); do
+    /usr/local/graft/bin/gpurun --timeout "$lim" -- "$@" > "$log" 2>&1
+    rc=$?
+    if grep -q "status=transient" "$log" && ! grep -q "run [1-9][0-9.]*s of limit" "$log"; then
+        echo "attempt $i: no box, waiting" >> "$log.attempts"
+        sleep 150
+        continue
+    fi
+    exit $rc
+done
+exit 3

@@ -9,6 +9,7 @@ import collections
 import csv
 import json
 import sys
+from pathlib import Path
 
 
 def main():
@@ -32,8 +33,11 @@ def main():
                   "valu_busy": round(c["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * cyc), 3) if cyc else None,
                   "launches_per_step": c["launches"] / steps}
         print(f"{k:22s} VALU {res[k]['valu_wave_insts_per_step'] / 1e6:8.1f} M wave-insts/step  busy {res[k]['valu_busy']}")
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench import kernel_source_hash
     json.dump({"meta": {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE",
-                        "steps_executed": steps}, "kernels": res}, open(out, "w"), indent=1)
+                        "steps_executed": steps}, "kernel_source_sha256_16": kernel_source_hash(), "kernels": res},
+              open(out, "w"), indent=1)
 
 
 if __name__ == "__main__":
