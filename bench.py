@@ -33,6 +33,9 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "fhe-spear_amd" / "python"))
+# fixed seeds throughout: the timed output is checked against the oracle's digest of the same workload,
+# so encryption randomness must be the reproducible kind (fhs_host.hip parity_rng)
+os.environ.setdefault("FHESPEAR_PARITY_RNG", "1")
 sys.path.insert(0, str(REPO))
 
 import numpy as np  # noqa: E402
@@ -675,6 +678,8 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, 
         res = {"sec_per_block": round(sec, 5), "steps": steps, "warmup": warmup,
                "sec_per_block_all": [round(v, 5) for v in secs],
                "stages_ms": {k: round(1e3 * v / steps, 2) for k, v in stage.items()},
+               "server_ms": round(1e3 * sum(v for k, v in stage.items() if k.startswith("server_")) / steps, 2),
+               "client_ms": round(1e3 * sum(v for k, v in stage.items() if k.startswith("client_")) / steps, 2),
                "max_abs_err_vs_plaintext_block": err,
                "workload": cfg["workload"], "n_gpus": world,
                "parallelism": (f"giant-step-split projections x{world}" if split

@@ -1072,6 +1072,13 @@ static uint64_t prf_u64(const PrfKey& K, uint64_t sid) {
     return w0;
 }
 static uint64_t stream_id(uint64_t kind, uint64_t a, uint64_t b) { return (kind << 56) | (a << 16) | b; }
+// Reproducible randomness for parity checks (FHESPEAR_PARITY_RNG set: tests/conftest.py, bench.py, smoke):
+// encryption counters start at 0 and a public key's mask key is PRF(secret key, generation) alone, so a
+// seeded key reproduces the oracle's ciphertexts.  Otherwise each secret key's symmetric-encryption
+// counter starts at a fresh random offset and each public key's mask key has 256 fresh random bits
+// mixed in: a secret key recreated from the same 32 key bytes (another process, another context) never
+// repeats an encryption mask, which would reveal the difference of the two messages.
+static bool parity_rng() { return getenv("FHESPEAR_PARITY_RNG") != nullptr; }
 enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6, ST_PK_RNG = 7 };
 
 // sample a small polynomial (ternary/CBD) over `limbs` primes and NTT it
@@ -1093,7 +1100,9 @@ extern "C" fhs_status fhs_secret_key_create(fhs_context* c, const uint8_t* key32
     } else if (!os_random(K.k, sizeof(K.k))) {
         return fail(FHS_ERR_INVALID, "secret_key: /dev/urandom unavailable");
     }
-    auto* sk = new fhs_secret_key{c, nullptr, K, 0};
+    uint64_t ctr0 = 0;   // stream ids carry 40 counter bits: a random start below 2^39 leaves 2^39 encryptions
+    if (!parity_rng() && !os_random(&ctr0, sizeof ctr0)) return fail(FHS_ERR_INVALID, "secret_key: /dev/urandom unavailable");
+    auto* sk = new fhs_secret_key{c, nullptr, K, ctr0 & ((1ull << 39) - 1)};
     hipError_t e = dalloc(c, &sk->s, 8ull * c->K * c->N);
     if (e != hipSuccess) { delete sk; return hip_fail(e, "secret key"); }
     e = sample_small_ntt(c, fhs::SAMPLE_TERNARY, sk->key, stream_id(ST_SECRET, 0, 0), sk->s, c->K);
@@ -1387,6 +1396,11 @@ extern "C" fhs_status fhs_gen_public_key(fhs_context* c, fhs_secret_key* sk, fhs
         pk->rng.k[2 * w] = (uint32_t)w0;
         pk->rng.k[2 * w + 1] = (uint32_t)(w0 >> 32);
     }
+    if (!parity_rng()) {   // fresh bits: the same secret key recreated elsewhere never repeats a mask stream
+        PrfKey nonce{};
+        if (!os_random(nonce.k, sizeof nonce.k)) { delete pk; return fail(FHS_ERR_INVALID, "public key: /dev/urandom unavailable"); }
+        for (int w = 0; w < 8; ++w) pk->rng.k[w] ^= nonce.k[w];
+    }
     const size_t S = (size_t)c->L0 * c->N;
     hipError_t e = dalloc(c, &pk->pk, 16 * S);
     if (e != hipSuccess) { delete pk; return hip_fail(e, "public key"); }
@@ -1632,18 +1646,23 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
 // bg:361-432 on the device -- upload the D x D matrix once (D^2 doubles instead of D x slots),
 // gather the rolled, tiled diagonal rows in HBM, encode them.  Values identical to
 // encode_*_vector_batch on the host-prepared rows, hence identical limbs.
-extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, const double* M2, int64_t ld, int trans,
-                                              int D, int G, double scale, int ci, fhs_plaintext** out) {
-    ENTER(c);
-    if (!M1 || !out) return fail(FHS_ERR_INVALID, "encode_diagonals: null argument");
+// The encoder behind encode_matrix_diagonals: diagonal rows `rows[0..nrows)` (indices into 0..D-1, any
+// order) of the D x D view, giant group g rolled by g G, tiled, encoded -- out[k] is row rows[k].  Runs
+// of consecutive indices are gathered by one launch each (a sharded matvec's rank needs a contiguous
+// range of giant groups, or on a grid the same baby share of every group of its column).
+static fhs_status encode_diag_rows(fhs_context* c, const double* M1, const double* M2, int64_t ld, int trans, int D,
+                                   int G, double scale, int ci, const int* rows, int nrows, fhs_plaintext** out) {
+    if (!M1 || !out || (nrows > 0 && !rows)) return fail(FHS_ERR_INVALID, "encode_diagonals: null argument");
     if (D < 1 || G < 1 || G > D) return fail(FHS_ERR_INVALID, "encode_diagonals: need 1 <= G <= D");
     if (ld < D) return fail(FHS_ERR_INVALID, "encode_diagonals: leading dimension below D");
+    for (int k = 0; k < nrows; ++k)
+        if (rows[k] < 0 || rows[k] >= D) return fail(FHS_ERR_INVALID, "encode_diagonals: row index out of range");
     const size_t n = c->N / 2;
     if ((size_t)D > n) return fail(FHS_ERR_INVALID, "encode_diagonals: dimension larger than the slot count");
     fhs_status st = encode_checks(c, n, scale, ci);
     if (st != FHS_OK) return st;
     const bool is_real = M2 == nullptr;
-    BatchOut bo(out, (size_t)D);
+    BatchOut bo(out, (size_t)nrows);
     const size_t mb = 8ull * D * D, stride = is_real ? n : 2 * n;
     uint64_t *dm = nullptr, *dvals = nullptr;
     HIPCHK(dalloc(c, &dm, mb * (is_real ? 1 : 2)), "encode_diagonals matrix");
@@ -1652,15 +1671,20 @@ extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, 
     if (e == hipSuccess && !is_real)
         e = hipMemcpy2DAsync((char*)dm + mb, 8ull * D, M2, 8ull * ld, 8ull * D, D, hipMemcpyHostToDevice, c->st);
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // caller's buffers may be reused on return
+    const double* m1 = reinterpret_cast<const double*>(dm);
+    const double* m2 = is_real ? nullptr : reinterpret_cast<const double*>((char*)dm + mb);
     const size_t chunk = 2048;
-    for (size_t base = 0; e == hipSuccess && st == FHS_OK && base < (size_t)D; base += chunk) {
-        const size_t cnt = std::min(chunk, (size_t)D - base);
+    for (size_t base = 0; e == hipSuccess && st == FHS_OK && base < (size_t)nrows; base += chunk) {
+        const size_t cnt = std::min(chunk, (size_t)nrows - base);
         e = dalloc(c, &dvals, 8 * cnt * stride);
         if (e != hipSuccess) break;
-        const double* m1 = reinterpret_cast<const double*>(dm);
-        const double* m2 = is_real ? nullptr : reinterpret_cast<const double*>((char*)dm + mb);
-        e = fhs::launch_diag_gather(m1, m2, D, G, (int)n, (int)base, (int)cnt, trans ? 1 : 0,
-                                    reinterpret_cast<double*>(dvals), c->st);
+        for (size_t k = 0; e == hipSuccess && k < cnt;) {   // one gather per run of consecutive rows
+            size_t r = 1;
+            while (k + r < cnt && rows[base + k + r] == rows[base + k] + (int)r) ++r;
+            e = fhs::launch_diag_gather(m1, m2, D, G, (int)n, rows[base + k], (int)r, trans ? 1 : 0,
+                                        reinterpret_cast<double*>(dvals) + k * stride, c->st);
+            k += r;
+        }
         if (e == hipSuccess)
             st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci, out + base);
         dfree(c, dvals, 8 * cnt * stride);
@@ -1668,6 +1692,19 @@ extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, 
     dfree(c, dm, mb * (is_real ? 1 : 2));
     if (e != hipSuccess) return hip_fail(e, "encode_diagonals");
     return bo.keep(st);
+}
+extern "C" fhs_status fhs_encode_diagonals_ex(fhs_context* c, const double* M1, const double* M2, int64_t ld, int trans,
+                                              int D, int G, double scale, int ci, fhs_plaintext** out) {
+    ENTER(c);
+    std::vector<int> rows(D > 0 ? D : 0);
+    for (int k = 0; k < (int)rows.size(); ++k) rows[k] = k;
+    return encode_diag_rows(c, M1, M2, ld, trans, D, G, scale, ci, rows.data(), (int)rows.size(), out);
+}
+extern "C" fhs_status fhs_encode_diagonals_rows(fhs_context* c, const double* M1, const double* M2, int64_t ld,
+                                                int trans, int D, int G, double scale, int ci, const int* rows,
+                                                int nrows, fhs_plaintext** out) {
+    ENTER(c);
+    return encode_diag_rows(c, M1, M2, ld, trans, D, G, scale, ci, rows, nrows, out);
 }
 extern "C" fhs_status fhs_encode_diagonals(fhs_context* c, const double* M1, const double* M2, int D, int G,
                                            double scale, int ci, fhs_plaintext** out) {
@@ -2011,6 +2048,24 @@ static fhs_status decode_compose(fhs_context* c, const fhs_plaintext* pt, int k,
     crt_compose(c, host, k, m);
     return FHS_OK;
 }
+// slots z_j = m(zeta^(5^j)) = sum_{k < N/2} (m_k + i m_{k+N/2}) zeta^k omega^(s_j k), omega = zeta^4,
+// 5^j = 4 s_j + 1: an N/2-point FFT of the twisted half-pairs, read at s_j = slot_index[j] / 2; the first
+// `nslots` slots to re_im
+static void decode_slots(const fhs_context* c, const double* m, double scale, size_t nslots, double* re_im) {
+    const size_t n = c->N / 2;
+    std::vector<std::complex<double>> v(n);
+    for (size_t k2 = 0; k2 < n; ++k2) {
+        const double a = m[k2] / scale, b = m[k2 + n] / scale;
+        const double cr = c->dec_twist[k2].real(), ci = c->dec_twist[k2].imag();
+        v[k2] = {a * cr - b * ci, a * ci + b * cr};
+    }
+    fft_inplace(v, c->fft_w, c->logN - 1, 2);
+    for (size_t j = 0; j < nslots; ++j) {
+        const std::complex<double> z = v[c->slot_index[j] >> 1];
+        re_im[2 * j] = z.real();
+        re_im[2 * j + 1] = z.imag();
+    }
+}
 extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double* re_im) {
     ENTER(c);
     if (!pt || !re_im) return fail(FHS_ERR_INVALID, "decode: null argument");
@@ -2032,23 +2087,105 @@ extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double
         if (s != FHS_OK) return s;
     }
     ht.mark("decode: intt + crt");
-    // slots z_j = m(zeta^(5^j)) = sum_{k < N/2} (m_k + i m_{k+N/2}) zeta^k omega^(s_j k), omega = zeta^4,
-    // 5^j = 4 s_j + 1: an N/2-point FFT of the twisted half-pairs, read at s_j = slot_index[j] / 2
-    const size_t n = N / 2;
-    std::vector<std::complex<double>> v(n);
-    for (size_t k2 = 0; k2 < n; ++k2) {
-        const double a = m[k2] / pt->scale, b = m[k2 + n] / pt->scale;
-        const double cr = c->dec_twist[k2].real(), ci = c->dec_twist[k2].imag();
-        v[k2] = {a * cr - b * ci, a * ci + b * cr};
-    }
-    fft_inplace(v, c->fft_w, c->logN - 1, 2);
-    for (size_t j = 0; j < n; ++j) {
-        const std::complex<double> z = v[c->slot_index[j] >> 1];
-        re_im[2 * j] = z.real();
-        re_im[2 * j + 1] = z.imag();
-    }
+    decode_slots(c, m.data(), pt->scale, N / 2, re_im);
     ht.mark("decode: fft");
     return FHS_OK;
+}
+
+// Client-side batch (the client-aided block decrypts 2-3 outputs per stage): every plaintext's INTT,
+// centred CRT composition and check are enqueued together, their coefficients land in one pinned host
+// buffer, and ONE synchronisation replaces one per plaintext; then the slot FFTs, `nslots` slots each
+// (out: count x nslots x (re, im)).  Same arithmetic as fhs_decode, so the same doubles; a plaintext whose
+// check fails (an aliased coefficient) or that needs more limbs than the GPU composition takes goes
+// through fhs_decode's path on its own.
+extern "C" fhs_status fhs_decode_batch(fhs_context* c, const fhs_plaintext* const* pts, int count, int nslots,
+                                       double* re_im) {
+    ENTER(c);
+    const size_t N = c->N, n = N / 2;
+    if (!pts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > n)
+        return fail(FHS_ERR_INVALID, "decode_batch: bad arguments");
+    static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;
+    static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;
+    std::vector<int> fast(count, 0);
+    size_t tmp_words = 0, aux_words = 0;
+    for (int i = 0; i < count; ++i) {
+        if (!pts[i]) return fail(FHS_ERR_INVALID, "decode_batch: null plaintext");
+        const int l = pts[i]->l, k = full ? l : decode_limbs(c, pts[i]->scale, l), kk = std::min(l, k + 1);
+        fast[i] = kk < l && kk <= fhs::kCrtMaxL && !host_crt;
+        if (fast[i]) {
+            tmp_words += (size_t)l * N;
+            aux_words += (size_t)(l - kk) * fhs::kCrtVtabWords + 1;
+        }
+    }
+    uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr;
+    double* host = nullptr;
+    std::vector<unsigned> hflag(count, 0);
+    std::vector<std::vector<uint64_t>> vts(count);
+    std::vector<fhs::CrtConsts> Ks(count);
+    hipError_t e = hipSuccess;
+    if (tmp_words) {
+        e = dalloc(c, &tmp, 8 * tmp_words);
+        if (e == hipSuccess) e = dalloc(c, &dbl, 8 * N * count);
+        if (e == hipSuccess) e = dalloc(c, &aux, 8 * aux_words);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&host), 8 * N * count, hipHostMallocDefault);
+        size_t to = 0, ao = 0;
+        for (int i = 0; e == hipSuccess && i < count; ++i) {
+            if (!fast[i]) continue;
+            const fhs_plaintext* pt = pts[i];
+            const int l = pt->l, k = full ? l : decode_limbs(c, pt->scale, l), kk = std::min(l, k + 1), nx = l - kk;
+            crt_consts(c, kk, Ks[i]);
+            std::vector<uint64_t>& vt = vts[i];
+            vt.assign((size_t)nx * fhs::kCrtVtabWords, 0);
+            for (int x = 0; x < nx; ++x) {
+                uint64_t* v = vt.data() + (size_t)x * fhs::kCrtVtabWords;
+                const uint64_t q = c->q[kk + x];
+                const hu128 R = (~(hu128)0) / q;
+                v[0] = q;
+                v[1] = (uint64_t)R;
+                v[2] = (uint64_t)(R >> 64);
+                const uint64_t t64 = (uint64_t)((((hu128)1) << 64) % q);
+                uint64_t pw = 1 % q;
+                for (int w = 0; w < Ks[i].W; ++w) {
+                    v[3 + w] = pw;
+                    pw = h_mulmod(pw, t64, q);
+                }
+            }
+            uint64_t* t = tmp + to;
+            uint64_t* a = aux + ao;
+            unsigned* flag = reinterpret_cast<unsigned*>(a + vt.size());
+            e = hipMemcpyAsync(t, pt->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
+            if (e == hipSuccess && nx > 0) e = stage_h2d(c, a, vt.data(), 8 * vt.size());
+            if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4, c->st);
+            if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, t, l, l, 1, 0, c->st);
+            if (e == hipSuccess)
+                e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
+                                            t + (size_t)kk * N, nx, a, flag);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(host + (size_t)i * N, reinterpret_cast<double*>(dbl) + (size_t)i * N, 8 * N,
+                                   hipMemcpyDeviceToHost, c->st);
+            if (e == hipSuccess) e = hipMemcpyAsync(&hflag[i], flag, 4, hipMemcpyDeviceToHost, c->st);
+            to += (size_t)l * N;
+            ao += vt.size() + 1;
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    }
+    fhs_status st = e == hipSuccess ? FHS_OK : hip_fail(e, "decode_batch");
+    std::vector<double> m;
+    for (int i = 0; st == FHS_OK && i < count; ++i) {
+        double* out = re_im + (size_t)i * 2 * nslots;
+        if (fast[i] && hflag[i] == 0) {
+            decode_slots(c, host + (size_t)i * N, pts[i]->scale, (size_t)nslots, out);
+            continue;
+        }
+        std::vector<double> full_slots(2 * n);   // the single-plaintext path (exact recomposition)
+        st = fhs_decode(c, pts[i], full_slots.data());
+        if (st == FHS_OK) std::copy(full_slots.begin(), full_slots.begin() + 2 * nslots, out);
+    }
+    if (host) hipHostFree(host);
+    if (aux) dfree(c, aux, 8 * aux_words);
+    if (dbl) dfree(c, dbl, 8 * N * count);
+    if (tmp) dfree(c, tmp, 8 * tmp_words);
+    return st;
 }
 
 // ============================================================================ encryption

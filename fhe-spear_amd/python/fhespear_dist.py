@@ -136,6 +136,89 @@ def from_buffer(ph, ctx, buf, ncomp, chain_index, scale):
     return ct
 
 
+def broadcast_ciphertext(ph, ctx, ct, src: int, dist, device, group=None):
+    """Global rank `src`'s ciphertext (None on the other ranks) -> a ciphertext on every rank of `group`:
+    a small header (chain index, size, scale) then the limbs as one int64 buffer (RCCL broadcast over
+    xGMI; gloo stages both through host memory).  Returns `ct` itself on src."""
+    import torch
+    me = dist.get_rank()
+    host = dist.get_backend(group) == "gloo"
+    hdr = torch.zeros(3, dtype=torch.float64, device="cpu" if host else device)
+    if me == src:
+        hdr.copy_(torch.tensor([ct.chain_index(), ct.size(), ct.scale()], dtype=torch.float64))
+    dist.broadcast(hdr, src=src, group=group)
+    ci, ncomp, scale = int(hdr[0].item()), int(hdr[1].item()), float(hdr[2].item())
+    buf = torch.empty(ncomp * ctx.limbs(ci) * ctx.N, dtype=torch.int64, device=device)
+    if me == src:
+        to_buffer(ph, ctx, ct, buf)
+    if host:
+        h = buf.cpu()
+        dist.broadcast(h, src=src, group=group)
+        if me != src:
+            buf.copy_(h)
+    else:
+        dist.broadcast(buf, src=src, group=group)
+    return ct if me == src else from_buffer(ph, ctx, buf, ncomp, ci, scale)
+
+
+def broadcast_ciphertexts(ph, ctx, cts, src: int, dist, device, n: int, group=None):
+    """`n` ciphertexts of one level and scale (e.g. the G baby steps of an input: north_star "baby steps
+    computed once and broadcast") from global rank `src` to every rank of `group`, as one buffer."""
+    import torch
+    me = dist.get_rank()
+    host = dist.get_backend(group) == "gloo"
+    hdr = torch.zeros(3, dtype=torch.float64, device="cpu" if host else device)
+    if me == src:
+        hdr.copy_(torch.tensor([cts[0].chain_index(), cts[0].size(), cts[0].scale()], dtype=torch.float64))
+    dist.broadcast(hdr, src=src, group=group)
+    ci, ncomp, scale = int(hdr[0].item()), int(hdr[1].item()), float(hdr[2].item())
+    w = ncomp * ctx.limbs(ci) * ctx.N
+    buf = torch.empty(n * w, dtype=torch.int64, device=device)
+    if me == src:
+        for k, c in enumerate(cts):
+            to_buffer(ph, ctx, c, buf[k * w:(k + 1) * w])
+    if host:
+        h = buf.cpu()
+        dist.broadcast(h, src=src, group=group)
+        if me != src:
+            buf.copy_(h)
+    else:
+        dist.broadcast(buf, src=src, group=group)
+    if me == src:
+        return list(cts)
+    return [from_buffer(ph, ctx, buf[k * w:(k + 1) * w], ncomp, ci, scale) for k in range(n)]
+
+
+def send_ciphertext(ph, ctx, ct, src: int, dst: int, dist, device):
+    """Point to point: `ct` on global rank src -> a ciphertext on dst (returned there; None elsewhere,
+    `ct` itself when src == dst).  Header then limbs; gloo through host memory."""
+    import torch
+    me = dist.get_rank()
+    if src == dst:
+        return ct if me == src else None
+    if me not in (src, dst):
+        return None
+    host = dist.get_backend() == "gloo"
+    hdr = torch.zeros(3, dtype=torch.float64, device="cpu" if host else device)
+    if me == src:
+        hdr.copy_(torch.tensor([ct.chain_index(), ct.size(), ct.scale()], dtype=torch.float64))
+        dist.send(hdr, dst=dst)
+        buf = torch.empty(ct.size() * ct.coeff_modulus_size() * ctx.N, dtype=torch.int64, device=device)
+        to_buffer(ph, ctx, ct, buf)
+        dist.send(buf.cpu() if host else buf, dst=dst)
+        return None
+    dist.recv(hdr, src=src)
+    ci, ncomp, scale = int(hdr[0].item()), int(hdr[1].item()), float(hdr[2].item())
+    buf = torch.empty(ncomp * ctx.limbs(ci) * ctx.N, dtype=torch.int64, device=device)
+    if host:
+        h = buf.cpu()
+        dist.recv(h, src=src)
+        buf.copy_(h)
+    else:
+        dist.recv(buf, src=src)
+    return from_buffer(ph, ctx, buf, ncomp, ci, scale)
+
+
 def stage_groups(n_proj: int, world: int):
     """Latency mode for one block stage: its n_proj projections -> contiguous, balanced groups of
     ranks (sizes differ by <= 1), each group sharding one projection's giant steps.  None when

@@ -124,6 +124,7 @@ _SIGS = {
     "fhs_encode_real": (C.c_int, [_vp, _dblp, C.c_size_t, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_encode_real_batch": (C.c_int, [_vp, _dblp, C.c_size_t, C.c_size_t, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_decode": (C.c_int, [_vp, _vp, _dblp]),
+    "fhs_decode_batch": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _dblp]),
     "fhs_encrypt_symmetric": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_encrypt_asymmetric": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_decrypt": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
@@ -163,6 +164,8 @@ _SIGS = {
     "fhs_encode_diagonals": (C.c_int, [_vp, _dblp, _dblp, C.c_int, C.c_int, C.c_double, C.c_int, C.POINTER(_vp)]),
     "fhs_encode_diagonals_ex": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int,
                                           C.POINTER(_vp)]),
+    "fhs_encode_diagonals_rows": (C.c_int, [_vp, _vp, _vp, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_double, C.c_int,
+                                            _vp, C.c_int, C.POINTER(_vp)]),
     "fhs_host_alloc": (C.c_int, [_u64, C.POINTER(_vp)]),
     "fhs_host_free": (C.c_int, [_vp]),
     "fhs_random_plaintexts": (C.c_int, [_vp, _u64, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
@@ -641,11 +644,12 @@ class ckks_encoder:
         (fhs_encode_precise), for constant plaintexts such as the bootstrap transforms."""
         return self._batch(ctx, mat, scale, chain_index, True, precise)
 
-    def encode_matrix_diagonals(self, ctx, M, G, scale, chain_index=1, M2=None):
+    def encode_matrix_diagonals(self, ctx, M, G, scale, chain_index=1, M2=None, rows=None):
         """Extension (no reference symbol): the caller-side pipeline of bg:198-203 + bg:361-432 --
         diagonals of the D x D matrix M (complex-packed with M2: bg:394-432), giant group g rolled by
         g G, tiled to the slots, encoded -- on the GPU from the matrix itself.  Limb-identical to
-        encode_double_vector_batch / encode_complex_vector_batch of the numpy-prepared rows."""
+        encode_double_vector_batch / encode_complex_vector_batch of the numpy-prepared rows.
+        rows (sharded matvecs): encode only these diagonal indices, returned in that order."""
         def view(X):   # (pointer, leading dimension, transposed) of a float64 2-D view, copying only if needed
             X = np.asarray(X)
             if X.dtype != np.float64:
@@ -665,6 +669,14 @@ class ckks_encoder:
             A, B2 = np.ascontiguousarray(A), np.ascontiguousarray(B2)
             lda, ta = A.shape[1], 0
         D = A.shape[0]
+        if rows is not None:
+            r = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
+            hs = (_vp * max(1, len(r)))()
+            _check(_lib.fhs_encode_diagonals_rows(ctx._h, _vp(A.ctypes.data),
+                                                  None if B2 is None else _vp(B2.ctypes.data), int(lda), int(ta), D,
+                                                  int(G), float(scale), int(chain_index), _vp(r.ctypes.data), len(r),
+                                                  hs), "encode_matrix_diagonals")
+            return [plaintext(ctx, _vp(hs[i])) for i in range(len(r))]
         hs = (_vp * D)()
         _check(_lib.fhs_encode_diagonals_ex(ctx._h, _vp(A.ctypes.data), None if B2 is None else _vp(B2.ctypes.data),
                                             int(lda), int(ta), D, int(G), float(scale), int(chain_index), hs),
@@ -682,6 +694,16 @@ class ckks_encoder:
     def decode_complex_vector(self, ctx, pt):
         z = self._decode(ctx, pt)
         return (z[:, 0] + 1j * z[:, 1]).tolist()
+
+    def decode_batch(self, ctx, pts, nslots=None):
+        """Extension: the first `nslots` slots (default all) of every plaintext, with one device
+        synchronisation for the batch (fhs_decode_batch); complex array [len(pts), nslots] -- the same
+        values decode_complex_vector gives."""
+        n = ctx.N // 2 if nslots is None else int(nslots)
+        out = np.empty((len(pts), n, 2), dtype=np.float64)
+        hs = (_vp * max(1, len(pts)))(*[p._h for p in pts])
+        _check(_lib.fhs_decode_batch(ctx._h, hs, len(pts), n, out.ctypes.data_as(_dblp)), "decode_batch")
+        return out[..., 0] + 1j * out[..., 1]
 
 
 # ------------------------------------------------------------------ evaluator (pb:165-205)

@@ -136,6 +136,11 @@ fhs_status fhs_encode_real_batch(fhs_context* ctx, const double* values, size_t 
                                  int chain_index, fhs_plaintext** out_array);
 /* pb:150-156 decode: writes N/2 complex (re, im) */
 fhs_status fhs_decode(fhs_context* ctx, const fhs_plaintext* pt, double* re_im_out);
+/* decode of `count` plaintexts with one device synchronisation (the client's decrypt_vec of a block
+ * stage, bg:784-892): the first `nslots` slots of each, re_im_out = count x nslots x (re, im); the same
+ * doubles as fhs_decode */
+fhs_status fhs_decode_batch(fhs_context* ctx, const fhs_plaintext* const* pts, int count, int nslots,
+                            double* re_im_out);
 
 /* ---- encryption (pb:105-116) ---- */
 fhs_status fhs_encrypt_symmetric(fhs_context* ctx, fhs_secret_key* sk, const fhs_plaintext* pt, fhs_ciphertext** out);
@@ -224,6 +229,12 @@ fhs_status fhs_encode_diagonals(fhs_context* ctx, const double* M1, const double
  * trans = 1 means the block holds M^T (M[m][c] = A[c * ld + m]), e.g. numpy's W[:, lo:hi].T */
 fhs_status fhs_encode_diagonals_ex(fhs_context* ctx, const double* A1, const double* A2, int64_t ld, int trans, int D,
                                    int G, double scale, int chain_index, fhs_plaintext** out_array);
+/* only the diagonals rows[0..nrows) (indices < D, any order; out_array[k] is diagonal rows[k]): the rows one
+ * rank of a sharded matvec needs (fhespear_dist giant_groups / grid_rows) -- limb-identical to the same
+ * plaintexts of the full encode */
+fhs_status fhs_encode_diagonals_rows(fhs_context* ctx, const double* A1, const double* A2, int64_t ld, int trans, int D,
+                                     int G, double scale, int chain_index, const int* rows, int nrows,
+                                     fhs_plaintext** out_array);
 /* encode_complex_vector_batch with an extended-precision (long double) canonical-embedding FFT on the
  * host and exact 128-bit rounding: for constant plaintexts whose f64 encoding error (~2^-52 log n
  * relative) matters -- the bootstrap's CoeffToSlot / SlotToCoeff diagonals.  |values x scale| < 2^126. */

@@ -6,6 +6,9 @@ import pytest
 
 REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO))
+# reproducible encryption randomness (encryption counters from 0, public-key masks from the secret key
+# alone) so seeded keys reproduce the oracle's ciphertexts; inherited by the tools the tests start
+os.environ.setdefault("FHESPEAR_PARITY_RNG", "1")
 sys.path.insert(0, str(REPO / "fhe-spear_amd" / "python"))
 
 

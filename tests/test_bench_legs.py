@@ -21,7 +21,9 @@ def test_block_leg_with_cpu_limb_check(require_gpu):
     res = bench.run_block(args, ph, None, 0, 1, 0, 1, 1, capture=True, config="block_small")
     cap = res.pop("_capture")
     assert res["sec_per_block"] > 0 and set(res["stages_ms"]) == {"server_rkv", "server_wo", "server_ffn_key",
-                                                                   "server_ffn_val"}
+                                                                   "server_ffn_val", "client_encrypt",
+                                                                   "client_decrypt", "client_numpy"}
+    assert res["client_ms"] > 0 and res["server_ms"] > 0
     assert cap["ct_in"].shape == (2, 6, 4096) and cap["ct_out"].shape == (2, 5, 4096) and len(cap["pts"]) == 64
     par = bench.cpu_check_block_projection(cap)
     assert par["r_projection_limbs_match_cpu_port"], par

@@ -487,6 +487,19 @@ def test_encode_matrix_diagonals_equals_host_rows(ph, N, D):
                                             chain_index=2)
         for k in (0, G, D - 1):
             assert np.array_equal(gv[k].to_numpy(), wv[k].to_numpy()), f"view diagonal {k}"
+    # a sharded matvec's rank encodes only its rows (fhs_encode_diagonals_rows): a giant column's
+    # contiguous range and a grid rank's scattered baby share, real and complex, same limbs as the full set
+    import fhespear_dist as fd
+    B = -(-D // G)
+    for rows in (list(range(G, min(D, 3 * G))), fd.grid_rows(G, B, D, 4, 2, 3), [D - 1, 0, G]):
+        sub = enc.encode_matrix_diagonals(ctx, W1, G, 2.0 ** 59, chain_index=2, rows=rows)
+        subc = enc.encode_matrix_diagonals(ctx, W1, G, 2.0 ** 59, chain_index=2, M2=W2, rows=rows)
+        assert len(sub) == len(rows)
+        for p, pc, k in zip(sub, subc, rows):
+            assert np.array_equal(p.to_numpy(), got[k].to_numpy()), f"row subset, diagonal {k}"
+            assert np.array_equal(pc.to_numpy(), gotc[k].to_numpy()), f"complex row subset, diagonal {k}"
+    with pytest.raises(ValueError):
+        enc.encode_matrix_diagonals(ctx, W1, G, 2.0 ** 59, chain_index=2, rows=[D])
 
 
 def test_bsgs_matches_oracle_on_cfg2_ring(ph):
@@ -612,3 +625,71 @@ def test_ffn_block_ct_ct_chain(ph):
         dec = ck.decrypt(ct, D)
         assert np.corrcoef(dec, ref)[0, 1] > 0.999
         assert np.max(np.abs(dec - ref)) < 1e-6
+
+
+_RNG_PROBE = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import pyPhantom as ph
+p = ph.params(ph.scheme_type.ckks)
+p.set_poly_modulus_degree(1024)
+p.set_special_modulus_size(1)
+p.set_coeff_modulus(ph.create_coeff_modulus(1024, [59, 59, 59]))
+ctx = ph.context(p)
+enc = ph.ckks_encoder(ctx)
+pt = enc.encode_double_vector(ctx, np.linspace(0, 1, 16), 2.0 ** 40)
+a, b = ph.secret_key(ctx, seed=5), ph.secret_key(ctx, seed=5)
+sym = np.array_equal(a.encrypt_symmetric(ctx, pt).to_numpy(), b.encrypt_symmetric(ctx, pt).to_numpy())
+asym = np.array_equal(a.gen_publickey(ctx).encrypt_asymmetric(ctx, pt).to_numpy(),
+                      b.gen_publickey(ctx).encrypt_asymmetric(ctx, pt).to_numpy())
+dec = np.array(enc.decode_double_vector(ctx, b.decrypt(ctx, a.gen_publickey(ctx).encrypt_asymmetric(ctx, pt))))[:16]
+print("RESULT", int(sym), int(asym), float(np.max(np.abs(dec - np.linspace(0, 1, 16)))))
+"""
+
+
+def test_encryption_randomness_fresh_outside_parity_mode(require_gpu):
+    """outside parity mode, two secret keys made from the same 32 key bytes (as in two
+    processes) never repeat a symmetric-encryption mask, and their public keys never share a mask
+    stream; with FHESPEAR_PARITY_RNG (the tests' and the bench's setting) they reproduce each other,
+    which is what makes oracle parity of seeded encryptions possible.  Decryption works either way."""
+    import os
+    import subprocess
+    import sys
+    py = str(REPO / "fhe-spear_amd" / "python")
+    res = {}
+    for mode in ("parity", "fresh"):
+        env = dict(os.environ)
+        env.pop("FHESPEAR_PARITY_RNG", None)
+        if mode == "parity":
+            env["FHESPEAR_PARITY_RNG"] = "1"
+        out = subprocess.run([sys.executable, "-c", _RNG_PROBE, py], env=env, capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, out.stderr[-2000:]
+        line = [l for l in out.stdout.splitlines() if l.startswith("RESULT")][-1].split()
+        res[mode] = (int(line[1]), int(line[2]), float(line[3]))
+    assert res["parity"][:2] == (1, 1), res
+    assert res["fresh"][:2] == (0, 0), res
+    assert res["parity"][2] < 1e-6 and res["fresh"][2] < 1e-6, res
+
+
+def test_decode_batch_equals_single_decodes(ph):
+    """fhs_decode_batch (the client's decrypt_vec of a block stage in one synchronisation) returns the
+    same doubles as fhs_decode one plaintext at a time: real and complex encodings at two levels, and a
+    plaintext whose coefficients exceed the first limbs' range (the aliased case that falls back to the
+    all-limb composition)."""
+    N, L0, P = 4096, 8, 2
+    ctx, sk, primes = make_ctx(ph, N, L0, P, seed=31)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(32)
+    pts = [enc.encode_double_vector(ctx, rng.normal(0, 1, N // 2), 2.0 ** 59),
+           enc.encode_complex_vector(ctx, rng.normal(0, 1, N // 2) + 1j * rng.normal(0, 1, N // 2), 2.0 ** 59, 3),
+           sk.decrypt(ctx, sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, rng.normal(0, 1, 64), 2.0 ** 50)))]
+    o = oracle_for(primes, N, P)
+    pts.append(ph.plaintext_from_numpy(ctx, rand_pt(o, rng, L0), 1, 2.0 ** 40))   # aliased: all-limb fallback
+    for n in (N // 2, 64):
+        got = enc.decode_batch(ctx, pts, n)
+        assert got.shape == (len(pts), n)
+        for i, p in enumerate(pts):
+            want = np.array(enc.decode_complex_vector(ctx, p))[:n]
+            assert np.array_equal(got[i], want), (i, n)

@@ -5,6 +5,7 @@ unchanged against this backend where the reference is present (INTEGRATION.md); 
 because the reference does not travel to the GPU box.
 
     python tools/ffn_block.py [--N 16384 --L0 36 --D 2048 --F 4096 --blocks 2 [--bootstrap]]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/ffn_block.py --dist [--shard giant|grid|baby]
 
 --bootstrap runs tf's main loop (tf:233-298): magnitude calibration of W_val (tf:181-196), a
 bootstrap whenever fewer than 4 levels remain (tf:239-266, ckks_bootstrapper + one rescale), and
@@ -149,6 +150,134 @@ def ffn_block(ck, ct_x, W_key, W_val, D, F):
     return ph.add(ck.ctx, xa, acc)
 
 
+# ------------------------------------------------------------------ over ranks (Config 5)
+class FfnRanks:
+    """The FFN block's chunks over the ranks of one node (tf:26-118 sharded; BASELINE configs[4] on 8
+    GPUs).  Every rank holds the same keys (the client's seed) so that any rank's partial work is a
+    valid share; rank 0 is where the chain's ciphertext lives between blocks (and the client decrypts).
+
+    * chunk c of the F/D key chunks (and of the value chunks) gets a contiguous, balanced rank group
+      (fhespear_dist.stage_groups; with fewer ranks than chunks the chunks are dealt round-robin);
+    * the key chunks share one input, hence one set of baby steps: baby_mode "recompute" has every
+      rank rotate its share itself, "broadcast" has rank 0 compute the G baby steps once and broadcast
+      them (north_star "baby steps computed once and broadcast"; giant shard only);
+    * inside a group each chunk's BSGS is sharded by shard="giant" (giant groups, fhespear_dist.
+      bsgs_giant_sharded), "grid" (rb baby shares x giant columns, bsgs_grid_sharded; rb = the caller's
+      when it divides the group, else fhespear_dist.grid_rb) or "baby" (rb = group size); each rank
+      encodes only the diagonal rows it needs (encode_matrix_diagonals rows=);
+    * the square / relinearize / rescale of key chunk c run on its group root, which then broadcasts
+      the squared chunk to its group for the value matmul; the value chunks' rescaled outputs come to
+      rank 0 and are added there in chunk order, then the residual (tf:96-109).
+    Every term is the one-rank chain's: the output limbs are identical (tests/test_ffn_dist.py)."""
+
+    def __init__(self, ck, D, F, dist, rank, world, shard="giant", rb=None, baby_mode="recompute", device="cuda:0"):
+        import fhespear_dist as fd
+        if shard not in ("giant", "grid", "baby"):
+            raise ValueError(f"shard {shard!r}: 'giant', 'grid' or 'baby'")
+        if baby_mode not in ("recompute", "broadcast"):
+            raise ValueError(f"baby_mode {baby_mode!r}: 'recompute' or 'broadcast'")
+        self.ck, self.D, self.F, self.dist, self.rank, self.world = ck, D, F, dist, rank, world
+        self.shard, self.baby_mode, self.device = shard, baby_mode, device
+        self.G, self.B = bsgs_params(D)
+        self.chunks = int(np.ceil(F / D))
+        groups = fd.stage_groups(self.chunks, world)
+        self.groups = groups if groups is not None else [[c % world] for c in range(self.chunks)]
+        # process groups, made by every rank in the same order (torch.distributed.new_group is collective)
+        self.pg, self.rbs, self.cols = {}, {}, {}
+        for c, ranks in enumerate(self.groups):
+            key = tuple(ranks)
+            if key not in self.pg:
+                self.pg[key] = dist.new_group(list(ranks)) if len(ranks) > 1 else None
+                R = len(ranks)
+                r = 1 if shard == "giant" else (R if shard == "baby" else (rb if rb and R % rb == 0 else fd.grid_rb(R)))
+                self.rbs[key] = r
+                self.cols[key] = fd.grid_groups(dist, ranks, r) if r > 1 and R > 1 else {}
+
+    def _zero(self, ci):
+        ck = self.ck
+        return ck.encoder.encode_double_vector_batch(ck.ctx, np.zeros((self.G, ck.slots)), ck.scale, chain_index=ci)
+
+    def _rows(self, ranks):
+        import fhespear_dist as fd
+        R, idx, rb = len(ranks), ranks.index(self.rank), self.rbs[tuple(ranks)]
+        if rb == 1:
+            return [g * self.G + b for g in fd.giant_groups(self.B, R, idx) for b in range(self.G) if g * self.G + b < self.D]
+        return fd.grid_rows(self.G, self.B, self.D, R, rb, idx)
+
+    def matmul(self, ct, M, ranks, baby=None):
+        """bg:435-485 for one chunk over `ranks` (this rank among them): the rescaled output on ranks[0]."""
+        import fhespear_dist as fd
+        ck, ph = self.ck, self.ck.ph
+        G, B, D, ci = self.G, self.B, self.D, ct.chain_index()
+        if len(ranks) == 1:
+            return matmul(ck, ct, M, D, baby if baby is not None else baby_steps(ck, ct, G))
+        key = tuple(ranks)
+        rows = self._rows(ranks)
+        pts = dict(zip(rows, ck.encoder.encode_matrix_diagonals(ck.ctx, M, G, ck.scale, chain_index=ci, rows=rows)))
+        zero = self._zero(ci)
+        if self.rbs[key] == 1:
+            return fd.bsgs_giant_sharded(ph, ck.ctx, baby if baby is not None else baby_steps(ck, ct, G), pts, G, B, D,
+                                         ck.gk, zero, self.dist, self.device, ranks=ranks, group=self.pg[key])
+        return fd.bsgs_grid_sharded(ph, ck.ctx, ct, pts, G, B, D, ck.gk, zero[0], self.dist, self.rbs[key], self.device,
+                                    ranks=ranks, group=self.pg[key], col_groups=self.cols[key])
+
+    def block(self, ct_x, W_key, W_val):
+        """x -> x + W_val^T ((W_key^T x)^2) over the ranks; ct_x on rank 0, the output on rank 0."""
+        import fhespear_dist as fd
+        ck, ph, D, F, dist, me, dev = self.ck, self.ck.ph, self.D, self.F, self.dist, self.rank, self.device
+        cx = fd.broadcast_ciphertext(ph, ck.ctx, ct_x if me == 0 else None, 0, dist, dev)
+        baby = None
+        if self.baby_mode == "broadcast" and self.shard == "giant":   # G baby steps computed once
+            mine = baby_steps(ck, cx, self.G) if me == 0 else None
+            baby = fd.broadcast_ciphertexts(ph, ck.ctx, mine, 0, dist, dev, self.G)
+        elif any(len(r) == 1 and me in r for r in self.groups) or self.shard == "giant":
+            baby = baby_steps(ck, cx, self.G)            # shared by every chunk this rank computes whole
+        sq = {}
+        for c, ranks in enumerate(self.groups):          # key chunks (tf:38-55) + square (tf:57-61)
+            if me not in ranks:
+                continue
+            lo, hi = c * D, min(c * D + D, F)
+            if hi - lo == D and not HOST_DIAGONALS[0]:
+                M = W_key[:, lo:hi].T
+            else:
+                M = np.zeros((D, D))
+                M[:hi - lo, :] = W_key[:, lo:hi].T
+            k = self.matmul(cx, M, ranks, baby if len(ranks) == 1 or self.shard == "giant" else None)
+            if me == ranks[0]:
+                s = ph.relinearize(ck.ctx, ph.multiply(ck.ctx, k, k), ck.rlk)
+                sq[c] = ph.rescale_to_next(ck.ctx, s)
+        parts = {}
+        for c, ranks in enumerate(self.groups):          # value chunks (tf:65-91)
+            if me not in ranks:
+                continue
+            s = sq.get(c) if me == ranks[0] else None
+            if len(ranks) > 1:
+                s = fd.broadcast_ciphertext(ph, ck.ctx, s, ranks[0], dist, dev, group=self.pg[tuple(ranks)])
+            lo, hi = c * D, min(c * D + D, F)
+            if hi - lo == D and not HOST_DIAGONALS[0]:
+                M = W_val[lo:hi, :].T
+            else:
+                M = np.zeros((D, D))
+                M[:, :hi - lo] = W_val[lo:hi, :].T
+            p = self.matmul(s, M, ranks)
+            if me == ranks[0]:
+                parts[c] = p
+        acc = None
+        for c, ranks in enumerate(self.groups):          # parts to rank 0, added in chunk order
+            got = fd.send_ciphertext(ph, ck.ctx, parts.get(c), ranks[0], 0, dist, dev)
+            if me == 0:
+                if acc is None:
+                    acc = got
+                else:
+                    acc, got = align(ph, ck.ctx, acc, got)
+                    acc = ph.add(ck.ctx, acc, got)
+        if me != 0:
+            return None
+        xa, acc = align(ph, ck.ctx, ct_x, acc)           # tf:96-109
+        acc.set_scale(xa.scale())
+        return ph.add(ck.ctx, xa, acc)
+
+
 def plain_ffn(x, W_key, W_val):
     return x + (x @ W_key) ** 2 @ W_val
 
@@ -204,6 +333,43 @@ def run_chain(ck, x_cal, W_keys, W_vals, D, F, use_bootstrap, log=print):
     return out
 
 
+def ct_digest(ct):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(ct.to_numpy()).tobytes()).hexdigest()
+
+
+def run_ranks(ph, a, dist, rank, world, device):
+    """--blocks FFN blocks (random weights, same seeds on every rank) through FfnRanks on rank 0's chain
+    (world 1 without --dist: the one-rank ffn_block); rank 0 prints the final ciphertext's limb digest,
+    the per-block times and the decrypted error against the plaintext chain."""
+    rng = np.random.default_rng(42)
+    ck = Ckks(ph, a.N, a.L0, a.P, a.D)
+    x = rng.normal(0, 0.1, a.D)
+    ct = ck.encrypt_replicated(x) if rank == 0 else None
+    ref = x.copy()
+    fr = FfnRanks(ck, a.D, a.F, dist, rank, world, a.shard, a.rb, a.baby_mode, device) if dist is not None else None
+    times = []
+    for b in range(a.blocks):
+        Wk = rng.normal(0, 0.02, (a.D, a.F))
+        Wv = rng.normal(0, 0.02, (a.F, a.D))
+        if dist is not None:
+            dist.barrier()
+        ck.ctx.synchronize()
+        t0 = time.perf_counter()
+        ct = fr.block(ct, Wk, Wv) if fr is not None else ffn_block(ck, ct, Wk, Wv, a.D, a.F)
+        ck.ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+        times.append(time.perf_counter() - t0)
+        ref = plain_ffn(ref, Wk, Wv)
+        if rank == 0:
+            err = float(np.max(np.abs(ck.decrypt(ct, a.D) - ref)))
+            print(f"block {b}: {1e3 * times[-1]:.1f} ms chain_index={ct.chain_index()} max_err={err:.3e}", flush=True)
+    if rank == 0:
+        print(f"ffn world {world} shard {a.shard if dist is not None else 'none'} babies {a.baby_mode}: "
+              f"mean block {1e3 * np.mean(times):.1f} ms, ct_sha256 {ct_digest(ct)}", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--N", type=int, default=16384)
@@ -215,9 +381,36 @@ def main():
     ap.add_argument("--bootstrap", action="store_true")
     ap.add_argument("--host-diagonals", action="store_true",
                     help="numpy diagonal prep as the reference caller does (default: pyPhantom encode_matrix_diagonals)")
+    ap.add_argument("--dist", action="store_true",
+                    help="blocks over ranks (torchrun; SURVEY §8e Config 5): FfnRanks, even at world 1")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--shard", default="giant", choices=("giant", "grid", "baby"))
+    ap.add_argument("--rb", type=int, default=None)
+    ap.add_argument("--baby-mode", default="recompute", choices=("recompute", "broadcast"))
     a = ap.parse_args()
     HOST_DIAGONALS[0] = a.host_diagonals
+    import os
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.dist or world > 1:
+        import torch
+        import torch.distributed as dist
+        rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+        if a.backend == "nccl":               # RCCL over xGMI, one GPU per rank
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:                                 # gloo: host-staged exchange (ranks may share a GPU)
+            dist.init_process_group("gloo")
+            local = int(os.environ.get("FHESPEAR_DEVICE", local))
+        os.environ["FHESPEAR_DEVICE"] = str(local)
+        import pyPhantom as ph
+        run_ranks(ph, a, dist, rank, world, f"cuda:{local}")
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     import pyPhantom as ph
+    if not a.bootstrap and a.blocks and os.environ.get("FFN_DIGEST"):   # the one-rank reference of --dist runs
+        run_ranks(ph, a, None, 0, 1, "cuda:0")
+        return
     rng = np.random.default_rng(42)
     if a.bootstrap:
         t0 = time.perf_counter()

@@ -2,7 +2,7 @@
 # GPU box: one parametrised script for every gpurun call (replaces the per-round one-offs).
 #   tools/gpu.sh OUT STEP [STEP ...]      (OUT is a directory under gpurun_out/)
 # Steps, run in order, each under its own time limit; the script stops at the first failure:
-#   tests[=pytest args]     GPU suite (default: all of tests/ -m gpu)           -> OUT/pytest.log
+#   tests[=pytest args]     GPU suite (default: all of tests/ -m gpu; args may quote, e.g. -k 'a or b')
 #   smoke                   __graft_entry__.smoke()                              -> OUT/smoke.log
 #   bench[=bench args]      one bench line (default: the driver's default line)  -> OUT/bench.json
 #   ab=NAME[:ENV=v,ENV=v]   cfg2 matvec-only bench under extra environment       -> OUT/ab_NAME.json
@@ -27,7 +27,8 @@ for step in "$@"; do
     [ "$name" != "$step" ] && arg=${step#*=}
     case "$name" in
     tests)
-        timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 300 --timeout-method thread $arg \
+        # eval: quotes inside the step's argument group (e.g. -k 'a or b')
+        eval "timeout -k 10 1500 python -u -m pytest -m gpu -x -v --durations=25 --timeout 300 --timeout-method thread ${arg:-tests}" \
             > "$OUT/pytest.log" 2>&1 || fail tests "$OUT/pytest.log"
         tail -1 "$OUT/pytest.log" ;;
     smoke)

@@ -100,12 +100,11 @@ def _wkv(block, xs, r, k, v, state, v_first):
         v = v + (v_first - v) * sigmoid(block.v0 + (xs["v"] @ block.v1) @ block.v2)
         v_h = v.reshape(H, hs)
         v_first_out = v_first
-    new_state = state.copy()
-    wkv_heads = np.zeros((H, hs))
-    for h in range(H):
-        sa = new_state[h] @ (-kk_h[h])
-        new_state[h] = new_state[h] * decay[h] + np.outer(sa, kk_h[h] * a_h[h]) + np.outer(v_h[h], k_h[h])
-        wkv_heads[h] = new_state[h] @ r_h[h]
+    # every head at once (bg:838-845 loop over heads): sa = S (-kk), S' = S diag(decay) + sa (kk a)^T + v k^T,
+    # wkv = S' r
+    sa = np.einsum("hij,hj->hi", state, -kk_h)
+    new_state = state * decay[:, None, :] + sa[:, :, None] * (kk_h * a_h)[:, None, :] + v_h[:, :, None] * k_h[:, None, :]
+    wkv_heads = np.einsum("hij,hj->hi", new_state, r_h)
     wkv = group_norm(wkv_heads.reshape(D), H, block.ln_x_w, block.ln_x_b)
     wkv = wkv + ((r_h * k_h * block.r_k).sum(axis=1, keepdims=True) * v_h).reshape(D)
     g = sigmoid(xs["g"] @ block.g1) @ block.g2
@@ -177,6 +176,18 @@ class Server:
 
     def decrypt_vec_complex(self, ct, n):
         return np.array(self.encoder.decode_complex_vector(self.ctx, self.sk.decrypt(self.ctx, ct)))[:n]
+
+    # the client's calls of one stage batched: one encode upload for all its inputs, one synchronisation
+    # for all its decodes (pyPhantom encode_*_batch, decode_batch) -- the same values as one at a time
+    def encrypt_replicated_batch(self, xs, cplx=False):
+        reps = -(-self.slots // len(xs[0]))
+        rows = np.stack([np.tile(np.asarray(x), reps)[:self.slots] for x in xs])
+        enc = self.encoder.encode_complex_vector_batch if cplx else self.encoder.encode_double_vector_batch
+        return [self.sk.encrypt_symmetric(self.ctx, pt) for pt in enc(self.ctx, rows, self.scale)]
+
+    def decrypt_vecs(self, cts, n):
+        """complex slots [len(cts), n] (real parts for real-packed outputs)"""
+        return self.encoder.decode_batch(self.ctx, [self.sk.decrypt(self.ctx, c) for c in cts], n)
 
     # bg:361-432
     def encode_real(self, M, rows=None):
@@ -499,77 +510,87 @@ def _scale_word(scale, like):
     return torch.tensor([scale], dtype=torch.float64).view(torch.int64).to(like.device)
 
 
+def _enc(srv, xs, cplx=False):
+    """the stage's inputs encrypted together when the server batches (Server), else one at a time"""
+    if hasattr(srv, "encrypt_replicated_batch"):
+        return srv.encrypt_replicated_batch(xs, cplx)
+    return [srv.encrypt_replicated_complex(x.real, x.imag) if cplx else srv.encrypt_replicated(x) for x in xs]
+
+
+def _dec(srv, cts, n):
+    if hasattr(srv, "decrypt_vecs"):
+        return srv.decrypt_vecs(cts, n)
+    return np.stack([srv.decrypt_vec_complex(c, n) for c in cts])
+
+
 def client_aided_block(run, x, x_prev_att, x_prev_ffn, state, v_first):
     """bg:756-899 with the server projections dealt by `run` (BlockRunner).  The client (rank 0)
-    computes; other ranks return None for the activations but take part in every stage."""
+    computes; other ranks return None for the activations but take part in every stage.
+    Timings (seconds): server_<stage> = the stage's projections alone (input broadcast, matvecs, output
+    gather); client_encrypt / client_decrypt = the client's encode+encrypt and decrypt+decode calls (one
+    batch per stage); client_numpy = its float64 math (layer norms, WKV state, gates)."""
     srv, block, client = run.srv, run.block, run.rank == 0
     D = block.D
-    t = {}
+    t = {"client_encrypt": 0.0, "client_decrypt": 0.0, "client_numpy": 0.0}
     sync = srv.ctx.synchronize
+    clock = time.perf_counter
 
-    def timed(key, fn):
+    def timed(key, fn, *args):
         sync()
-        t0 = time.perf_counter()
-        r = fn()
+        t0 = clock()
+        r = fn(*args)
         sync()
-        t[key] = time.perf_counter() - t0
+        t[key] = t.get(key, 0.0) + clock() - t0
         return r
 
+    def enc(xs, cplx=False):
+        return timed("client_encrypt", _enc, srv, xs, cplx) if client else [None] * len(xs)
+
+    def dec(cts):
+        return timed("client_decrypt", _dec, srv, cts, D)
+
+    t0 = clock()
     x_ln = xs = None
     if client:
         x_ln, xs = _mix(block, x, x_prev_att)
-
-    def rkv():
-        ins = {}
-        for n in ("r", "k", "v"):
-            ins[n] = (srv.encrypt_replicated(xs[n]) if client else None, n)
-        outs = run.stage(0, ins)
-        return {n: srv.decrypt_vec(outs[n], D) for n in outs} if client else None
-    dec = timed("server_rkv", rkv)
-
+    t["client_numpy"] += clock() - t0
+    cts = enc([xs[n] for n in ("r", "k", "v")] if client else [0, 0, 0])
+    outs = timed("server_rkv", run.stage, 0, {n: (c, n) for n, c in zip(("r", "k", "v"), cts)})
     gated = new_state = v_first_out = None
     if client:
-        gated, new_state, v_first_out = _wkv(block, xs, dec["r"], dec["k"], dec["v"], state, v_first)
-
-    def wo():
-        outs = run.stage(1, {"o": (srv.encrypt_replicated(gated) if client else None, "o")})
-        return srv.decrypt_vec(outs["o"], D) if client else None
-    att = timed("server_wo", wo)
-
+        d = dec([outs[n] for n in ("r", "k", "v")]).real
+        t0 = clock()
+        gated, new_state, v_first_out = _wkv(block, xs, d[0], d[1], d[2], state, v_first)
+        t["client_numpy"] += clock() - t0
+    (ct_o,) = enc([gated] if client else [0])
+    outs = timed("server_wo", run.stage, 1, {"o": (ct_o, "o")})
     x_k_ffn = x_ffn_ln = None
     if client:
+        att = dec([outs["o"]])[0].real
+        t0 = clock()
         x = x + att
         x_ffn_ln = layer_norm(x, block.ln2_w, block.ln2_b)
         x_k_ffn = x_ffn_ln + (x_prev_ffn - x_ffn_ln) * block.x_k_ffn
-
+        t["client_numpy"] += clock() - t0
     n_pairs = block.F // D // 2
-
-    def ffn_key():
-        ct = srv.encrypt_replicated(x_k_ffn) if client else None
-        outs = run.stage(2, {f"ffn_key_{p}": (ct, "x_k_ffn") for p in range(n_pairs)})
-        if not client:
-            return None
+    (ct_k,) = enc([x_k_ffn] if client else [0])
+    outs = timed("server_ffn_key", run.stage, 2, {f"ffn_key_{p}": (ct_k, "x_k_ffn") for p in range(n_pairs)})
+    fk_sq = None
+    if client:
+        z = dec([outs[f"ffn_key_{p}"] for p in range(n_pairs)])
+        t0 = clock()
         fk = np.empty(block.F)
         for p in range(n_pairs):             # bg:585-587: real -> chunk 2p, imag -> chunk 2p+1
-            z = srv.decrypt_vec_complex(outs[f"ffn_key_{p}"], D)
-            fk[2 * p * D:(2 * p + 1) * D] = z.real
-            fk[(2 * p + 1) * D:(2 * p + 2) * D] = z.imag
-        return fk
-    fk = timed("server_ffn_key", ffn_key)
-    fk_sq = np.maximum(fk, 0.0) ** 2 if client else None
-
-    def ffn_val():
-        ins = {}
-        for p in range(n_pairs):             # bg:612-640: Enc(x0 + i x1) against (M0, -M1)
-            c0 = fk_sq[2 * p * D:(2 * p + 1) * D] if client else None
-            c1 = fk_sq[(2 * p + 1) * D:(2 * p + 2) * D] if client else None
-            ins[f"ffn_val_{p}"] = (srv.encrypt_replicated_complex(c0, c1) if client else None, f"v{p}")
-        outs = run.stage(3, ins)
-        if not client:
-            return None
-        return sum(srv.decrypt_vec_complex(outs[f"ffn_val_{p}"], D).real for p in range(n_pairs))
-    v_ffn = timed("server_ffn_val", ffn_val)
+            fk[2 * p * D:(2 * p + 1) * D] = z[p].real
+            fk[(2 * p + 1) * D:(2 * p + 2) * D] = z[p].imag
+        fk_sq = np.maximum(fk, 0.0) ** 2
+        t["client_numpy"] += clock() - t0
+    # bg:612-640: Enc(x0 + i x1) against (M0, -M1)
+    cts = enc([fk_sq[2 * p * D:(2 * p + 1) * D] + 1j * fk_sq[(2 * p + 1) * D:(2 * p + 2) * D]
+               for p in range(n_pairs)] if client else [0] * n_pairs, cplx=True)
+    outs = timed("server_ffn_val", run.stage, 3, {f"ffn_val_{p}": (cts[p], f"v{p}") for p in range(n_pairs)})
     if client:
+        v_ffn = dec([outs[f"ffn_val_{p}"] for p in range(n_pairs)]).real.sum(axis=0)
         x = x + v_ffn
     return x, x_ln, x_ffn_ln, new_state, v_first_out, t
 
@@ -601,8 +622,9 @@ def run_blocks(ph, args, dist=None, rank=0, world=1, device=0, log=print):
         if rank == 0:
             err = float(np.max(np.abs(st[0] - ref[0])))
             corr = float(np.corrcoef(st[0], ref[0])[0, 1])
-            sec = sum(tm.values())
-            rec = dict(block=b, server_seconds=sec, stages=tm, max_err=err, corr=corr,
+            sec = sum(v for k, v in tm.items() if k.startswith("server_"))
+            rec = dict(block=b, server_seconds=sec, client_seconds=sum(v for k, v in tm.items() if k.startswith("client_")),
+                       stages=tm, max_err=err, corr=corr,
                        mag=float(np.max(np.abs(ref[0]))),
                        x_sha256=hashlib.sha256(np.ascontiguousarray(st[0]).tobytes()).hexdigest())
             recs.append(rec)
