@@ -145,7 +145,8 @@ static bool conv_pm_ok(uint64_t q, int ns) {
 // convert3x_value, fhs_kernels.hip k_centered_x): per digit j (primes 3j..3j+2, j < dnum with 3j + 3 <=
 // L0) the exact Q_S / q_u, the rounding thresholds ((2k - 1) Q_S + 1) / 2 and 2^179 - v Q_S (192-bit
 // words, little-endian) into xd[j][32]; per prime m the base-2^60 weights 2^60, 2^120 mod m (split-30
-// packed) and -2^179 mod m into xt[i][4].  |X| < Q_S / 2 < 2^176, so U = X + 2^179 lies in (0, 2^180).
+// packed) and -2^179 mod m into xt[i][4].  |X| < Q_S / 2 < 2^179 (three primes below 2^60; < 2^176 for the
+// 59-bit chain), so U = X + 2^179 lies in (0, 2^180): exactly three 60-bit words.
 static void modup_xform_tables(const uint64_t* primes, int K, int L0, int dnum, uint64_t* xd, uint64_t* xt) {
     auto mul192 = [](const uint64_t a[3], uint64_t m, uint64_t r[3]) {   // r = a m mod 2^192
         hu128 cy = 0;
@@ -3153,6 +3154,8 @@ extern "C" fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* 
     if (!q3 || !y3 || !out) return FHS_ERR_INVALID;
     const uint64_t w = pm_word(m, 14);
     if (!w || !conv_pm_ok(m, 3)) return fail(FHS_ERR_INVALID, "debug_modup_xform: target not on the pseudo-Mersenne fold");
+    for (int u = 0; u < 3; ++u)   // centered_x_pack has three rounding thresholds: S < 3 Q_S needs y < q
+        if (y3[u] >= q3[u]) return fail(FHS_ERR_INVALID, "debug_modup_xform: residues must be < q");
     const uint64_t pr[4] = {q3[0], q3[1], q3[2], m};
     uint64_t xd[32] = {0}, xt[16] = {0};
     modup_xform_tables(pr, 4, 3, 1, xd, xt);
@@ -3174,6 +3177,8 @@ extern "C" fhs_status fhs_debug_moddown_xform(const uint64_t* p3, const uint64_t
     if (!w || !conv_pm_ok(q, 3)) return fail(FHS_ERR_INVALID, "debug_moddown_xform: target not on the pseudo-Mersenne fold");
     for (int k = 0; k < 3; ++k)
         if (p3[k] >= (1ull << 59)) return fail(FHS_ERR_INVALID, "debug_moddown_xform: special primes must be < 2^59");
+    for (int k = 0; k < 3; ++k)
+        if (y3[k] >= p3[k]) return fail(FHS_ERR_INVALID, "debug_moddown_xform: residues must be < p");
     uint64_t xd[32] = {0}, xt[4] = {0};
     for (int u = 0; u < 3; ++u) {   // as fhs_context_create's md_xd
         const hu128 h = (hu128)p3[(u + 1) % 3] * p3[(u + 2) % 3];

@@ -44,8 +44,19 @@ struct DevTables {
                               // l % 3 == 0), 1 (P = 1:
                               // modup_convert1), 0 (generic)
 };
-// ModUp of level l reads the X form (k_centered_x + modup_convert3x) instead of residues + counts
-inline bool modup_xform(const DevTables& T, int l) { return T.modup_dp == 3 && l % 3 == 0 && T.logN >= 9; }
+// The ModUp launch shape and the input form it reads are decided by these two predicates only
+// (launch_centered writes the X form exactly when launch_modup's k_modup_h<.., 3> reads it).
+#ifndef FHS_MODUP_HALF
+#define FHS_MODUP_HALF 1       // k_modup_h: half-limb LDS, two workgroups per CU
+#endif
+#ifndef FHS_NTT_HALF_MIN
+#define FHS_NTT_HALF_MIN 14    // generic NTT kernels use the half-limb form (two workgroups per CU) from this LOGN
+#endif
+// ModUp runs the half-limb kernel k_modup_h (else the full-limb k_modup, which reads residues + counts)
+constexpr bool modup_uses_half(int logN) { return (FHS_MODUP_HALF && logN >= 9) || logN >= FHS_NTT_HALF_MIN; }
+// ModUp of level l reads the X form (k_centered_x + modup_convert3x) instead of residues + counts: full
+// 3-limb digits on the half-limb kernel's DP = 3 instantiation
+inline bool modup_xform(const DevTables& T, int l) { return T.modup_dp == 3 && l % 3 == 0 && modup_uses_half(T.logN); }
 
 // One key-switch of a batch: out = KS_key( galois_elt(a) ) + (galois_elt(add0), add1).
 // Items whose `a` is the same polynomial share ONE ModUp (hoisting): the exact centred base

@@ -32,7 +32,6 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 // alternatives and their records are listed in DESIGN.md and profiles/r0*/ab_*).
 #define FHS_INNER_WAVES 16     // waves per k_bsgs_inner workgroup sharing one LDS baby-step slice
 #define FHS_INNER_VEC 2        // consecutive coefficients per lane in k_bsgs_inner (16-byte loads)
-#define FHS_MODUP_HALF 1       // k_modup_h: half-limb LDS, two workgroups per CU
 #define FHS_MODDOWN_HALF 1     // k_moddown_h: half-limb LDS
 #define FHS_INTT_HALF 1        // k_ks_intt_h: half-limb LDS inverse NTT
 #ifndef FHS_MODUPH_CH
@@ -116,10 +115,7 @@ constexpr size_t lds_bytes() { return (size_t)((1 << LOGN) + (1 << LOGN) / 16) *
 // ---- one-limb transforms, full limb in LDS (N <= 16384: 136 KiB) or half a limb (N = 32768):
 // the half form does the global first forward stage / last inverse stage, which pairs e with
 // e + N/2, in registers and transforms each half in LDS (k_modup_h explains the scheme).
-#ifndef FHS_NTT_HALF_MIN
-#define FHS_NTT_HALF_MIN 14   // generic NTT kernels use the half-limb form (two workgroups per CU) from this LOGN
-                              // (A/B at N = 16384: 2048-diagonal encode + matvec 18.64 -> 18.12 ms, bench unchanged)
-#endif
+// FHS_NTT_HALF_MIN (fhs_kernels.h): A/B at N = 16384, 2048-diagonal encode + matvec 18.64 -> 18.12 ms, bench unchanged
 template <int LOGN> constexpr bool ntt_half() { return LOGN >= FHS_NTT_HALF_MIN; }
 template <int LOGN, bool H = ntt_half<LOGN>()> constexpr int ntt_threads() { return H ? (1 << LOGN) / 32 : (1 << LOGN) / 16; }
 template <int LOGN, bool H = ntt_half<LOGN>()> constexpr int ntt_lds_words() {
@@ -928,9 +924,10 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     const int mgrid = xcd_grid(E, dn * U);
     const dim3 g(mgrid), b((1 << LOGN) / 32);
-    if (!((FHS_MODUP_HALF && LOGN >= 9) || ntt_half<LOGN>()))
+    static_assert(modup_uses_half(LOGN) || !ntt_half<LOGN>(), "the full-limb ModUp needs N <= 16384");
+    if (!modup_uses_half(LOGN))   // residues + counts (launch_centered wrote no X form: modup_xform is false)
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
-    else if (T.modup_dp == 3 && l % 3 == 0)   // every digit of this level full (3 limbs)
+    else if (modup_xform(T, l))   // every digit of this level full (3 limbs), X form (launch_centered)
         hipLaunchKernelGGL((k_modup_h<LOGN, 3>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else if (T.modup_dp == 1)
         hipLaunchKernelGGL((k_modup_h<LOGN, 1>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);

@@ -193,7 +193,7 @@ __host__ __device__ __forceinline__ bool ge192(const u64 s[3], const u64* t) {
     return s[2] != t[2] ? s[2] > t[2] : (s[1] != t[1] ? s[1] > t[1] : s[0] >= t[0]);
 }
 // y[u] (< q_u) -> U = X + 2^179 as split-30 packed base-2^60 words, X = S - v Q_S the centred digit
-// value: S = sum_u y_u Q_S/q_u < 3 Q_S, v = round(S/Q_S) (never a tie: Q_S is odd), |X| < Q_S/2 < 2^176
+// value: S = sum_u y_u Q_S/q_u < 3 Q_S, v = round(S/Q_S) (never a tie: Q_S is odd), |X| < Q_S/2 < 2^179 (primes < 2^60)
 __host__ __device__ __forceinline__ void centered_x_pack(const u64 y[3], const u64* D, u64 out[3]) {
     u128x lo = 0;   // S below 2^128
     u64 s2 = 0;     // S >> 128

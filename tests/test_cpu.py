@@ -333,6 +333,43 @@ def test_modup_xform_matches_centred_extension(orc):
                 assert out.value == X % qs[t], (j, t, y)
 
 
+def test_modup_xform_on_60_bit_primes(orc):
+    """The X form's edge: with 60-bit primes q = 2^60 - d, |X| < Q_S/2 < 2^179 and
+    U = X + 2^179 < 2^180 fill the three 60-bit words.  Residues at y = q - 1, zero, and sums steered to
+    both sides of every rounding threshold k + 1/2 (k = 0, 1, 2) against big integers; a residue >= q
+    (outside centered_x_pack's three thresholds) is rejected, not mis-rounded."""
+    import ctypes
+    from math import prod
+    lib = _lib()
+    U64 = ctypes.c_uint64
+    lib.fhs_debug_modup_xform.argtypes = [ctypes.POINTER(U64), ctypes.POINTER(U64), U64, ctypes.POINTER(U64)]
+    qs = orc.create_coeff_modulus(16384, [60] * 15)
+    assert all((1 << 59) < q < (1 << 60) for q in qs)
+    rng = np.random.default_rng(41)
+    out = U64()
+    for j in range(3):
+        q3 = qs[3 * j:3 * j + 3]
+        Q = prod(q3)
+        targets = [t for t in range(15) if t // 3 != j]
+        cases = [[q - 1 for q in q3], [0, 0, 0], [q3[0] - 1, q3[1] - 1, 0]]
+        for k in range(3):   # S / Q next to k + 1/2, from below and above
+            for delta in (-2, -1, 0, 1, 2):
+                y = [int(rng.integers(0, q)) for q in q3]
+                f = y[0] / q3[0] + y[1] / q3[1]
+                target = (k + 0.5 - f) % 1.0
+                y[2] = (int(target * q3[2]) + delta) % q3[2]
+                cases.append(y)
+        for y in cases:
+            S = sum(yu * (Q // qu) for yu, qu in zip(y, q3))
+            X = S - ((2 * S + Q) // (2 * Q)) * Q
+            assert 2 * abs(X) < Q and abs(X) < 2 ** 179 and X + 2 ** 179 < 2 ** 180
+            for t in targets:
+                assert lib.fhs_debug_modup_xform((U64 * 3)(*q3), (U64 * 3)(*y), qs[t], ctypes.byref(out)) == 0
+                assert out.value == X % qs[t], (j, t, y)
+        bad = [q3[0], 0, 0]
+        assert lib.fhs_debug_modup_xform((U64 * 3)(*q3), (U64 * 3)(*bad), qs[targets[0]], ctypes.byref(out)) != 0
+
+
 def test_moddown_xform_matches_fast_base_conversion(orc):
     """ModDown's X form (k_special_x + moddown_convert3x, the same __host__ __device__ routines through
     fhs_debug_moddown_xform) against big integers: (sum_k y_k P/p_k) mod q_i, the fast base conversion's
