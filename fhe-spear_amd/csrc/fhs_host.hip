@@ -119,6 +119,8 @@ static uint64_t pm_word(uint64_t q, int logN) {
     return (d << 8) | (lazy ? 128u : 0u) | (uint64_t)b;
 }
 
+// A 59-bit prime q = 2^59 - d with d < 2^27: the precondition of convert3x_b59's bounds.
+static bool b59_prime(uint64_t q) { return q < (1ull << 59) && (1ull << 59) - q < (1ull << 27); }
 // Bit 40 of PrimeK.pm: the ModUp conversion may reduce its split-30 sums directly
 // (fhs_modarith.h acc3_reduce_pm): with ns <= P source limbs (< 2^60 each) and the v (Q mod m)
 // correction folded into L, every intermediate of that routine stays in its word and the result is
@@ -929,6 +931,11 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     for (int i = 0; i < K && P == 3; ++i) small_e1 = small_e1 && mu_xt[(size_t)i * 4] < (1ull << 30);
     T.modup_dp = (P == 3 && L0 % 3 == 0 && all_cpm && small_e1) ? 3 : (P == 1 ? 1 : 0);
     T.md_xform = T.modup_dp == 3 && md_x_ok;
+    // every prime 2^59 - d with d < 2^27 (SEAL's 59-bit Create() primes at N <= 65536): the X-form
+    // conversions reduce with compile-time folds (convert3x_b59)
+    bool b59 = T.modup_dp == 3;
+    for (int i = 0; i < K && b59; ++i) b59 = b59_prime(c->q[i]);
+    T.conv_b59 = b59;
     HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");
     HIPCHK(up(twf.data(), 8 * twf.size(), (const void**)&T.tw_fwd), "tables");
     HIPCHK(up(twi.data(), 8 * twi.size(), (const void**)&T.tw_inv), "tables");
@@ -3148,8 +3155,13 @@ extern "C" fhs_status fhs_context_stream(fhs_context* c, void** stream) {
     return FHS_OK;
 }
 
+// x (any 64-bit value, or a value < 2m when canonical is asked) congruent to want (< m)?
+static bool x_ok(uint64_t x, uint64_t want, uint64_t m, bool lt2m) {
+    return (!lt2m || x < 2 * m) && x % m == want;
+}
 // The ModUp X form's arithmetic on the host (the same __host__ __device__ routines the kernels run):
 // y3 (residues of a 3-prime digit q3, after the inverse-hat scaling) -> the centred digit value mod m.
+// For a 59-bit target the kernels' convert3x_b59 (folded and unfolded) must give congruent values.
 extern "C" fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* y3, uint64_t m, uint64_t* out) {
     if (!q3 || !y3 || !out) return FHS_ERR_INVALID;
     const uint64_t w = pm_word(m, 14);
@@ -3167,6 +3179,13 @@ extern "C" fhs_status fhs_debug_modup_xform(const uint64_t* q3, const uint64_t* 
                                        (unsigned)(w & 127), (unsigned)(w >> 8));
     if (x >= 2 * m) return fail(FHS_ERR_INVALID, "debug_modup_xform: result above 2m");
     *out = x >= m ? x - m : x;
+    if (b59_prime(m)) {
+        const uint32_t d = (uint32_t)((1ull << 59) - m);
+        for (int canon = 0; canon < 2; ++canon)
+            if (!x_ok(convert3x_b59(words[0], words[1], words[2], (uint32_t)t[0], unpack30(t[1]), t[2], d, canon), *out,
+                      m, canon))
+                return fail(FHS_ERR_INVALID, "debug_modup_xform: convert3x_b59 disagrees");
+    }
     return FHS_OK;
 }
 // ModDown's X form on the host (k_special_x + moddown_convert3x arithmetic): y3 (special residues < p_k,
@@ -3194,6 +3213,13 @@ extern "C" fhs_status fhs_debug_moddown_xform(const uint64_t* p3, const uint64_t
                                        (unsigned)(w & 127), (unsigned)(w >> 8));
     if (x >= 2 * q) return fail(FHS_ERR_INVALID, "debug_moddown_xform: result above 2q");
     *out = x >= q ? x - q : x;
+    if (b59_prime(q)) {
+        const uint32_t d = (uint32_t)((1ull << 59) - q);
+        for (int canon = 0; canon < 2; ++canon)
+            if (!x_ok(convert3x_b59(words[0], words[1], words[2], (uint32_t)xt[0], unpack30(xt[1]), 0, d, canon), *out,
+                      q, canon))
+                return fail(FHS_ERR_INVALID, "debug_moddown_xform: convert3x_b59 disagrees");
+    }
     return FHS_OK;
 }
 extern "C" fhs_status fhs_debug_reduce128(uint64_t q, uint64_t lo, uint64_t hi, uint64_t* out, int* pm_used) {

@@ -744,7 +744,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 16) k_modup(DevTables T, const u
 // (pseudo-Mersenne fold, PrimeK.pm bit 40), radix-4 first stages (fwd_quad_first2), buffer loads:
 // x = V0 + V1 e1 + V2 e2 + c3 (e1 = 2^60, e2 = 2^120, c3 = -2^179 mod m) as split-30 sums (each within
 // the 3-product bounds conv_pm_ok proves for this prime), folded by acc3_reduce_pm to [0, 2m).
-template <int LOGN>
+template <int LOGN, bool B59>
 __device__ __forceinline__ void modup_convert3x(const u64* yb, const u64* xt, const RedU& R, const u64* tw, int tid,
                                                 u64* lds, u64 hi[16]) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32, CH = FHS_MODUPH_CH;
@@ -765,7 +765,10 @@ __device__ __forceinline__ void modup_convert3x(const u64* yb, const u64* xt, co
         }
         u64 x[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = convert3x_value(V[0][k], V[1][k], V[2][k], e1, e2, c3, R.b, R.d);
+        for (int k = 0; k < 4; ++k)   // B59: the upper half (k >= 2) is multiplied by the stage-0 twiddle first,
+                                      // so any congruent 64-bit value will do (no final fold)
+            x[k] = B59 ? convert3x_b59(V[0][k], V[1][k], V[2][k], e1, e2, c3, R.d, k < 2)
+                       : convert3x_value(V[0][k], V[1][k], V[2][k], e1, e2, c3, R.b, R.d);
         fwd_quad_first2<TH>(x, w4, m, R.lazy, lds, tid, ch, hi);
     }
 }
@@ -810,7 +813,7 @@ constexpr int modup_h_lds_words() { return (1 << (LOGN - 1)) + (1 << (LOGN - 1))
 // DP: the digit size with a specialised conversion compiled in (3: modup_convert3x, 1: modup_convert1,
 // 0: the generic loop only) -- one instantiation per context shape, so the rarely used paths cost the
 // usual one no registers
-template <int LOGN, int DP>
+template <int LOGN, int DP, bool B59>
 __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoef, const unsigned char* vcnt, u64* ext,
                                              int l, int t, int mi, int tid, u64* lds) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;   // 16 coefficient pairs per thread
@@ -836,7 +839,7 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
     if constexpr (DP == 3) {   // every digit 3 limbs, every target on the fold (launch_modup checks)
         // the usual digit (P = 3 limbs, pseudo-Mersenne target): compile-time digit size, buffer loads
         // whose limb / chunk offsets are scalar (no per-load address arithmetic on the VALU)
-        modup_convert3x<LOGN>(yb, T.modup_xt + (size_t)pt * 4, R, tw, tid, lds, hi);
+        modup_convert3x<LOGN, B59>(yb, T.modup_xt + (size_t)pt * 4, R, tw, tid, lds, hi);
     } else if (DP == 1 && ns == 1 && PK(T, s0).q <= 3 * m) {   // y + v negQ < q_u + m <= 4 m: the NTT's input bound
         modup_convert1<LOGN>(yb, vb, negQ, m, w0, w0p, tid, lds, hi);
     } else {
@@ -900,14 +903,26 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
         // the radix-4 conversion (modup_convert3x, FHS_MODUP_R4) did each half's local stage 0 already
         constexpr int S0 = DP == 3 ? 1 : 0;
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0>(lds, tid, tw, m, R.lazy, 1 + h);
-        // buffer stores: per-lane offset tid, the half / row offset in soffset
+        // buffer stores: per-lane offset tid, the half / row offset in soffset.  The extended limbs feed only
+        // the key inner products, whose split-30 sums take any value < 2^60: lazy outputs are folded once
+        // (pm_fold_lt60), without fwd_canon's final subtraction.  The wave-uniform lazy choice is made once
+        // per sweep, outside the unrolled loop, so its 16 LDS reads issue together (a choice per element
+        // split the loop into blocks, each waiting for its own read)
         const __amdgpu_buffer_rsrc_t ro = brsrc(o, N * 8);
+        if (R.lazy) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-            bstore64_aux<FHS_MODUP_STORE_AUX>(fwd_canon(lds[row_pad<TH>(tid, c)], R), ro, tid * 8, (h * NH + c * TH) * 8);
+            for (int c = 0; c < 16; ++c)
+                bstore64_aux<FHS_MODUP_STORE_AUX>(pm_fold_lt60(lds[row_pad<TH>(tid, c)], R), ro, tid * 8,
+                                                  (h * NH + c * TH) * 8);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 16; ++c)
+                bstore64_aux<FHS_MODUP_STORE_AUX>(fwd_canon(lds[row_pad<TH>(tid, c)], R), ro, tid * 8,
+                                                  (h * NH + c * TH) * 8);
+        }
     }
 }
-template <int LOGN, int DP>
+template <int LOGN, int DP, bool B59>
 __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, const u64* const* uniq,
                                                                  const u64* acoef, const unsigned char* vcnt, u64* ext,
                                                                  int l, int U) {
@@ -915,7 +930,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     int t, mi;
     if (!xcd_tinner(E, dn * U, t, mi)) return;
-    modup_h_body<LOGN, DP>(T, acoef, vcnt, ext, l, t, mi, threadIdx.x, lds);
+    modup_h_body<LOGN, DP, B59>(T, acoef, vcnt, ext, l, t, mi, threadIdx.x, lds);
 }
 
 template <int LOGN>
@@ -927,12 +942,14 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
     static_assert(modup_uses_half(LOGN) || !ntt_half<LOGN>(), "the full-limb ModUp needs N <= 16384");
     if (!modup_uses_half(LOGN))   // residues + counts (launch_centered wrote no X form: modup_xform is false)
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);
+    else if (modup_xform(T, l) && T.conv_b59)   // every digit full (3 limbs), X form, 59-bit primes
+        hipLaunchKernelGGL((k_modup_h<LOGN, 3, true>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else if (modup_xform(T, l))   // every digit of this level full (3 limbs), X form (launch_centered)
-        hipLaunchKernelGGL((k_modup_h<LOGN, 3>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+        hipLaunchKernelGGL((k_modup_h<LOGN, 3, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else if (T.modup_dp == 1)
-        hipLaunchKernelGGL((k_modup_h<LOGN, 1>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+        hipLaunchKernelGGL((k_modup_h<LOGN, 1, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else
-        hipLaunchKernelGGL((k_modup_h<LOGN, 0>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+        hipLaunchKernelGGL((k_modup_h<LOGN, 0, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
 }
 
 // (b2) key inner product with the automorphism applied on the fly, lazy 128-bit over digits:
@@ -1174,7 +1191,7 @@ __device__ __forceinline__ void moddown_convert3(const u64* y, const u64* hat, i
 }
 
 // moddown_convert3 from the X form (k_special_x): x = V0 + V1 (2^60 mod q_i) + V2 (2^120 mod q_i)
-template <int LOGN>
+template <int LOGN, bool B59>
 __device__ __forceinline__ void moddown_convert3x(const u64* y, const u64* xt, const RedU& R, const u64* tw, int tid,
                                                   u64* lds, u64 hi[16]) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
@@ -1194,7 +1211,9 @@ __device__ __forceinline__ void moddown_convert3x(const u64* y, const u64* xt, c
         }
         u64 x[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = convert3x_value(v[0][k], v[1][k], v[2][k], e1, e2, 0, R.b, R.d);
+        for (int k = 0; k < 4; ++k)   // B59: upper half unfolded, as modup_convert3x
+            x[k] = B59 ? convert3x_b59(v[0][k], v[1][k], v[2][k], e1, e2, 0, R.d, k < 2)
+                       : convert3x_value(v[0][k], v[1][k], v[2][k], e1, e2, 0, R.b, R.d);
         fwd_quad_first2<TH>(x, w4, R.q, R.lazy, lds, tid, ch, hi);
     }
 }
@@ -1202,7 +1221,7 @@ __device__ __forceinline__ void moddown_convert3x(const u64* y, const u64* xt, c
 // k_moddown with half the limb in LDS (see k_modup_h): conversion of both coefficients of each
 // (e, e + N/2) pair, global NTT stage 0 in registers, then each half transformed in LDS and finished
 // ((acc - conv) P^-1 + sigma(c0)).  Same values as k_moddown.
-template <int LOGN, bool MX>
+template <int LOGN, bool MX, bool B59 = false>
 __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, const KsItem* items, const u64* acc,
                                                                    const u64* ycoef, int l, int R) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
@@ -1221,7 +1240,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     const u64 halfq = T.ks_seal ? T.md_pinv[3 * T.L0 + i] : 0;
     u64 hi[16];
     if constexpr (MX) {   // T.md_xform: y holds the special digit's X form
-        moddown_convert3x<LOGN>(y, T.modup_xt + (size_t)i * 4, RU, tw, tid, lds, hi);
+        moddown_convert3x<LOGN, B59>(y, T.modup_xt + (size_t)i * 4, RU, tw, tid, lds, hi);
     } else if (P_ == 3 && RU.cpm && !T.ks_seal) {
         moddown_convert3<LOGN>(y, T.md_hat + i, T.L0, RU, tw, tid, lds, hi);
     } else {
@@ -1434,6 +1453,10 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
         if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
             if (T.md_xform) {   // the special digit to its X form, then the two-product conversion
                 hipLaunchKernelGGL(k_special_x, dim3((T.N + 255) / 256, 2 * R), dim3(256), 0, st, T, ycoef, 2 * R);
+                if (T.conv_b59)
+                    hipLaunchKernelGGL((k_moddown_h<LOGN, true, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
+                                       it, acc, ycoef, l, R);
+                else
                 hipLaunchKernelGGL((k_moddown_h<LOGN, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc,
                                    ycoef, l, R);
             } else {

@@ -192,7 +192,7 @@ typedef unsigned __int128 u128x;
 __host__ __device__ __forceinline__ bool ge192(const u64 s[3], const u64* t) {
     return s[2] != t[2] ? s[2] > t[2] : (s[1] != t[1] ? s[1] > t[1] : s[0] >= t[0]);
 }
-// y[u] (< q_u) -> U = X + 2^179 as split-30 packed base-2^60 words, X = S - v Q_S the centred digit
+// y[u] (< q_u) -> U = X + 2^179 as base-2^60 words (V0 plain, V1 and V2 split-30 packed), X = S - v Q_S the centred digit
 // value: S = sum_u y_u Q_S/q_u < 3 Q_S, v = round(S/Q_S) (never a tie: Q_S is odd), |X| < Q_S/2 < 2^179 (primes < 2^60)
 __host__ __device__ __forceinline__ void centered_x_pack(const u64 y[3], const u64* D, u64 out[3]) {
     u128x lo = 0;   // S below 2^128
@@ -214,7 +214,7 @@ __host__ __device__ __forceinline__ void centered_x_pack(const u64 y[3], const u
     const u64 u2 = s2 + C[2] + (u64)(u01 < c01);
     const u64 u0 = (u64)u01, u1 = (u64)(u01 >> 64);
     constexpr u64 M60 = (1ull << 60) - 1;
-    out[0] = pack30(u0 & M60);
+    out[0] = u0 & M60;   // plain: the conversions add it whole (convert3x_b59) or split it (convert3x_value)
     out[1] = pack30(((u0 >> 60) | (u1 << 4)) & M60);
     out[2] = pack30((u1 >> 56) | (u2 << 8));
 }
@@ -224,11 +224,37 @@ __host__ __device__ __forceinline__ void centered_x_pack(const u64 y[3], const u
 // M < 3 p30^2 + 2^30, H < p30^2, p30 = 2^30 - 1)
 __host__ __device__ __forceinline__ u64 convert3x_value(u64 p0, u64 p1, u64 p2, uint32_t e1, Split30 e2, u64 c3,
                                                         unsigned b, unsigned d) {
-    const Split30 a = unpack30(p0), v1 = unpack30(p1), v2 = unpack30(p2);
+    const Split30 a = {(uint32_t)p0 & 0x3FFFFFFFu, (uint32_t)(p0 >> 30)}, v1 = unpack30(p1), v2 = unpack30(p2);
     const u64 L = (u64)a.lo + c3 + mul32w(v1.lo, e1) + mul32w(v2.lo, e2.lo);
     const u64 M = (u64)a.hi + mul32w(v1.hi, e1) + mul32w(v2.lo, e2.hi) + mul32w(v2.hi, e2.lo);
     const u64 H = mul32w(v2.hi, e2.hi);
     return acc3_reduce_pm(L, M, H, b, d);
+}
+
+// The same value for a 59-bit target m = 2^59 - d with d < 2^27 (DevTables::conv_b59: every prime of the
+// chain), where 2^59 == d makes every fold a 32 x 32 product and the sums stay below 2^63:
+//   L = V0 + c3 + v1.lo e1 + v2.lo e2.lo < 2^60 + 2^59 + 2^60 + 2^60,  M = v1.hi e1 + v2.lo e2.hi + v2.hi e2.lo
+//   < 2^58 + 2^59 + 2^60 (e1 = 2d < 2^28, e2 < 2^59),  H = v2.hi e2.hi < 2^59;
+//   x == L + M 2^30 + H 2^60 == A + B d,  A = L + (M mod 2^29) 2^30 < 2^62 + 2^59,  B = (M >> 29) + 2H < 2^32 + 2^60;
+//   B d = B0 d + B1 d 2^32 (B0 < 2^32, B1 < 2^29), and with B1 d = h 2^27 + r:  B1 d 2^32 == h d + r 2^32;
+//   s = A + B0 d + r 2^32 + h d < 2^62 + 3 * 2^59 + 2^55 < 2^63.
+// canon: one more fold, s mod 2^59 + (s >> 59) d < 2^59 + 2^4 d < 2m (the NTT's added inputs); otherwise s
+// itself (any 64-bit value congruent to x: the inputs the first butterfly multiplies by a twiddle).
+// About 18 instructions without the fold, against ~34 for convert3x_value with a run-time b.
+__host__ __device__ __forceinline__ u64 convert3x_b59(u64 V0, u64 p1, u64 p2, uint32_t e1, Split30 e2, u64 c3,
+                                                      uint32_t d, bool canon) {
+    const Split30 v1 = unpack30(p1), v2 = unpack30(p2);
+    const u64 L = V0 + c3 + mul32w(v1.lo, e1) + mul32w(v2.lo, e2.lo);
+    const u64 M = mul32w(v1.hi, e1) + mul32w(v2.lo, e2.hi) + mul32w(v2.hi, e2.lo);
+    const u64 H = mul32w(v2.hi, e2.hi);
+    const u64 A = L + ((M & ((1ull << 29) - 1)) << 30);
+    const u64 B = (M >> 29) + (H << 1);
+    const u64 b1d = mul32w((uint32_t)(B >> 32), d);
+    u64 sv = A + mul32w((uint32_t)B, d);
+    sv += (b1d & ((1ull << 27) - 1)) << 32;
+    sv += mul32w((uint32_t)(b1d >> 27), d);
+    if (!canon) return sv;
+    return (sv & ((1ull << 59) - 1)) + mul32w((uint32_t)(sv >> 59), d);
 }
 
 // c += L + M 2^30 + H 2^60 (< 2^123 for 8 products), then clear
@@ -353,6 +379,12 @@ __device__ __forceinline__ u64 reduce128(u64 lo, u64 hi, const RedU& R) {
 __device__ __forceinline__ u64 pm_fold64(u64 x, const RedU& R) {
     const u64 h = x >> R.b;
     return csub((x & ((1ull << R.b) - 1)) + (u64)(uint32_t)h * R.d, R.q);
+}
+// A lazy forward-NTT output (< (4 + 2 logN) q < 2^64; lazy implies q = 2^b - d on the fold, b >= 41) folded
+// once: < 2^b + 2^(64-b) 2^32 < 2^60 and congruent to x, but not canonical -- for consumers that take any
+// value below 2^60 (the key inner products' split-30 sums read ModUp's extended limbs)
+__device__ __forceinline__ u64 pm_fold_lt60(u64 x, const RedU& R) {
+    return (x & ((1ull << R.b) - 1)) + (u64)(uint32_t)(x >> R.b) * R.d;
 }
 // Canonical residue of a forward-NTT output: lazy outputs are < (4 + 2 logN) q, Harvey ones < 4q.
 __device__ __forceinline__ u64 fwd_canon(u64 x, const RedU& R) {
