@@ -291,6 +291,51 @@ def bsgs_giant_sharded(ph, ctx, baby, pts, G: int, B: int, D: int, gk, zero_pts,
     return ph.rescale_to_next(ctx, total)
 
 
+def linear_transform_sharded(ph, ctx, babies, pts, G: int, elts, gk, rescale: bool, zero_pts, dist, device="cuda",
+                             ranks=None, group=None):
+    """One fused BSGS linear transform (ph.linear_transform: the bootstrap's CoeffToSlot / SlotToCoeff
+    groups) with its giant groups split over `ranks` (global ranks of `group`): each rank sums its share
+    of the groups before ModDown (the identity group -- zero plaintexts `zero_pts` when it is another
+    rank's -- first, as the kernel expects), the partial ciphertexts are summed mod q_i on ranks[0], which
+    rescales when asked.  Every term is an exact residue: limb-identical to the one-GPU transform.  A rank
+    beyond the number of groups contributes nothing.  Returns the output on ranks[0], None elsewhere."""
+    import torch
+    me = dist.get_rank()
+    ranks = list(range(dist.get_world_size())) if ranks is None else list(ranks)
+    n_groups, idx = len(elts), ranks.index(me)
+    active = min(len(ranks), n_groups)
+    share = giant_groups(n_groups, active, idx) if idx < active else []
+    part = None
+    if share:
+        flat, es = [], [1]
+        if share[0] == 0:
+            first, rest = [0], share[1:]
+        else:
+            first, rest = [], share
+            flat.extend(zero_pts[:G])
+        for g in first + rest:
+            if g:
+                es.append(elts[g])
+            flat.extend(pts[g * G:(g + 1) * G])
+        part = ph.linear_transform(ctx, babies, flat, G, es, gk, rescale=False)
+    ci = babies[0].chain_index()
+    l = ctx.limbs(ci)
+    buf = torch.zeros(2 * l * ctx.N, dtype=torch.int64, device=device)
+    if part is not None:
+        to_buffer(ph, ctx, part, buf)
+    rows = [int(q) for q in ctx.primes[:l]] * 2
+    if dist.get_backend(group) == "gloo":
+        h = buf.cpu()
+        modular_reduce_sum(dist, h, rows, root=ranks[0], group=group)
+        buf.copy_(h)
+    else:
+        modular_reduce_sum(dist, buf, rows, root=ranks[0], group=group)
+    if me != ranks[0]:
+        return None
+    total = from_buffer(ph, ctx, buf, 2, ci, babies[0].scale() * pts[0].scale())
+    return ph.rescale_to_next(ctx, total) if rescale else total
+
+
 # ------------------------------------------------------------------ baby-step sharding (§8e(2), VERDICT r2 #7)
 def baby_steps_share(G: int, world: int, rank: int) -> list[int]:
     """Contiguous, balanced share of the baby steps 0..G-1 for `rank` (baby step 0 is the input)."""

@@ -512,6 +512,57 @@ class Bootstrapper:
         y.set_scale(y.scale() * d_prime / (self.q0 * 2.0 ** -PRESCALE_BITS))
         return y
 
+    # -- over ranks (SURVEY.md §8e Config 5): the CoeffToSlot / SlotToCoeff transforms sharded
+    def _linear_ranks(self, x, st, rescale, dist, device, ranks, group):
+        """_linear with its giant groups split over `ranks` (fhespear_dist.linear_transform_sharded): x on
+        ranks[0] (None elsewhere) is broadcast, every rank rotates the baby steps and sums its groups,
+        the partial sums meet on ranks[0].  The same limbs as _linear."""
+        import fhespear_dist as fd
+        ph, ctx = self._ph, self.ctx
+        x = fd.broadcast_ciphertext(ph, ctx, x, ranks[0], dist, device, group)
+        steps = [s for s in st.baby_steps if s % self.n]
+        rot = iter(ph.hoisting(ctx, x, self.gk, steps)) if steps else iter(())
+        babies = [x if s % self.n == 0 else next(rot) for s in st.baby_steps]
+        elts = [1 if s % self.n == 0 else pow(5, s % self.n, 2 * self.N) for s in st.giant_steps]
+        if getattr(st, "zero_pts", None) is None:   # the identity group of a rank that has another's groups
+            st.zero_pts = self.encoder.encode_complex_vector_batch(ctx, np.zeros((st.G, self.n)), st.pt_scale,
+                                                                   chain_index=st.ci)
+        return fd.linear_transform_sharded(ph, ctx, babies, st.pts, st.G, elts, self.gk, rescale, st.zero_pts, dist,
+                                           device, ranks, group)
+
+    def bootstrap_ranks(self, ctx, ct, dist, device, ranks=None, group=None):
+        """bootstrap() over the ranks of `group` (global ranks `ranks`, default all): ct on ranks[0], None
+        elsewhere; every rank calls.  The pre-scale, ModRaise, conjugation split and EvalMod run on ranks[0];
+        each CoeffToSlot / SlotToCoeff linear stage is one fused transform whose giant groups are dealt over
+        the ranks.  Returns the bootstrapped ciphertext on ranks[0] (None elsewhere), limb-identical to
+        bootstrap()."""
+        if self.ctx is None:
+            raise ValueError("ckks_bootstrapper: call setup() and keygen() first")
+        ph = self._ph
+        ranks = list(range(dist.get_world_size())) if ranks is None else list(ranks)
+        root = dist.get_rank() == ranks[0]
+        x = d_prime = None
+        if root:
+            x = self._prescale(ct)
+            d_prime = x.scale()
+            x = self._mod_raise(x)
+        for st in self.cts:
+            x = self._linear_ranks(x, st, True, dist, device, ranks, group)
+        y = None
+        if root:
+            re, im = self._split(x)
+            re, im = self._evalmod(re), self._evalmod(im)
+            y = ph.add(self.ctx, re, ph.multiply_plain(self.ctx, im,
+                                                        ph.mod_switch_to(self.ctx, self.pt_plus_i, im.chain_index())))
+        for st in self.stc:
+            if root and y.chain_index() != st.ci:
+                y = ph.mod_switch_to(self.ctx, y, st.ci)
+            y = self._linear_ranks(y, st, not st.last, dist, device, ranks, group)
+        if not root:
+            return None
+        y.set_scale(y.scale() * d_prime / (self.q0 * 2.0 ** -PRESCALE_BITS))
+        return y
+
     # -- bg:154
     def bootstrap(self, ctx, ct):
         if self.ctx is None:

@@ -25,23 +25,32 @@ def _digest(out):
     return m.group(1)
 
 
-def _one_rank():
-    if "d" not in _REF:
+# the bootstrapping chain (tf:233-298): N = 1024, L0 = 18, P = 3, level budget (2, 2); six blocks use up
+# the fresh levels, so a bootstrap runs before the sixth, its CoeffToSlot / SlotToCoeff groups over the ranks
+BOOT_ARGS = ["--N", "1024", "--L0", "18", "--P", "3", "--D", "16", "--F", "32", "--blocks", "6", "--bootstrap"]
+
+
+def _one_rank(args=None):
+    args = ARGS if args is None else args
+    key = " ".join(args)
+    if key not in _REF:
         env = dict(os.environ, FHESPEAR_DEVICE="0", FFN_DIGEST="1")
-        out = subprocess.run([sys.executable, str(REPO / "tools" / "ffn_block.py")] + ARGS, env=env,
-                             capture_output=True, text=True, timeout=120)
+        out = subprocess.run([sys.executable, str(REPO / "tools" / "ffn_block.py")] + args, env=env,
+                             capture_output=True, text=True, timeout=200)
         assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
-        _REF["d"] = _digest(out)
-    return _REF["d"]
+        _REF[key] = _digest(out)
+    return _REF[key]
 
 
-def _ranks(world, extra, port):
+def _ranks(world, extra, port, args=None):
     env = dict(os.environ, FHESPEAR_DEVICE="0", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(port), str(REPO / "tools" / "ffn_block.py"),
-           "--dist", "--backend", "gloo"] + ARGS + list(extra)
-    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=200)
+           "--dist", "--backend", "gloo"] + (ARGS if args is None else args) + list(extra)
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    if args is BOOT_ARGS:
+        assert re.search(r"bootstraps [1-9]", out.stdout), out.stdout[-2000:]
     return _digest(out)
 
 
@@ -60,3 +69,13 @@ def test_ffn_chain_over_ranks_is_limb_identical(require_gpu, world, extra):
     import zlib
     port = 29700 + 20 * world + zlib.crc32(" ".join(extra).encode()) % 20
     assert _ranks(world, extra, port) == _one_rank()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,extra", [(2, []), (4, ["--shard", "grid", "--rb", "2"])])
+def test_ffn_chain_with_bootstrap_over_ranks_is_limb_identical(require_gpu, world, extra):
+    """The chain with a bootstrap in it: the FFN chunks over the ranks as above, and the bootstrap's
+    CoeffToSlot / SlotToCoeff linear transforms with their giant groups dealt over every rank
+    (ckks_bootstrapper.bootstrap_ranks, fhespear_dist.linear_transform_sharded) -- the final ciphertext
+    limb-identical to the one-rank chain's."""
+    assert _ranks(world, extra, 29800 + 10 * world, BOOT_ARGS) == _one_rank(BOOT_ARGS)

@@ -343,15 +343,32 @@ def run_ranks(ph, a, dist, rank, world, device):
     (world 1 without --dist: the one-rank ffn_block); rank 0 prints the final ciphertext's limb digest,
     the per-block times and the decrypted error against the plaintext chain."""
     rng = np.random.default_rng(42)
-    ck = Ckks(ph, a.N, a.L0, a.P, a.D)
+    ck = Ckks(ph, a.N, a.L0, a.P, a.D, bootstrap=a.bootstrap)
     x = rng.normal(0, 0.1, a.D)
     ct = ck.encrypt_replicated(x) if rank == 0 else None
     ref = x.copy()
     fr = FfnRanks(ck, a.D, a.F, dist, rank, world, a.shard, a.rb, a.baby_mode, device) if dist is not None else None
-    times = []
+    times, boots = [], 0
     for b in range(a.blocks):
         Wk = rng.normal(0, 0.02, (a.D, a.F))
         Wv = rng.normal(0, 0.02, (a.F, a.D))
+        if a.bootstrap:   # tf:239-266: fewer than 4 levels left -> bootstrap (+ one rescale)
+            need = int(rank == 0 and (ck.L0 - 1) - ct.chain_index() < 4)
+            if dist is not None:
+                import torch
+                flag = torch.tensor([need], dtype=torch.int64, device="cpu" if dist.get_backend() == "gloo" else device)
+                dist.broadcast(flag, src=0)
+                need = int(flag.item())
+            if need:
+                boots += 1
+                if dist is None:
+                    ct = ck.ph.rescale_to_next(ck.ctx, ck.bootstrap(ct))
+                else:                          # its linear transforms' giant groups over every rank
+                    if rank == 0:
+                        while ct.coeff_modulus_size() > 2:
+                            ct = ck.ph.mod_switch_to_next(ck.ctx, ct)
+                    out = ck.bt.bootstrap_ranks(ck.ctx, ct if rank == 0 else None, dist, device)
+                    ct = ck.ph.rescale_to_next(ck.ctx, out) if rank == 0 else None
         if dist is not None:
             dist.barrier()
         ck.ctx.synchronize()
@@ -367,7 +384,7 @@ def run_ranks(ph, a, dist, rank, world, device):
             print(f"block {b}: {1e3 * times[-1]:.1f} ms chain_index={ct.chain_index()} max_err={err:.3e}", flush=True)
     if rank == 0:
         print(f"ffn world {world} shard {a.shard if dist is not None else 'none'} babies {a.baby_mode}: "
-              f"mean block {1e3 * np.mean(times):.1f} ms, ct_sha256 {ct_digest(ct)}", flush=True)
+              f"mean block {1e3 * np.mean(times):.1f} ms, bootstraps {boots}, ct_sha256 {ct_digest(ct)}", flush=True)
 
 
 def main():
@@ -408,7 +425,7 @@ def main():
         dist.destroy_process_group()
         return
     import pyPhantom as ph
-    if not a.bootstrap and a.blocks and os.environ.get("FFN_DIGEST"):   # the one-rank reference of --dist runs
+    if a.blocks and os.environ.get("FFN_DIGEST"):   # the one-rank reference of --dist runs
         run_ranks(ph, a, None, 0, 1, "cuda:0")
         return
     rng = np.random.default_rng(42)
