@@ -1315,9 +1315,11 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
                 }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const u64 v = fwd_canon(lds[row_pad<TH>(tid, c0 + k)], RU);
-                    bstore64(addmod(shoup(submod(av[k], v, q), pinv, pinv_s, q), dv[k], q), ro, tid * 8,
-                             (h * NH + (c0 + k) * TH) * 8);
+                    // B59: the NTT output folded once (< 2q) and a + 2q - v handed to the Shoup product
+                    // (any 64-bit input) -- no run-time lazy choice per element, no canonicalisation
+                    const u64 x = lds[row_pad<TH>(tid, c0 + k)];
+                    const u64 dif = B59 ? av[k] + q2 - fold59(x, RU.d) : submod(av[k], fwd_canon(x, RU), q);
+                    bstore64(addmod(shoup(dif, pinv, pinv_s, q), dv[k], q), ro, tid * 8, (h * NH + (c0 + k) * TH) * 8);
                 }
             }
         } else {
@@ -1328,8 +1330,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
                 for (int k = 0; k < 4; ++k) av[k] = bload64(rac, tid * 8, (h * NH + (c0 + k) * TH) * 8);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const u64 v = fwd_canon(lds[row_pad<TH>(tid, c0 + k)], RU);
-                    bstore64(shoup(submod(av[k], v, q), pinv, pinv_s, q), ro, tid * 8, (h * NH + (c0 + k) * TH) * 8);
+                    const u64 x = lds[row_pad<TH>(tid, c0 + k)];
+                    const u64 dif = B59 ? av[k] + q2 - fold59(x, RU.d) : submod(av[k], fwd_canon(x, RU), q);
+                    bstore64(shoup(dif, pinv, pinv_s, q), ro, tid * 8, (h * NH + (c0 + k) * TH) * 8);
                 }
             }
         }

@@ -386,6 +386,11 @@ __device__ __forceinline__ u64 pm_fold64(u64 x, const RedU& R) {
 __device__ __forceinline__ u64 pm_fold_lt60(u64 x, const RedU& R) {
     return (x & ((1ull << R.b) - 1)) + (u64)(uint32_t)(x >> R.b) * R.d;
 }
+// Any 64-bit x for a 59-bit prime q = 2^59 - d, d < 2^27 (DevTables::conv_b59): one fold to
+// < 2^59 + 2^5 d < 2q, congruent to x -- a forward-NTT output (lazy or Harvey) ready for a + 2q - x
+__device__ __forceinline__ u64 fold59(u64 x, uint32_t d) {
+    return (x & ((1ull << 59) - 1)) + mul32w((uint32_t)(x >> 59), d);
+}
 // Canonical residue of a forward-NTT output: lazy outputs are < (4 + 2 logN) q, Harvey ones < 4q.
 __device__ __forceinline__ u64 fwd_canon(u64 x, const RedU& R) {
     if (R.lazy) return pm_fold64(x, R);
