@@ -25,9 +25,10 @@ def _digest(out):
     return m.group(1)
 
 
-# the bootstrapping chain (tf:233-298): N = 1024, L0 = 18, P = 3, level budget (2, 2); six blocks use up
-# the fresh levels, so a bootstrap runs before the sixth, its CoeffToSlot / SlotToCoeff groups over the ranks
-BOOT_ARGS = ["--N", "1024", "--L0", "18", "--P", "3", "--D", "16", "--F", "32", "--blocks", "6", "--bootstrap"]
+# the bootstrapping chain (tf:233-298): N = 1024, L0 = 24, P = 3, level budget (2, 2) (bootstrap depth 16);
+# seven blocks use up the fresh levels, so a bootstrap runs before the eighth, its CoeffToSlot / SlotToCoeff
+# groups over the ranks
+BOOT_ARGS = ["--N", "1024", "--L0", "24", "--P", "3", "--D", "16", "--F", "32", "--blocks", "8", "--bootstrap"]
 
 
 def _one_rank(args=None):
