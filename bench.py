@@ -358,6 +358,9 @@ def main():
     del evs
     ktimes = ph.kernel_timer_read(ctx, reset=True)
     ph.kernel_timer_arm(ctx, [])
+    # the pinned descriptor ring's segment re-entries so far, and how many had to wait for the GPU (a wait
+    # drains the queue: the r03 host stall's candidate cause, now event-gated per segment)
+    staging = dict(zip(("segment_reentries", "reentries_that_waited"), ph.staging_stats(ctx)))
     elapsed = t1 - t0
     if dist is not None:
         import torch
@@ -502,6 +505,7 @@ def main():
             "ntt_valu_roofline": valu,
             "matvec_roofline": matvec_roof,
             "kernels": rows,
+            "staging_ring": staging,
             "parity": parity,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -2125,6 +2125,7 @@ extern "C" fhs_status fhs_decode_batch(fhs_context* c, const fhs_plaintext* cons
             aux_words += (size_t)(l - kk) * fhs::kCrtVtabWords + 1;
         }
     }
+    HostTrace ht;
     uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr;
     double* host = nullptr;
     std::vector<unsigned> hflag(count, 0);
@@ -2175,7 +2176,9 @@ extern "C" fhs_status fhs_decode_batch(fhs_context* c, const fhs_plaintext* cons
             to += (size_t)l * N;
             ao += vt.size() + 1;
         }
+        ht.mark("decode_batch: enqueue");
         if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+        ht.mark("decode_batch: gpu");
     }
     fhs_status st = e == hipSuccess ? FHS_OK : hip_fail(e, "decode_batch");
     std::vector<double> m;
@@ -2189,6 +2192,7 @@ extern "C" fhs_status fhs_decode_batch(fhs_context* c, const fhs_plaintext* cons
         st = fhs_decode(c, pts[i], full_slots.data());
         if (st == FHS_OK) std::copy(full_slots.begin(), full_slots.begin() + 2 * nslots, out);
     }
+    ht.mark("decode_batch: slots");
     if (host) hipHostFree(host);
     if (aux) dfree(c, aux, 8 * aux_words);
     if (dbl) dfree(c, dbl, 8 * N * count);
