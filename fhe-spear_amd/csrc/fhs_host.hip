@@ -346,6 +346,9 @@ struct fhs_context {
     hipEvent_t ring_ev[kRingSegs] = {};
     uint64_t ring_waits = 0, ring_blocked = 0;   // segment re-entries; of those, the ones that had to wait
     fhs::Stager stager{};
+    // pinned, grow-only: the decoder's slots (and flags) come back through it
+    double* readback = nullptr;
+    size_t readback_bytes = 0;
     // grow-only scratch buffers reused across calls (stream order makes reuse safe): a large
     // allocation costs host time per GB
     enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_ENC_PTRS, SCR_COUNT };
@@ -951,6 +954,33 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     HIPCHK(up(md_pinv.data(), 8 * md_pinv.size(), (const void**)&T.md_pinv), "tables");
     HIPCHK(up(rs.data(), 8 * rs.size(), (const void**)&T.rescale), "tables");
     HIPCHK(up(pow2.data(), 8 * pow2.size(), (const void**)&T.pow2), "tables");
+    // host encoder / decoder tables
+    c->fft_w.resize(N);
+    for (uint64_t k = 0; k < N; ++k) c->fft_w[k] = std::polar(1.0, 2.0 * M_PI * (double)k / (double)N);
+    c->dec_twist.resize(N);
+    for (uint64_t k = 0; k < N; ++k)
+        c->dec_twist[k] = {std::cos(M_PI * (double)k / (double)N), std::sin(M_PI * (double)k / (double)N)};
+    c->slot_index.resize(N / 2);
+    uint64_t e5 = 1;
+    for (uint64_t j = 0; j < N / 2; ++j) {
+        c->slot_index[j] = (e5 - 1) / 2;
+        e5 = (e5 * 5) & (2 * N - 1);
+    }
+    {   // GPU decoder tables (fhs_kernels.hip k_decode_fft): the host decoder's own values
+        const size_t H = N / 2;
+        std::vector<double> dw(2 * H), dt(2 * H);
+        std::vector<unsigned> dp(H);
+        for (size_t k = 0; k < H; ++k) {
+            dw[2 * k] = c->fft_w[2 * k].real();
+            dw[2 * k + 1] = c->fft_w[2 * k].imag();
+            dt[2 * k] = c->dec_twist[k].real();
+            dt[2 * k + 1] = c->dec_twist[k].imag();
+            dp[k] = (unsigned)(c->slot_index[k] >> 1);
+        }
+        HIPCHK(up(dw.data(), 8 * dw.size(), (const void**)&T.dec_w), "tables");
+        HIPCHK(up(dt.data(), 8 * dt.size(), (const void**)&T.dec_twist), "tables");
+        HIPCHK(up(dp.data(), 4 * dp.size(), (const void**)&T.dec_pos), "tables");
+    }
     {   // GPU encoder tables (fhs_kernels.hip k_encode)
         const size_t H = N / 2;
         const int logH = c->logN - 1;
@@ -980,18 +1010,6 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     c->tables.push_back(c->items_dev);
     HIPCHK(hipMalloc(&c->ptrs_dev, sizeof(void*) * 2 * fhs_context::kMaxPtrs), "pointer buffer");
     c->tables.push_back(c->ptrs_dev);
-    // encoder tables
-    c->fft_w.resize(N);
-    for (uint64_t k = 0; k < N; ++k) c->fft_w[k] = std::polar(1.0, 2.0 * M_PI * (double)k / (double)N);
-    c->dec_twist.resize(N);
-    for (uint64_t k = 0; k < N; ++k)
-        c->dec_twist[k] = {std::cos(M_PI * (double)k / (double)N), std::sin(M_PI * (double)k / (double)N)};
-    c->slot_index.resize(N / 2);
-    uint64_t e5 = 1;
-    for (uint64_t j = 0; j < N / 2; ++j) {
-        c->slot_index[j] = (e5 - 1) / 2;
-        e5 = (e5 * 5) & (2 * N - 1);
-    }
     {
         std::lock_guard<std::mutex> lk(g_live_mu);
         g_live.insert(c.get());
@@ -1021,6 +1039,7 @@ static void ctx_free(fhs_context* c) {
             for (void* p : kv.second) hipFree(p);
         c->free_blocks.clear();
         if (c->ring) hipHostFree(c->ring);
+        if (c->readback) hipHostFree(c->readback);
         for (hipEvent_t e : c->ring_ev)
             if (e) hipEventDestroy(e);
         for (auto& v : c->timer_pairs)
@@ -2074,130 +2093,159 @@ static void decode_slots(const fhs_context* c, const double* m, double scale, si
         re_im[2 * j + 1] = z.imag();
     }
 }
+static hipError_t readback_buf(fhs_context* c, size_t bytes, double** out) {
+    if (bytes > c->readback_bytes) {   // every earlier use ended with a stream synchronisation
+        if (c->readback) hipHostFree(c->readback);
+        c->readback = nullptr;
+        c->readback_bytes = 0;
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&c->readback), bytes, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        c->readback_bytes = bytes;
+    }
+    *out = c->readback;
+    return hipSuccess;
+}
+
+// Decode `count` plaintexts to their first `nslots` slots (out: count x nslots x (re, im)), all on the GPU:
+// per plaintext the INTT, centred CRT composition of the limbs the scale needs (+1) and the check against
+// the rest (decode_coeffs_dev's arithmetic); then one k_decode_fft + gather over all of them; only the
+// slots come back, through the pinned readback buffer, after ONE synchronisation.  A plaintext whose
+// check fails (an aliased coefficient) or that needs more limbs than the GPU composition takes is
+// composed exactly from all its limbs (decode_compose) and decoded on its own.  FHESPEAR_DECODE_HOST_FFT=1
+// runs the slot FFT on the host instead (decode_slots: the same operations, so the same doubles; A/B and
+// test knob).
+static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, int count, int nslots, double* re_im) {
+    const size_t N = c->N, n = N / 2;
+    if (!pts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > n)
+        return fail(FHS_ERR_INVALID, "decode: bad arguments");
+    if (count == 0) return FHS_OK;
+    static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;       // A/B and test knobs
+    static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;
+    static const bool host_fft = getenv("FHESPEAR_DECODE_HOST_FFT") != nullptr;
+    std::vector<int> fast(count, 0), kks(count, 0);
+    size_t tmp_words = 0, aux_words = (size_t)count;   // aux: the scales, then per fast plaintext vtab + flag
+    for (int i = 0; i < count; ++i) {
+        if (!pts[i]) return fail(FHS_ERR_INVALID, "decode: null plaintext");
+        const int l = pts[i]->l, k = full ? l : decode_limbs(c, pts[i]->scale, l);
+        kks[i] = std::min(l, k + 1);
+        fast[i] = kks[i] < l && kks[i] <= fhs::kCrtMaxL && !host_crt;
+        if (fast[i]) {
+            tmp_words += (size_t)l * N;
+            aux_words += (size_t)(l - kks[i]) * fhs::kCrtVtabWords + 1;
+        }
+    }
+    HostTrace ht;
+    const size_t per_out = host_fft ? N : 2 * (size_t)nslots;   // doubles back per plaintext
+    const size_t dbl_b = 8 * N * count, spec_b = 16 * n * count, dout_b = 16 * (size_t)nslots * count;
+    uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr, *spec = nullptr, *dout = nullptr;
+    double* rb = nullptr;
+    std::vector<fhs::CrtConsts> Ks(count);
+    hipError_t e = readback_buf(c, 8 * per_out * count + 4 * (size_t)count, &rb);
+    if (e == hipSuccess && tmp_words) e = dalloc(c, &tmp, 8 * tmp_words);
+    if (e == hipSuccess) e = dalloc(c, &dbl, dbl_b);
+    if (e == hipSuccess) e = dalloc(c, &aux, 8 * aux_words);
+    if (e == hipSuccess) e = dalloc(c, &spec, spec_b);
+    if (e == hipSuccess) e = dalloc(c, &dout, dout_b);
+    unsigned* hflag = reinterpret_cast<unsigned*>(rb + per_out * count);
+    double* dscales = reinterpret_cast<double*>(aux);
+    std::vector<double> scales(count);
+    for (int i = 0; i < count; ++i) {
+        scales[i] = pts[i]->scale;
+        hflag[i] = 0;
+    }
+    if (e == hipSuccess) e = stage_h2d(c, dscales, scales.data(), 8 * count);
+    size_t to = 0, ao = (size_t)count;
+    for (int i = 0; e == hipSuccess && i < count; ++i) {
+        if (!fast[i]) continue;
+        const fhs_plaintext* pt = pts[i];
+        const int l = pt->l, kk = kks[i], nx = l - kk;
+        crt_consts(c, kk, Ks[i]);
+        std::vector<uint64_t> vt((size_t)nx * fhs::kCrtVtabWords, 0);
+        for (int x = 0; x < nx; ++x) {
+            uint64_t* v = vt.data() + (size_t)x * fhs::kCrtVtabWords;
+            const uint64_t q = c->q[kk + x];
+            const hu128 R = (~(hu128)0) / q;
+            v[0] = q;
+            v[1] = (uint64_t)R;
+            v[2] = (uint64_t)(R >> 64);
+            const uint64_t t64 = (uint64_t)((((hu128)1) << 64) % q);
+            uint64_t pw = 1 % q;
+            for (int w = 0; w < Ks[i].W; ++w) {
+                v[3 + w] = pw;
+                pw = h_mulmod(pw, t64, q);
+            }
+        }
+        uint64_t* t = tmp + to;
+        uint64_t* a = aux + ao;
+        unsigned* flag = reinterpret_cast<unsigned*>(a + vt.size());
+        e = hipMemcpyAsync(t, pt->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
+        if (e == hipSuccess && nx > 0) e = stage_h2d(c, a, vt.data(), 8 * vt.size());
+        if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4, c->st);
+        if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, t, l, l, 1, 0, c->st);
+        if (e == hipSuccess)
+            e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
+                                        t + (size_t)kk * N, nx, a, flag);
+        if (e == hipSuccess) e = hipMemcpyAsync(&hflag[i], flag, 4, hipMemcpyDeviceToHost, c->st);
+        to += (size_t)l * N;
+        ao += vt.size() + 1;
+    }
+    // the slots of every plaintext (a slow one's are recomputed below)
+    if (e == hipSuccess && !host_fft)
+        e = fhs::launch_decode_slots(c->T, reinterpret_cast<const double*>(dbl), dscales, count,
+                                     reinterpret_cast<double*>(spec), nslots, reinterpret_cast<double*>(dout), c->st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(rb, host_fft ? (void*)dbl : (void*)dout, 8 * per_out * count, hipMemcpyDeviceToHost, c->st);
+    ht.mark("decode: enqueue");
+    if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+    ht.mark("decode: gpu");
+    fhs_status st = e == hipSuccess ? FHS_OK : hip_fail(e, "decode");
+    std::vector<double> m;
+    for (int i = 0; st == FHS_OK && i < count; ++i) {
+        if (fast[i] && hflag[i] == 0) continue;
+        st = decode_compose(c, pts[i], pts[i]->l, m);   // exact: all limbs
+        if (st != FHS_OK) break;
+        double* slot = rb + (size_t)i * per_out;
+        if (host_fft) {
+            std::copy(m.begin(), m.end(), slot);
+            continue;
+        }
+        double* di = reinterpret_cast<double*>(dbl) + (size_t)i * N;
+        e = hipMemcpyAsync(di, m.data(), 8 * N, hipMemcpyHostToDevice, c->st);
+        if (e == hipSuccess)
+            e = fhs::launch_decode_slots(c->T, di, dscales + i, 1, reinterpret_cast<double*>(spec), nslots,
+                                         reinterpret_cast<double*>(dout), c->st);
+        if (e == hipSuccess) e = hipMemcpyAsync(slot, dout, 8 * per_out, hipMemcpyDeviceToHost, c->st);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+        if (e != hipSuccess) st = hip_fail(e, "decode");
+    }
+    for (int i = 0; st == FHS_OK && i < count; ++i) {
+        double* out = re_im + (size_t)i * 2 * nslots;
+        if (host_fft)
+            decode_slots(c, rb + (size_t)i * N, pts[i]->scale, (size_t)nslots, out);
+        else
+            std::memcpy(out, rb + (size_t)i * per_out, 8 * per_out);
+    }
+    ht.mark("decode: slots");
+    if (dout) dfree(c, dout, dout_b);
+    if (spec) dfree(c, spec, spec_b);
+    if (aux) dfree(c, aux, 8 * aux_words);
+    if (dbl) dfree(c, dbl, dbl_b);
+    if (tmp) dfree(c, tmp, 8 * tmp_words);
+    return st;
+}
 extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double* re_im) {
     ENTER(c);
     if (!pt || !re_im) return fail(FHS_ERR_INVALID, "decode: null argument");
-    const size_t N = c->N;
-    const int l = pt->l;
-    static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;   // A/B and test knob
-    const int k = full ? l : decode_limbs(c, pt->scale, l), kk = std::min(l, k + 1);
-    HostTrace ht;
-    std::vector<double> m;
-    static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;   // A/B and test knob
-    bool exact = false;
-    fhs_status s = FHS_OK;
-    if (kk < l && kk <= fhs::kCrtMaxL && !host_crt) {   // kk limbs composed, checked against the other l - kk
-        s = decode_coeffs_dev(c, pt, kk, l, m, &exact);
-        if (s != FHS_OK) return s;
-    }
-    if (!exact) {   // all l limbs (the only composition when kk = l; else an aliased coefficient was caught)
-        s = decode_compose(c, pt, l, m);
-        if (s != FHS_OK) return s;
-    }
-    ht.mark("decode: intt + crt");
-    decode_slots(c, m.data(), pt->scale, N / 2, re_im);
-    ht.mark("decode: fft");
-    return FHS_OK;
+    return decode_many(c, &pt, 1, (int)(c->N / 2), re_im);
 }
-
-// Client-side batch (the client-aided block decrypts 2-3 outputs per stage): every plaintext's INTT,
-// centred CRT composition and check are enqueued together, their coefficients land in one pinned host
-// buffer, and ONE synchronisation replaces one per plaintext; then the slot FFTs, `nslots` slots each
-// (out: count x nslots x (re, im)).  Same arithmetic as fhs_decode, so the same doubles; a plaintext whose
-// check fails (an aliased coefficient) or that needs more limbs than the GPU composition takes goes
-// through fhs_decode's path on its own.
+// Client-side batch (the client-aided block decrypts 2-3 outputs per stage): decode_many over all of
+// them, one synchronisation, only the first `nslots` slots of each back to the host.
 extern "C" fhs_status fhs_decode_batch(fhs_context* c, const fhs_plaintext* const* pts, int count, int nslots,
                                        double* re_im) {
     ENTER(c);
-    const size_t N = c->N, n = N / 2;
-    if (!pts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > n)
+    if (!pts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > c->N / 2)
         return fail(FHS_ERR_INVALID, "decode_batch: bad arguments");
-    static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;
-    static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;
-    std::vector<int> fast(count, 0);
-    size_t tmp_words = 0, aux_words = 0;
-    for (int i = 0; i < count; ++i) {
-        if (!pts[i]) return fail(FHS_ERR_INVALID, "decode_batch: null plaintext");
-        const int l = pts[i]->l, k = full ? l : decode_limbs(c, pts[i]->scale, l), kk = std::min(l, k + 1);
-        fast[i] = kk < l && kk <= fhs::kCrtMaxL && !host_crt;
-        if (fast[i]) {
-            tmp_words += (size_t)l * N;
-            aux_words += (size_t)(l - kk) * fhs::kCrtVtabWords + 1;
-        }
-    }
-    HostTrace ht;
-    uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr;
-    double* host = nullptr;
-    std::vector<unsigned> hflag(count, 0);
-    std::vector<std::vector<uint64_t>> vts(count);
-    std::vector<fhs::CrtConsts> Ks(count);
-    hipError_t e = hipSuccess;
-    if (tmp_words) {
-        e = dalloc(c, &tmp, 8 * tmp_words);
-        if (e == hipSuccess) e = dalloc(c, &dbl, 8 * N * count);
-        if (e == hipSuccess) e = dalloc(c, &aux, 8 * aux_words);
-        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&host), 8 * N * count, hipHostMallocDefault);
-        size_t to = 0, ao = 0;
-        for (int i = 0; e == hipSuccess && i < count; ++i) {
-            if (!fast[i]) continue;
-            const fhs_plaintext* pt = pts[i];
-            const int l = pt->l, k = full ? l : decode_limbs(c, pt->scale, l), kk = std::min(l, k + 1), nx = l - kk;
-            crt_consts(c, kk, Ks[i]);
-            std::vector<uint64_t>& vt = vts[i];
-            vt.assign((size_t)nx * fhs::kCrtVtabWords, 0);
-            for (int x = 0; x < nx; ++x) {
-                uint64_t* v = vt.data() + (size_t)x * fhs::kCrtVtabWords;
-                const uint64_t q = c->q[kk + x];
-                const hu128 R = (~(hu128)0) / q;
-                v[0] = q;
-                v[1] = (uint64_t)R;
-                v[2] = (uint64_t)(R >> 64);
-                const uint64_t t64 = (uint64_t)((((hu128)1) << 64) % q);
-                uint64_t pw = 1 % q;
-                for (int w = 0; w < Ks[i].W; ++w) {
-                    v[3 + w] = pw;
-                    pw = h_mulmod(pw, t64, q);
-                }
-            }
-            uint64_t* t = tmp + to;
-            uint64_t* a = aux + ao;
-            unsigned* flag = reinterpret_cast<unsigned*>(a + vt.size());
-            e = hipMemcpyAsync(t, pt->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
-            if (e == hipSuccess && nx > 0) e = stage_h2d(c, a, vt.data(), 8 * vt.size());
-            if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4, c->st);
-            if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, t, l, l, 1, 0, c->st);
-            if (e == hipSuccess)
-                e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
-                                            t + (size_t)kk * N, nx, a, flag);
-            if (e == hipSuccess)
-                e = hipMemcpyAsync(host + (size_t)i * N, reinterpret_cast<double*>(dbl) + (size_t)i * N, 8 * N,
-                                   hipMemcpyDeviceToHost, c->st);
-            if (e == hipSuccess) e = hipMemcpyAsync(&hflag[i], flag, 4, hipMemcpyDeviceToHost, c->st);
-            to += (size_t)l * N;
-            ao += vt.size() + 1;
-        }
-        ht.mark("decode_batch: enqueue");
-        if (e == hipSuccess) e = hipStreamSynchronize(c->st);
-        ht.mark("decode_batch: gpu");
-    }
-    fhs_status st = e == hipSuccess ? FHS_OK : hip_fail(e, "decode_batch");
-    std::vector<double> m;
-    for (int i = 0; st == FHS_OK && i < count; ++i) {
-        double* out = re_im + (size_t)i * 2 * nslots;
-        if (fast[i] && hflag[i] == 0) {
-            decode_slots(c, host + (size_t)i * N, pts[i]->scale, (size_t)nslots, out);
-            continue;
-        }
-        std::vector<double> full_slots(2 * n);   // the single-plaintext path (exact recomposition)
-        st = fhs_decode(c, pts[i], full_slots.data());
-        if (st == FHS_OK) std::copy(full_slots.begin(), full_slots.begin() + 2 * nslots, out);
-    }
-    ht.mark("decode_batch: slots");
-    if (host) hipHostFree(host);
-    if (aux) dfree(c, aux, 8 * aux_words);
-    if (dbl) dfree(c, dbl, 8 * N * count);
-    if (tmp) dfree(c, tmp, 8 * tmp_words);
-    return st;
+    return decode_many(c, pts, count, nslots, re_im);
 }
 
 // ============================================================================ encryption

@@ -32,6 +32,9 @@ struct DevTables {
     const double* enc_w;      // [N/2][2]  omega^-k, omega = exp(2 pi i / (N/2))   (GPU encoder FFT)
     const double* enc_twist;  // [N/2][2]  (2/N) zeta^-k, zeta = exp(i pi / N)
     const unsigned* enc_pos;  // [N/2]     rev_{log N - 1}((5^j mod 2N - 1) / 4): LDS slot of z_j
+    const double* dec_w;      // [N/2][2]  omega^k (the host decoder's fft_w[2k], bit for bit)   (GPU decoder FFT)
+    const double* dec_twist;  // [N/2][2]  zeta^k (the host decoder's dec_twist)
+    const unsigned* dec_pos;  // [N/2]     (5^j mod 2N - 1) / 4: spectrum bin of slot j
     int N, logN, L0, P, K, dnum;
     // key-switch convention: 0 = exact centred ModUp, ModDown without rounding (hoistable; the
     // default); 1 = SEAL's switch_key_inplace (P = 1): per-limb lift without centring, automorphism
@@ -138,6 +141,12 @@ hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);
 hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, int trans,
                               double* out, hipStream_t st);
+// CKKS decode of `count` centred coefficient vectors (m: count x N doubles in HBM) to their first nslots
+// slots (out: count x nslots x (re, im)), slot j of vector i = FFT_{N/2}(twist (m_k + i m_{k+N/2}) / scale_i)
+// at bin dec_pos[j]; spec: count x N/2 x 2 doubles of scratch.  The host decoder's operations in its order,
+// no contraction, so the same doubles (fhs_host.hip decode_slots).  scales: device, count doubles.
+hipError_t launch_decode_slots(const DevTables& T, const double* m, const double* scales, int count, double* spec,
+                               int nslots, double* out, hipStream_t st);
 hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int count, u64* out, int l, hipStream_t st);
 hipError_t launch_key_prod(const DevTables& T, const u64* a, const u64* b, u64* out, int limbs, hipStream_t st);
 // Centred CRT composition of the first l <= kCrtMaxL limbs (coefficient form) of one polynomial into

@@ -2060,6 +2060,98 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
     }
 }
 
+// ---- decoder FFT (launch_decode_slots).  fp contraction is off throughout: the host decoder's
+// fft_inplace / decode_slots evaluate these products and sums unfused (x86-64 without FMA), and the GPU
+// must round the same way to give the same doubles.
+__device__ __forceinline__ void dec_fft_stages(double2* a, int tid, int TH, int n_pts, int log_pts, const double2* W,
+                                               int logh) {
+#pragma clang fp contract(off)
+    for (int s = 0; s < log_pts; ++s) {   // DIT, bit-reversed in, natural out (fft_inplace's stage order)
+        const int half = 1 << s;
+        for (int b = tid; b < n_pts / 2; b += TH) {
+            const int k = b & (half - 1);
+            const int i = ((b >> s) << (s + 1)) + k, j = i + half;
+            const double2 w = W[(size_t)k << (logh - 1 - s)];
+            const double2 u = a[i], v = a[j];
+            const double vr = v.x * w.x - v.y * w.y, vi = v.x * w.y + v.y * w.x;
+            a[j] = double2{u.x - vr, u.y - vi};
+            a[i] = double2{u.x + vr, u.y + vi};
+        }
+        __syncthreads();
+    }
+}
+template <int LOGN>
+constexpr int dec_threads() {
+    constexpr int PTS = LOGN > 14 ? (1 << (LOGN - 2)) : (1 << (LOGN - 1));
+    return PTS / 2 < 1024 ? PTS / 2 : 1024;
+}
+// one workgroup per vector: twist + bit-reversed scatter into LDS, the N/2-point FFT (N = 2^15: two
+// N/4-point halves, the last stage from registers), the spectrum to spec
+template <int LOGN>
+__global__ void __launch_bounds__(dec_threads<LOGN>())
+    k_decode_fft(DevTables T, const double* m, const double* scales, double2* spec) {
+#pragma clang fp contract(off)
+    constexpr int N = 1 << LOGN, H = N / 2, LOGH = LOGN - 1;
+    constexpr bool SPLIT = LOGN > 14;
+    constexpr int PTS = SPLIT ? H / 2 : H, TH = dec_threads<LOGN>();
+    __shared__ double2 a[PTS];
+    const int tid = threadIdx.x;
+    const double* src = m + (size_t)blockIdx.x * N;
+    const double scale = scales[blockIdx.x];
+    const double2* W = reinterpret_cast<const double2*>(T.dec_w);
+    const double2* Z = reinterpret_cast<const double2*>(T.dec_twist);
+    double2* out = spec + (size_t)blockIdx.x * H;
+    double2 lo[SPLIT ? PTS / TH : 1];
+    for (int h = 0; h < (SPLIT ? 2 : 1); ++h) {
+        if (h) __syncthreads();
+        for (int k = tid; k < H; k += TH) {
+            const unsigned pos = __brev((unsigned)k) >> (32 - LOGH);
+            if (SPLIT && (int)(pos / PTS) != h) continue;
+            const double x = src[k] / scale, y = src[k + H] / scale;
+            const double2 z = Z[k];
+            a[pos - h * PTS] = double2{x * z.x - y * z.y, x * z.y + y * z.x};
+        }
+        __syncthreads();
+        dec_fft_stages(a, tid, TH, PTS, SPLIT ? LOGH - 1 : LOGH, W, LOGH);
+        if constexpr (!SPLIT) {
+            for (int k = tid; k < H; k += TH) out[k] = a[k];
+        } else if (h == 0) {
+#pragma unroll
+            for (int c = 0; c < PTS / TH; ++c) lo[c] = a[tid + c * TH];
+        }
+    }
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int c = 0; c < PTS / TH; ++c) {   // last stage: pairs (k, k + N/4), twiddle omega^k
+            const int k = tid + c * TH;
+            const double2 u = lo[c], v = a[k], w = W[k];
+            const double vr = v.x * w.x - v.y * w.y, vi = v.x * w.y + v.y * w.x;
+            out[k] = double2{u.x + vr, u.y + vi};
+            out[k + PTS] = double2{u.x - vr, u.y - vi};
+        }
+    }
+}
+// slot j of vector i: spectrum bin dec_pos[j]
+__global__ void k_decode_gather(DevTables T, const double2* spec, int count, int nslots, double2* out) {
+    const size_t H = (size_t)T.N / 2, total = (size_t)count * nslots;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+        const size_t i = e / nslots, j = e - i * nslots;
+        out[e] = spec[i * H + T.dec_pos[j]];
+    }
+}
+hipError_t launch_decode_slots(const DevTables& T, const double* m, const double* scales, int count, double* spec,
+                               int nslots, double* out, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    if (nslots < 1 || nslots > T.N / 2) return hipErrorInvalidValue;
+    FHS_DISPATCH_LOGN(T.logN, {
+        hipLaunchKernelGGL((k_decode_fft<LOGN>), dim3(count), dim3(dec_threads<LOGN>()), 0, st, T, m, scales,
+                           reinterpret_cast<double2*>(spec));
+    });
+    hipLaunchKernelGGL(k_decode_gather, dim3(eltwise_grid((size_t)count * nslots)), dim3(256), 0, st, T,
+                       reinterpret_cast<const double2*>(spec), count, nslots, reinterpret_cast<double2*>(out));
+    return hipGetLastError();
+}
+
 // forward NTT of `limbs` limbs of each polynomial ptrs[blockIdx.y] (plaintext batches)
 template <int LOGN>
 __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_ptrs(DevTables T, u64* const* ptrs, int limbs) {

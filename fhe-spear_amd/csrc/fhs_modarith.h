@@ -161,35 +161,15 @@ struct Split30 {
 __device__ __forceinline__ Split30 split30(u64 x) { return Split30{(uint32_t)x & 0x3FFFFFFFu, (uint32_t)(x >> 30)}; }
 __host__ __device__ __forceinline__ u64 pack30(u64 x) { return (u64)(((uint32_t)x) & 0x3FFFFFFFu) | ((x >> 30) << 32); }
 __host__ __device__ __forceinline__ Split30 unpack30(u64 p) { return Split30{(uint32_t)p, (uint32_t)(p >> 32)}; }
-// FHS_ASM_MAC (default 1): each partial product accumulated by one v_mad_u64_u32 written as a one-instruction
-// asm statement.  Left to itself the compiler forms M's two partials separately and adds their sum (two
-// mads with a zero addend plus a v_lshl_add_u64: 5 instructions per product instead of 4), which in the
-// Hadamard and the key inner products is one VALU instruction in every seven.
-#ifndef FHS_ASM_MAC
-#define FHS_ASM_MAC 1
-#endif
-__device__ __forceinline__ u64 mad32(uint32_t a, uint32_t b, u64 c) {
-#if FHS_ASM_MAC
-    u64 r, cc;   // cc: the carry-out lane mask (unused)
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(c));
-    return r;
-#else
-    return mul32w(a, b) + c;
-#endif
-}
+// The compiler forms M's two partials separately and adds their sum (a v_lshl_add_u64 more per product);
+// forcing the chain -- one v_mad_u64_u32 per partial as inline asm, or an empty asm between M's two mads --
+// measured slower on MI355X (r04c: key inner products 1.62 -> 1.90 ms/step, Hadamard 1.93 -> 1.96-1.98;
+// the asm blocks unrolling and adds hazard nops), so the plain expression stays.
 __device__ __forceinline__ void acc3_mac(Acc3& a, Split30 x, Split30 y) {
-#if FHS_ASM_MAC == 2   // compiler mads, an empty asm between M's two partials keeps them chained
     a.L += mul32w(x.lo, y.lo);
     a.M += mul32w(x.lo, y.hi);
-    asm("" : "+v"(a.M));
     a.M += mul32w(x.hi, y.lo);
     a.H += mul32w(x.hi, y.hi);
-#else
-    a.L = mad32(x.lo, y.lo, a.L);
-    a.M = mad32(x.lo, y.hi, a.M);
-    a.M = mad32(x.hi, y.lo, a.M);
-    a.H = mad32(x.hi, y.hi, a.H);
-#endif
 }
 // (L + M 2^30 + H 2^60) mod q, result in [0, 2q), for q = 2^b - d: the split-30 sums are cut at
 // bit b (A = L + (M mod 2^(b-30)) 2^30, B = M >> (b-30) + H 2^(60-b), x == A + B d) and folded once

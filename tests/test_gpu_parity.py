@@ -673,6 +673,55 @@ def test_encryption_randomness_fresh_outside_parity_mode(require_gpu):
     assert res["parity"][2] < 1e-6 and res["fresh"][2] < 1e-6, res
 
 
+_DECODE_PROBE = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import pyPhantom as ph
+out = []
+for N in (1024, 16384, 32768):   # 32768: the split FFT (two halves in LDS, last stage from registers)
+    p = ph.params(ph.scheme_type.ckks)
+    p.set_poly_modulus_degree(N)
+    p.set_special_modulus_size(1)
+    primes = ph.create_coeff_modulus(N, [59, 59, 59, 59])
+    p.set_coeff_modulus(primes)
+    ctx = ph.context(p)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(N)
+    z = rng.normal(0, 1, N // 2) + 1j * rng.normal(0, 1, N // 2)
+    pts = [enc.encode_complex_vector(ctx, z, 2.0 ** 45), enc.encode_double_vector(ctx, z.real[:100], 2.0 ** 30, 2)]
+    qs = [int(q) for q in primes[:3]]
+    limbs = np.stack([rng.integers(0, q, N, dtype=np.uint64) for q in qs])
+    pts.append(ph.plaintext_from_numpy(ctx, limbs, 1, 2.0 ** 40))   # aliased: the all-limb composition
+    out.append(np.array(enc.decode_complex_vector(ctx, pts[0])))
+    out.append(enc.decode_batch(ctx, pts, 64).ravel())
+np.save(sys.argv[2], np.concatenate(out))
+"""
+
+
+def test_gpu_slot_fft_equals_host_fft(require_gpu, tmp_path):
+    """The decoder's slot FFT on the GPU (k_decode_fft + gather, contraction off) gives the same doubles
+    as the host FFT it replaced (FHESPEAR_DECODE_HOST_FFT=1, decode_slots): N = 1024, 16384 and 32768 (the
+    split form), single and batched decodes, and an aliased plaintext (all-limb composition path)."""
+    import os
+    import subprocess
+    import sys
+    py = str(REPO / "fhe-spear_amd" / "python")
+    got = {}
+    for mode in ("gpu", "host"):
+        env = dict(os.environ)
+        env.pop("FHESPEAR_DECODE_HOST_FFT", None)
+        if mode == "host":
+            env["FHESPEAR_DECODE_HOST_FFT"] = "1"
+        f = tmp_path / f"{mode}.npy"
+        r = subprocess.run([sys.executable, "-c", _DECODE_PROBE, py, str(f)], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got[mode] = np.load(f)
+    assert got["gpu"].shape == got["host"].shape
+    assert np.array_equal(got["gpu"].view(np.uint64), got["host"].view(np.uint64))
+
+
 def test_decode_batch_equals_single_decodes(ph):
     """fhs_decode_batch (the client's decrypt_vec of a block stage in one synchronisation) returns the
     same doubles as fhs_decode one plaintext at a time: real and complex encodings at two levels, and a
