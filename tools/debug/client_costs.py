@@ -2,7 +2,7 @@
 each client call of one cfg3 block stage timed alone (synchronised, median of 7), batched as
 client_aided_block issues them, plus the host-side marks of one batched decode (FHESPEAR_HOST_TRACE).
 
-    FHESPEAR_HOST_TRACE=1 python tools/debug/client_costs.py
+    python tools/debug/client_costs.py
 """
 import os
 import sys
@@ -60,9 +60,10 @@ def main():
     x_ln, mixes = t("numpy _mix", lambda: rb._mix(blk, x, st[1]))
     t("numpy _wkv", lambda: rb._wkv(blk, mixes, xs[0], xs[1], xs[2], st[3], st[4]))
     t("numpy layer_norm", lambda: rb.layer_norm(x, blk.ln2_w, blk.ln2_b))
-    if os.environ.get("FHESPEAR_HOST_TRACE"):
-        print("one decode_batch(3) with host marks:", flush=True)
-        srv.encoder.decode_batch(srv.ctx, pts, D)
+    print("one decrypt_vecs(3) with host marks:", flush=True)
+    os.environ["FHESPEAR_HOST_TRACE"] = "1"   # read per call by the library's HostTrace
+    srv.decrypt_vecs(outs, D)
+    os.environ.pop("FHESPEAR_HOST_TRACE")
 
 
 if __name__ == "__main__":
