@@ -1653,9 +1653,9 @@ static fhs_status encode_many(fhs_context* c, const double* vals, size_t count, 
         const size_t cnt = std::min(chunk, count - base);
         uint64_t* dvals = nullptr;
         HIPCHK(dalloc(c, &dvals, std::max<size_t>(8, 8 * cnt * stride)), "encode staging");
-        if (stride) {
-            hipError_t e = hipMemcpyAsync(dvals, vals + base * stride, 8 * cnt * stride, hipMemcpyHostToDevice, c->st);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+        if (stride) {   // stage_h2d: through the pinned ring, no host wait, when it fits a segment (a client
+                        // batch of a few vectors), else a copy + synchronisation
+            hipError_t e = stage_h2d(c, dvals, vals + base * stride, 8 * cnt * stride);
             if (e != hipSuccess) { dfree(c, dvals, 8 * cnt * stride); return hip_fail(e, "encode upload"); }
         }
         ht.mark("encode: upload");
@@ -2123,7 +2123,7 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;
     static const bool host_fft = getenv("FHESPEAR_DECODE_HOST_FFT") != nullptr;
     std::vector<int> fast(count, 0), kks(count, 0);
-    size_t tmp_words = 0, aux_words = (size_t)count;   // aux: the scales, then per fast plaintext vtab + flag
+    size_t tmp_words = 0, vt_words = 0;
     for (int i = 0; i < count; ++i) {
         if (!pts[i]) return fail(FHS_ERR_INVALID, "decode: null plaintext");
         const int l = pts[i]->l, k = full ? l : decode_limbs(c, pts[i]->scale, l);
@@ -2131,9 +2131,11 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
         fast[i] = kks[i] < l && kks[i] <= fhs::kCrtMaxL && !host_crt;
         if (fast[i]) {
             tmp_words += (size_t)l * N;
-            aux_words += (size_t)(l - kks[i]) * fhs::kCrtVtabWords + 1;
+            vt_words += (size_t)(l - kks[i]) * fhs::kCrtVtabWords;
         }
     }
+    // aux: the scales (count doubles), every fast plaintext's vtab, then the count check flags
+    const size_t aux_words = (size_t)count + vt_words + ((size_t)count + 1) / 2;
     HostTrace ht;
     const size_t per_out = host_fft ? N : 2 * (size_t)nslots;   // doubles back per plaintext
     const size_t dbl_b = 8 * N * count, spec_b = 16 * n * count, dout_b = 16 * (size_t)nslots * count;
@@ -2148,21 +2150,21 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     if (e == hipSuccess) e = dalloc(c, &dout, dout_b);
     unsigned* hflag = reinterpret_cast<unsigned*>(rb + per_out * count);
     double* dscales = reinterpret_cast<double*>(aux);
-    std::vector<double> scales(count);
+    unsigned* dflag = reinterpret_cast<unsigned*>(aux + count + vt_words);
+    std::vector<uint64_t> head((size_t)count + vt_words, 0);   // scales and vtabs: one staged copy
     for (int i = 0; i < count; ++i) {
-        scales[i] = pts[i]->scale;
+        std::memcpy(&head[i], &pts[i]->scale, 8);
         hflag[i] = 0;
     }
-    if (e == hipSuccess) e = stage_h2d(c, dscales, scales.data(), 8 * count);
-    size_t to = 0, ao = (size_t)count;
-    for (int i = 0; e == hipSuccess && i < count; ++i) {
+    size_t vo = (size_t)count;
+    std::vector<size_t> vt_at(count, 0);
+    for (int i = 0; i < count; ++i) {
         if (!fast[i]) continue;
-        const fhs_plaintext* pt = pts[i];
-        const int l = pt->l, kk = kks[i], nx = l - kk;
+        const int kk = kks[i], nx = pts[i]->l - kk;
         crt_consts(c, kk, Ks[i]);
-        std::vector<uint64_t> vt((size_t)nx * fhs::kCrtVtabWords, 0);
-        for (int x = 0; x < nx; ++x) {
-            uint64_t* v = vt.data() + (size_t)x * fhs::kCrtVtabWords;
+        vt_at[i] = vo;
+        for (int x = 0; x < nx; ++x, vo += fhs::kCrtVtabWords) {
+            uint64_t* v = head.data() + vo;
             const uint64_t q = c->q[kk + x];
             const hu128 R = (~(hu128)0) / q;
             v[0] = q;
@@ -2175,20 +2177,23 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
                 pw = h_mulmod(pw, t64, q);
             }
         }
+    }
+    if (e == hipSuccess) e = stage_h2d(c, aux, head.data(), 8 * head.size());
+    if (e == hipSuccess) e = hipMemsetAsync(dflag, 0, 4 * (size_t)count, c->st);
+    size_t to = 0;
+    for (int i = 0; e == hipSuccess && i < count; ++i) {
+        if (!fast[i]) continue;
+        const fhs_plaintext* pt = pts[i];
+        const int l = pt->l, kk = kks[i], nx = l - kk;
         uint64_t* t = tmp + to;
-        uint64_t* a = aux + ao;
-        unsigned* flag = reinterpret_cast<unsigned*>(a + vt.size());
         e = hipMemcpyAsync(t, pt->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
-        if (e == hipSuccess && nx > 0) e = stage_h2d(c, a, vt.data(), 8 * vt.size());
-        if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4, c->st);
         if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, t, l, l, 1, 0, c->st);
         if (e == hipSuccess)
             e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
-                                        t + (size_t)kk * N, nx, a, flag);
-        if (e == hipSuccess) e = hipMemcpyAsync(&hflag[i], flag, 4, hipMemcpyDeviceToHost, c->st);
+                                        t + (size_t)kk * N, nx, aux + vt_at[i], dflag + i);
         to += (size_t)l * N;
-        ao += vt.size() + 1;
     }
+    if (e == hipSuccess) e = hipMemcpyAsync(hflag, dflag, 4 * (size_t)count, hipMemcpyDeviceToHost, c->st);
     // the slots of every plaintext (a slow one's are recomputed below)
     if (e == hipSuccess && !host_fft)
         e = fhs::launch_decode_slots(c->T, reinterpret_cast<const double*>(dbl), dscales, count,

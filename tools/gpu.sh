@@ -14,6 +14,7 @@
 #   rehearse=N[:bench args] N ranks sharing this one GPU (gloo, host-staged exchange; timings
 #                           meaningless): bench.py --gpus N self-launches them -> OUT/rehearse_nN.json
 #   py=SCRIPT[:args]        python SCRIPT args                                  -> OUT/py_<name>.log
+#   ptrace=SCRIPT[:args]    the same under rocprofv3 --kernel-trace --stats      -> OUT/ptrace_<name>/
 set -o pipefail
 OUT=gpurun_out/$1
 shift
@@ -72,6 +73,13 @@ for step in "$@"; do
             > "$OUT/rehearse_n$n.log" 2>&1 || fail "rehearse $n" "$OUT/rehearse_n$n.log"
         grep '^{' "$OUT/rehearse_n$n.log" | tail -1 > "$OUT/rehearse_n$n.json"
         python3 tools/show_bench.py "$OUT/rehearse_n$n.json" ;;
+    ptrace)
+        s=${arg%%:*}
+        a=""
+        [ "$s" != "$arg" ] && a=${arg#*:}
+        b=$(basename "$s" .py)
+        timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/ptrace_$b" -o run --output-format csv \
+            -- python3 -u "$s" $a > "$OUT/ptrace_$b.log" 2>&1 || fail "ptrace $s" "$OUT/ptrace_$b.log" ;;
     py)
         s=${arg%%:*}
         a=""
