@@ -1486,26 +1486,30 @@ extern "C" fhs_status fhs_plaintext_destroy(fhs_plaintext* pt) {
 // Output array of a batch creator: cleared on entry; if the call fails part-way (e.g. device OOM,
 // which bg:1164-1170 catches to fall back to on-the-fly encoding) the plaintexts already created
 // are destroyed and their slots reset to null, so a failed batch leaves no HBM behind.
-struct BatchOut {
-    fhs_plaintext** outs;
+static void destroy_obj(fhs_plaintext* p) { fhs_plaintext_destroy(p); }
+static void destroy_obj(fhs_ciphertext* p) { fhs_ciphertext_destroy(p); }
+template <class Obj>
+struct BatchOutT {
+    Obj** outs;
     size_t n;
     bool kept = false;
-    BatchOut(fhs_plaintext** o, size_t count) : outs(o), n(o ? count : 0) {
+    BatchOutT(Obj** o, size_t count) : outs(o), n(o ? count : 0) {
         for (size_t i = 0; i < n; ++i) outs[i] = nullptr;
     }
     fhs_status keep(fhs_status st) {
         kept = st == FHS_OK;
         return st;
     }
-    ~BatchOut() {
+    ~BatchOutT() {
         if (kept) return;
         for (size_t i = 0; i < n; ++i)
             if (outs[i]) {
-                fhs_plaintext_destroy(outs[i]);
+                destroy_obj(outs[i]);
                 outs[i] = nullptr;
             }
     }
 };
+using BatchOut = BatchOutT<fhs_plaintext>;
 extern "C" fhs_status fhs_ciphertext_info(const fhs_ciphertext* ct, int* ncomp, int* ci, int* l, double* scale) {
     if (!ct) return fail(FHS_ERR_INVALID, "null ciphertext");
     if (ncomp) *ncomp = ct->ncomp;
@@ -2180,17 +2184,32 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     }
     if (e == hipSuccess) e = stage_h2d(c, aux, head.data(), 8 * head.size());
     if (e == hipSuccess) e = hipMemsetAsync(dflag, 0, 4 * (size_t)count, c->st);
+    // coefficient form: the fast plaintexts copied side by side; one INTT launch over all of them when
+    // they share a level (the usual client batch), else one per plaintext
+    int lf = -1, nf = 0;
+    bool one_l = true;
+    for (int i = 0; i < count; ++i) {
+        if (!fast[i]) continue;
+        one_l &= lf < 0 || pts[i]->l == lf;
+        lf = pts[i]->l;
+        ++nf;
+    }
     size_t to = 0;
     for (int i = 0; e == hipSuccess && i < count; ++i) {
         if (!fast[i]) continue;
-        const fhs_plaintext* pt = pts[i];
-        const int l = pt->l, kk = kks[i], nx = l - kk;
+        const int l = pts[i]->l;
+        e = hipMemcpyAsync(tmp + to, pts[i]->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
+        if (e == hipSuccess && !one_l) e = fhs::launch_ntt_inv(c->T, tmp + to, l, l, 1, 0, c->st);
+        to += (size_t)l * N;
+    }
+    if (e == hipSuccess && nf > 0 && one_l) e = fhs::launch_ntt_inv(c->T, tmp, lf, lf, nf, (size_t)lf * N, c->st);
+    to = 0;
+    for (int i = 0; e == hipSuccess && i < count; ++i) {
+        if (!fast[i]) continue;
+        const int l = pts[i]->l, kk = kks[i], nx = l - kk;
         uint64_t* t = tmp + to;
-        e = hipMemcpyAsync(t, pt->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
-        if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, t, l, l, 1, 0, c->st);
-        if (e == hipSuccess)
-            e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
-                                        t + (size_t)kk * N, nx, aux + vt_at[i], dflag + i);
+        e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
+                                    t + (size_t)kk * N, nx, aux + vt_at[i], dflag + i);
         to += (size_t)l * N;
     }
     if (e == hipSuccess) e = hipMemcpyAsync(hflag, dflag, 4 * (size_t)count, hipMemcpyDeviceToHost, c->st);
@@ -2273,6 +2292,52 @@ extern "C" fhs_status fhs_encrypt_symmetric(fhs_context* c, fhs_secret_key* sk, 
     dfree(c, eb, 8 * S);
     *out = ct;
     return FHS_OK;
+}
+extern "C" fhs_status fhs_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key* sk, const fhs_plaintext* const* pts,
+                                                  int count, fhs_ciphertext** outs) {
+    ENTER(c);
+    if (!sk || !pts || !outs || count < 0) return fail(FHS_ERR_INVALID, "encrypt_batch: bad arguments");
+    for (int i = 0; i < count; ++i)
+        if (!pts[i]) return fail(FHS_ERR_INVALID, "encrypt_batch: null plaintext");
+    bool same = count > 0;
+    for (int i = 1; i < count; ++i) same &= pts[i]->l == pts[0]->l;
+    if (!same) {   // mixed levels: one at a time (the same counters in the same order)
+        for (int i = 0; i < count; ++i) {
+            const fhs_status s = fhs_encrypt_symmetric(c, sk, pts[i], &outs[i]);
+            if (s != FHS_OK) return s;
+        }
+        return FHS_OK;
+    }
+    BatchOutT<fhs_ciphertext> bo(outs, count);
+    const int l = pts[0]->l;
+    const size_t S = (size_t)l * c->N;
+    std::vector<uint64_t*> c1(count);
+    for (int i = 0; i < count; ++i) {
+        fhs_ciphertext* ct;
+        fhs_status s = new_ct(c, 2, pts[i]->ci, pts[i]->scale, &ct);
+        if (s != FHS_OK) return s;
+        outs[i] = ct;
+        c1[i] = ct->d + S;
+    }
+    const uint64_t ctr0 = sk->ctr;
+    sk->ctr += (uint64_t)count;
+    const uint64_t step = stream_id(0, 1, 0);   // consecutive counters: stream ids 2^16 apart
+    uint64_t *eb = nullptr, *dptrs = nullptr;
+    HIPCHK(dalloc(c, &eb, 8 * S * count), "encrypt");
+    hipError_t e = dalloc(c, &dptrs, 8 * (size_t)count);
+    if (e == hipSuccess) e = stage_h2d(c, dptrs, c1.data(), 8 * (size_t)count);
+    if (e == hipSuccess)
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, sk->key, stream_id(ST_ENC_SYM, ctr0, 0), nullptr, l, c->st,
+                               count, step, reinterpret_cast<fhs::u64* const*>(dptrs));
+    if (e == hipSuccess)
+        e = fhs::launch_sample(c->T, fhs::SAMPLE_CBD, sk->key, stream_id(ST_ENC_SYM, ctr0, 1), eb, l, c->st, count, step);
+    if (e == hipSuccess) e = fhs::launch_ntt_fwd(c->T, eb, l, l, count, S, c->st);
+    for (int i = 0; e == hipSuccess && i < count; ++i)
+        e = fhs::launch_encrypt_combine(c->T, 0, outs[i]->d, c1[i], sk->s, nullptr, nullptr, eb + (size_t)i * S, nullptr,
+                                        pts[i]->d, l, c->st);
+    if (dptrs) dfree(c, dptrs, 8 * (size_t)count);
+    dfree(c, eb, 8 * S * count);
+    return bo.keep(e == hipSuccess ? FHS_OK : hip_fail(e, "encrypt"));
 }
 extern "C" fhs_status fhs_encrypt_asymmetric(fhs_context* c, fhs_public_key* pk, const fhs_plaintext* pt,
                                              fhs_ciphertext** out) {

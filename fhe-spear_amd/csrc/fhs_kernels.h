@@ -131,7 +131,10 @@ hipError_t launch_encode(const DevTables& T, const double* vals, int count, size
 // SAMPLE_UNIFORM / TERNARY / CBD draw from the ChaCha20 PRF stream (K, sid); SAMPLE_SEEDED expands
 // the public seed `sid` (switching-key a_j); SAMPLE_TESTDATA is the non-secret SplitMix64 uniform of
 // random_plaintexts (K unused)
-hipError_t launch_sample(const DevTables& T, int mode, const ::PrfKey& K, u64 sid, u64* out, int l, hipStream_t st);
+// A batch of npoly polynomials: polynomial y draws stream sid + y sid_step into outs_dev[y] (device
+// pointer array), or out + y l N when outs_dev is null -- the same values as npoly single calls.
+hipError_t launch_sample(const DevTables& T, int mode, const ::PrfKey& K, u64 sid, u64* out, int l, hipStream_t st,
+                         int npoly = 1, u64 sid_step = 0, u64* const* outs_dev = nullptr);
 // b_j = e - a_j s + [limb in digit j] (P mod q) s_new  (switching-key component 0 of digit j)
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* b_out, const u64* a, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st);

@@ -1829,9 +1829,12 @@ __device__ __forceinline__ u64 rnd_testdata(u64 key, u64 ctr) { return sm64(key 
 // SAMPLE_TERNARY / SAMPLE_CBD: one small value per coefficient (block n), replicated over the limbs
 // in coefficient form (the caller runs the forward NTT); SAMPLE_SEEDED: public a_j expansion of the
 // seed `sid`; SAMPLE_TESTDATA: SplitMix64 uniform (random_plaintexts, not secret)
-__global__ void k_sample(DevTables T, int mode, PrfKey K, u64 sid, u64* out, int l) {
+// Polynomial blockIdx.y of a batch: stream sid + y sid_step, written to outs[y] (outs null: out + y l N).
+__global__ void k_sample(DevTables T, int mode, PrfKey K, u64 sid, u64* out, int l, u64 sid_step, u64* const* outs) {
     const int N = T.N;
     const size_t S = (size_t)l * N;
+    sid += blockIdx.y * sid_step;
+    out = outs ? outs[blockIdx.y] : out + blockIdx.y * S;
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
         const int i = (int)(idx / N), n = (int)(idx % N);
         const PrimeK& P = PK(T, i);
@@ -1860,8 +1863,11 @@ __global__ void k_sample(DevTables T, int mode, PrfKey K, u64 sid, u64* out, int
         out[idx] = v;
     }
 }
-hipError_t launch_sample(const DevTables& T, int mode, const PrfKey& K, u64 sid, u64* out, int l, hipStream_t st) {
-    hipLaunchKernelGGL(k_sample, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, mode, K, sid, out, l);
+hipError_t launch_sample(const DevTables& T, int mode, const PrfKey& K, u64 sid, u64* out, int l, hipStream_t st,
+                         int npoly, u64 sid_step, u64* const* outs_dev) {
+    if (npoly < 1) return hipSuccess;
+    const int g1 = eltwise_grid((size_t)l * T.N) / npoly, gx = g1 > 0 ? g1 : 1;
+    hipLaunchKernelGGL(k_sample, dim3(gx, npoly), dim3(256), 0, st, T, mode, K, sid, out, l, sid_step, outs_dev);
     return hipGetLastError();
 }
 
@@ -2236,6 +2242,7 @@ hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int coun
 }
 
 // ============================================================================ decode: centred CRT
+constexpr int kCrtCheckPer = 4;   // extra limbs checked per grid row
 __global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double* __restrict__ out, int N,
                               const u64* __restrict__ extra, int nx, const u64* __restrict__ vtab, unsigned* flag) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2290,12 +2297,18 @@ __global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double
             br = nb;
         }
     }
-    double v = 0;   // v 2^64 is exact, so one rounding per step as on the host
-    for (int w = W - 1; w >= 0; --w) v = __dadd_rn(__dmul_rn(v, 18446744073709551616.0), (double)x[w]);
-    out[n] = neg ? -v : v;
-    // the composition is the true coefficient only if it also matches every limb not composed
+    if (blockIdx.y == 0) {
+        double v = 0;   // v 2^64 is exact, so one rounding per step as on the host
+        for (int w = W - 1; w >= 0; --w) v = __dadd_rn(__dmul_rn(v, 18446744073709551616.0), (double)x[w]);
+        out[n] = neg ? -v : v;
+    }
+    // the composition is the true coefficient only if it also matches every limb not composed: row y of
+    // the grid checks limbs [y kCrtCheckPer, (y + 1) kCrtCheckPer) (the composition above is a few
+    // multiply-adds per limb; the check is the long part, serial in one thread it left the kernel
+    // latency-bound at N / 256 workgroups)
     bool bad = false;
-    for (int e = 0; e < nx; ++e) {
+    const int e1 = min(nx, (int)(blockIdx.y + 1) * kCrtCheckPer);
+    for (int e = blockIdx.y * kCrtCheckPer; e < e1; ++e) {
         const u64* vt = vtab + (size_t)e * kCrtVtabWords;
         const u64 q = vt[0];
         u64 lo = 0, hi = 0;   // sum_w x[w] (2^64w mod q) < W 2^123: no overflow
@@ -2314,7 +2327,9 @@ hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out,
                               int nx, const u64* vtab, unsigned* flag) {
     if (K.l < 1 || K.l > kCrtMaxL || K.W != K.l + 1) return hipErrorInvalidValue;
     if (nx > 0 && (!extra || !vtab || !flag)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_crt_compose, dim3((N + 255) / 256), dim3(256), 0, st, K, limbs, out, N, extra, nx, vtab, flag);
+    const int rows = nx > 0 ? (nx + kCrtCheckPer - 1) / kCrtCheckPer : 1;
+    hipLaunchKernelGGL(k_crt_compose, dim3((N + 255) / 256, rows), dim3(256), 0, st, K, limbs, out, N, extra, nx, vtab,
+                       flag);
     return hipGetLastError();
 }
 

@@ -126,6 +126,7 @@ _SIGS = {
     "fhs_decode": (C.c_int, [_vp, _vp, _dblp]),
     "fhs_decode_batch": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _dblp]),
     "fhs_encrypt_symmetric": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
+    "fhs_encrypt_symmetric_batch": (C.c_int, [_vp, _vp, _vp, C.c_int, _vp]),
     "fhs_encrypt_asymmetric": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_decrypt": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_add": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
@@ -586,6 +587,17 @@ class secret_key:
 
     def encrypt_symmetric(self, ctx, pt):
         return _ct(ctx, _lib.fhs_encrypt_symmetric, self._h, pt._h, what="encrypt_symmetric")
+
+    def encrypt_symmetric_batch(self, ctx, pts):
+        """fhs_encrypt_symmetric_batch: the same ciphertexts as encrypt_symmetric over `pts` in order, with
+        the samplers and NTTs run once over the batch."""
+        n = len(pts)
+        if n == 0:
+            return []
+        ins = (_vp * n)(*[p._h for p in pts])
+        outs = (_vp * n)()
+        _check(_lib.fhs_encrypt_symmetric_batch(ctx._h, self._h, ins, n, outs), "encrypt_symmetric_batch")
+        return [ciphertext(ctx, _vp(outs[i])) for i in range(n)]
 
     def decrypt(self, ctx, ct):
         return _pt(ctx, _lib.fhs_decrypt, self._h, ct._h, what="decrypt")

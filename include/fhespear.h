@@ -144,6 +144,11 @@ fhs_status fhs_decode_batch(fhs_context* ctx, const fhs_plaintext* const* pts, i
 
 /* ---- encryption (pb:105-116) ---- */
 fhs_status fhs_encrypt_symmetric(fhs_context* ctx, fhs_secret_key* sk, const fhs_plaintext* pt, fhs_ciphertext** out);
+/* `count` symmetric encryptions in one pass (the client's inputs of a block stage, bg:784-892): the same
+ * ciphertexts as `count` fhs_encrypt_symmetric calls in order (each takes the key's next encryption
+ * counter); the samplers and NTTs run once over the whole batch */
+fhs_status fhs_encrypt_symmetric_batch(fhs_context* ctx, fhs_secret_key* sk, const fhs_plaintext* const* pts, int count,
+                                       fhs_ciphertext** out_array);
 fhs_status fhs_encrypt_asymmetric(fhs_context* ctx, fhs_public_key* pk, const fhs_plaintext* pt, fhs_ciphertext** out);
 fhs_status fhs_decrypt(fhs_context* ctx, fhs_secret_key* sk, const fhs_ciphertext* ct, fhs_plaintext** out);
 

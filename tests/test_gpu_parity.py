@@ -722,6 +722,28 @@ def test_gpu_slot_fft_equals_host_fft(require_gpu, tmp_path):
     assert np.array_equal(got["gpu"].view(np.uint64), got["host"].view(np.uint64))
 
 
+def test_encrypt_symmetric_batch_equals_single_encryptions(ph):
+    """fhs_encrypt_symmetric_batch (the client's stage inputs in one pass: one sampler launch per
+    distribution and one NTT over the batch) gives limb for limb the ciphertexts of encrypt_symmetric
+    called in order with a key made from the same seed, and keeps the key's counter in step; a batch of
+    mixed levels goes one at a time."""
+    N, L0, P = 2048, 6, 2
+    ctx, _, _ = make_ctx(ph, N, L0, P, seed=41)
+    a, b = ph.secret_key(ctx, seed=42), ph.secret_key(ctx, seed=42)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(43)
+    pts = enc.encode_double_vector_batch(ctx, rng.normal(0, 1, (3, N // 2)), 2.0 ** 40)
+    for batch in (pts, [pts[0], enc.encode_double_vector(ctx, rng.normal(0, 1, 8), 2.0 ** 40, 2), pts[2]], pts[:1]):
+        want = [a.encrypt_symmetric(ctx, p) for p in batch]
+        got = b.encrypt_symmetric_batch(ctx, batch)
+        assert len(got) == len(want)
+        for g, w in zip(got, want):
+            assert np.array_equal(g.to_numpy(), w.to_numpy())
+    # counters in step afterwards
+    assert np.array_equal(a.encrypt_symmetric(ctx, pts[1]).to_numpy(), b.encrypt_symmetric(ctx, pts[1]).to_numpy())
+    assert b.encrypt_symmetric_batch(ctx, []) == []
+
+
 def test_decode_batch_equals_single_decodes(ph):
     """fhs_decode_batch (the client's decrypt_vec of a block stage in one synchronisation) returns the
     same doubles as fhs_decode one plaintext at a time: real and complex encodings at two levels, and a

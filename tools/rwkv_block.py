@@ -183,7 +183,7 @@ class Server:
         reps = -(-self.slots // len(xs[0]))
         rows = np.stack([np.tile(np.asarray(x), reps)[:self.slots] for x in xs])
         enc = self.encoder.encode_complex_vector_batch if cplx else self.encoder.encode_double_vector_batch
-        return [self.sk.encrypt_symmetric(self.ctx, pt) for pt in enc(self.ctx, rows, self.scale)]
+        return self.sk.encrypt_symmetric_batch(self.ctx, enc(self.ctx, rows, self.scale))
 
     def decrypt_vecs(self, cts, n):
         """complex slots [len(cts), n] (real parts for real-packed outputs)"""
