@@ -35,6 +35,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_MODDOWN_HALF 1     // k_moddown_h: half-limb LDS
 #define FHS_INTT_HALF 1        // k_ks_intt_h: half-limb LDS inverse NTT
 #ifndef FHS_MODUPH_CH
+#ifndef FHS_MODUP_QUADPAIR
+#define FHS_MODUP_QUADPAIR 1   // k_modup_h block decode: 1 = xcd_quadpair (inputs read by 4 XCDs), 0 = xcd_tinner
+#endif
 #define FHS_MODUPH_CH 2        // k_modup_h: coefficient pairs per conversion chunk
 #endif
 #define FHS_MODUPH_RL 3        // k_modup_h: radix (log2) of the NTT register passes
@@ -82,6 +85,18 @@ __device__ __forceinline__ bool xcd_mmajor(int E, int M, int& t, int& m) {
     if (nm <= 0 || k >= nm * E) return false;
     m = x + 8 * (k / E);
     t = k % E;
+    return true;
+}
+// quad-pair: XCD x takes the limbs t == x (mod 4) of the inputs m == x / 4 (mod 2) -- ~E/4 primes' twiddle
+// tables per XCD L2 (2.5 MiB at E = 39) and each input read by 4 XCDs instead of all 8 (t-inner as
+// xcd_tinner).  Grid = 8 * ceil(E/4) * ceil(M/2).
+__host__ __device__ __forceinline__ int xcd_grid_q(int E, int M) { return 8 * ((E + 3) / 4) * ((M + 1) / 2); }
+__device__ __forceinline__ bool xcd_quadpair(int E, int M, int& t, int& m) {
+    const int b = blockIdx.x, x = b & 7, k = b >> 3, pg = x & 3, mh = x >> 2;
+    const int nx = (E - pg + 3) >> 2, nm = (M - mh + 1) >> 1;
+    if (nx <= 0 || nm <= 0 || k >= nx * nm) return false;
+    t = pg + 4 * (k % nx);
+    m = mh + 2 * (k / nx);
     return true;
 }
 __host__ __device__ __forceinline__ int xcd_grid_m(int E, int M) { return 8 * ((M + 7) / 8) * E; }
@@ -929,7 +944,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_modup_h(DevTables T, co
     __shared__ __attribute__((aligned(16))) u64 lds[modup_h_lds_words<LOGN>()];
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     int t, mi;
-    if (!xcd_tinner(E, dn * U, t, mi)) return;
+    if (!(FHS_MODUP_QUADPAIR ? xcd_quadpair(E, dn * U, t, mi) : xcd_tinner(E, dn * U, t, mi))) return;
     modup_h_body<LOGN, DP, B59>(T, acoef, vcnt, ext, l, t, mi, threadIdx.x, lds);
 }
 
@@ -938,7 +953,7 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
                          u64* ext, int l, int U, hipStream_t st) {
     const int E = l + T.P, dn = (l + T.P - 1) / T.P;
     const int mgrid = xcd_grid(E, dn * U);
-    const dim3 g(mgrid), b((1 << LOGN) / 32);
+    const dim3 g(FHS_MODUP_QUADPAIR ? xcd_grid_q(E, dn * U) : mgrid), b((1 << LOGN) / 32);
     static_assert(modup_uses_half(LOGN) || !ntt_half<LOGN>(), "the full-limb ModUp needs N <= 16384");
     if (!modup_uses_half(LOGN))   // residues + counts (launch_centered wrote no X form: modup_xform is false)
         hipLaunchKernelGGL((k_modup<LOGN>), dim3(mgrid), dim3((1 << LOGN) / 16), 0, st, T, uniq, acoef, vcnt, ext, l, U);

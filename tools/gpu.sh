@@ -6,7 +6,7 @@
 #   smoke                   __graft_entry__.smoke()                              -> OUT/smoke.log
 #   bench[=bench args]      one bench line (default: the driver's default line)  -> OUT/bench.json
 #   ab=NAME[:ENV=v,ENV=v]   cfg2 matvec-only bench under extra environment       -> OUT/ab_NAME.json
-#   trace[=bench args]      rocprofv3 --kernel-trace --stats of a matvec-only bench -> OUT/trace/,
+#   trace[=bench args]      rocprofv3 --kernel-trace --stats of a matvec-only bench -> OUT/trace_<config>/,
 #                           OUT/rocprof_summary_<config>.json (tools/rocprof_summary.py: per-dispatch
 #                           steady state of the timed steps)
 #   pmc[=config]            FETCH_SIZE, WRITE_SIZE and VALU counter passes (one rocprofv3 run each)
@@ -47,12 +47,12 @@ for step in "$@"; do
         grep '^{' "$OUT/ab_$v.log" | tail -1 > "$OUT/ab_$v.json"
         python3 tools/show_bench.py "$OUT/ab_$v.json" "$v" ;;
     trace)
-        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
-            -- python3 bench.py --steps 20 --warmup 3 $MV $arg > "$OUT/trace.log" 2>&1 || fail trace "$OUT/trace.log"
         cfg=$(echo "$arg" | sed -n 's/.*--config \([a-z0-9_]*\).*/\1/p')
         cfg=${cfg:-cfg2}
-        grep '^{' "$OUT/trace.log" | tail -1 > "$OUT/trace_bench_$cfg.json"
-        python3 tools/rocprof_summary.py "$OUT/trace" "$OUT/trace_bench_$cfg.json" "$OUT/rocprof_summary_$cfg.json" ;;
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$cfg" -o run --output-format csv \
+            -- python3 bench.py --steps 20 --warmup 3 $MV $arg > "$OUT/trace_$cfg.log" 2>&1 || fail trace "$OUT/trace_$cfg.log"
+        grep '^{' "$OUT/trace_$cfg.log" | tail -1 > "$OUT/trace_bench_$cfg.json"
+        python3 tools/rocprof_summary.py "$OUT/trace_$cfg" "$OUT/trace_bench_$cfg.json" "$OUT/rocprof_summary_$cfg.json" ;;
     pmc)
         cfg=${arg:-cfg2}
         K="k_modup|k_ks_ip|k_bsgs_inner|k_moddown|k_ks_intt|k_giant_sum|k_centered"
