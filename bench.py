@@ -505,6 +505,9 @@ def main():
             "ntt_valu_roofline": valu,
             "matvec_roofline": matvec_roof,
             "kernels": rows,
+            "kernels_basis": (f"instrumented untimed pass of {prof_steps} steps before the timed region, every kernel "
+                              "bracketed by HIP events (each bracket adds queue time); the roofline entries time their "
+                              "kernel inside the timed region"),
             "staging_ring": staging,
             "parity": parity,
         }
