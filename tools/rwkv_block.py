@@ -102,9 +102,12 @@ def _wkv(block, xs, r, k, v, state, v_first):
         v_first_out = v_first
     # every head at once (bg:838-845 loop over heads): sa = S (-kk), S' = S diag(decay) + sa (kk a)^T + v k^T,
     # wkv = S' r
-    sa = np.einsum("hij,hj->hi", state, -kk_h)
-    new_state = state * decay[:, None, :] + sa[:, :, None] * (kk_h * a_h)[:, None, :] + v_h[:, :, None] * k_h[:, None, :]
-    wkv_heads = np.einsum("hij,hj->hi", new_state, r_h)
+    # the two rank-1 updates as one batched (hs x 2) @ (2 x hs) product, added in place: two 1 MB arrays per
+    # call instead of five (the client's share of the block is allocation-bound on a loaded host)
+    sa = np.matmul(state, -kk_h[:, :, None])[:, :, 0]
+    new_state = np.matmul(np.stack([sa, v_h], axis=2), np.stack([kk_h * a_h, k_h], axis=1))
+    new_state += state * decay[:, None, :]
+    wkv_heads = np.matmul(new_state, r_h[:, :, None])[:, :, 0]
     wkv = group_norm(wkv_heads.reshape(D), H, block.ln_x_w, block.ln_x_b)
     wkv = wkv + ((r_h * k_h * block.r_k).sum(axis=1, keepdims=True) * v_h).reshape(D)
     g = sigmoid(xs["g"] @ block.g1) @ block.g2
