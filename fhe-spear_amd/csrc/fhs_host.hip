@@ -2311,31 +2311,33 @@ extern "C" fhs_status fhs_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key
     BatchOutT<fhs_ciphertext> bo(outs, count);
     const int l = pts[0]->l;
     const size_t S = (size_t)l * c->N;
-    std::vector<uint64_t*> c1(count);
     for (int i = 0; i < count; ++i) {
         fhs_ciphertext* ct;
         fhs_status s = new_ct(c, 2, pts[i]->ci, pts[i]->scale, &ct);
         if (s != FHS_OK) return s;
         outs[i] = ct;
-        c1[i] = ct->d + S;
     }
     const uint64_t ctr0 = sk->ctr;
     sk->ctr += (uint64_t)count;
     const uint64_t step = stream_id(0, 1, 0);   // consecutive counters: stream ids 2^16 apart
-    uint64_t *eb = nullptr, *dptrs = nullptr;
+    std::vector<uint64_t*> ptrs(2 * (size_t)count);
+    for (int i = 0; i < count; ++i) {
+        ptrs[i] = outs[i]->d;
+        ptrs[count + i] = pts[i]->d;
+    }
+    uint64_t *eb = nullptr, *dptrs = nullptr, *small = nullptr;
+    const size_t small_b = ((size_t)c->N * count + 7) & ~(size_t)7;
     HIPCHK(dalloc(c, &eb, 8 * S * count), "encrypt");
-    hipError_t e = dalloc(c, &dptrs, 8 * (size_t)count);
-    if (e == hipSuccess) e = stage_h2d(c, dptrs, c1.data(), 8 * (size_t)count);
+    hipError_t e = dalloc(c, &dptrs, 16 * (size_t)count);
+    if (e == hipSuccess) e = dalloc(c, &small, small_b);
+    if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 16 * (size_t)count);
     if (e == hipSuccess)
-        e = fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, sk->key, stream_id(ST_ENC_SYM, ctr0, 0), nullptr, l, c->st,
-                               count, step, reinterpret_cast<fhs::u64* const*>(dptrs));
-    if (e == hipSuccess)
-        e = fhs::launch_sample(c->T, fhs::SAMPLE_CBD, sk->key, stream_id(ST_ENC_SYM, ctr0, 1), eb, l, c->st, count, step);
-    if (e == hipSuccess) e = fhs::launch_ntt_fwd(c->T, eb, l, l, count, S, c->st);
-    for (int i = 0; e == hipSuccess && i < count; ++i)
-        e = fhs::launch_encrypt_combine(c->T, 0, outs[i]->d, c1[i], sk->s, nullptr, nullptr, eb + (size_t)i * S, nullptr,
-                                        pts[i]->d, l, c->st);
-    if (dptrs) dfree(c, dptrs, 8 * (size_t)count);
+        e = fhs::launch_encrypt_sym_batch(c->T, sk->key, stream_id(ST_ENC_SYM, ctr0, 0), stream_id(ST_ENC_SYM, ctr0, 1),
+                                          step, reinterpret_cast<fhs::u64* const*>(dptrs), sk->s,
+                                          reinterpret_cast<const fhs::u64* const*>(dptrs + count), count, l,
+                                          reinterpret_cast<signed char*>(small), eb, c->st);
+    if (small) dfree(c, small, small_b);
+    if (dptrs) dfree(c, dptrs, 16 * (size_t)count);
     dfree(c, eb, 8 * S * count);
     return bo.keep(e == hipSuccess ? FHS_OK : hip_fail(e, "encrypt"));
 }

@@ -139,6 +139,13 @@ hipError_t launch_sample(const DevTables& T, int mode, const ::PrfKey& K, u64 si
 hipError_t launch_switch_key_assemble(const DevTables& T, u64* b_out, const u64* a, const u64* e_ntt, const u64* s_ntt,
                                       const u64* snew_ntt, int digit, hipStream_t st);
 hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int limbs, u64 elt, hipStream_t st);
+// `count` symmetric encryptions: ciphertext y (cts_dev[y]: c0 then c1, l limbs each) of plaintext pts_dev[y]
+// with mask stream sid_mask + y sid_step and CBD error stream sid_err + y sid_step -- the values of
+// launch_sample (UNIFORM, CBD) + launch_ntt_fwd + launch_encrypt_combine(mode 0) per ciphertext.
+// Scratch: small (count x N bytes), eb (count x l x N words).
+hipError_t launch_encrypt_sym_batch(const DevTables& T, const ::PrfKey& K, u64 sid_mask, u64 sid_err, u64 sid_step,
+                                    u64* const* cts_dev, const u64* s, const u64* const* pts_dev, int count, int l,
+                                    signed char* small, u64* eb, hipStream_t st);
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
                                   const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st);
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);

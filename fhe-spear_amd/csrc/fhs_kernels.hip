@@ -1927,6 +1927,76 @@ __global__ void k_encrypt(DevTables T, int mode, u64* c0, u64* c1, const u64* s_
         }
     }
 }
+// ---- batched symmetric encryption (launch_encrypt_sym_batch): the error's small value drawn once per
+// coefficient (k_sample did it once per coefficient AND limb: the same PRF block l times), its forward NTT
+// reading those values straight into the transform, and the mask a drawn inside the combine -- three
+// launches for the whole batch, the same values as k_sample + NTT + k_encrypt per ciphertext.
+__global__ void k_sample_small(int mode, PrfKey K, u64 sid, u64 sid_step, int N, signed char* out) {
+    sid += blockIdx.y * sid_step;
+    out += (size_t)blockIdx.y * N;
+    for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+        u64 r, unused;
+        prf128(K, sid, (uint32_t)n, r, unused);
+        int v;
+        if (mode == SAMPLE_TERNARY) {
+            const u64 t = r % 3;
+            v = t == 2 ? -1 : (int)t;
+        } else {
+            v = __popcll(r & 0x1FFFFFULL) - __popcll((r >> 21) & 0x1FFFFFULL);
+        }
+        out[n] = (signed char)v;
+    }
+}
+template <int LOGN>
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_small(DevTables T, const signed char* small, u64* out,
+                                                                      int limbs) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int b = blockIdx.x;
+    const RedU R = redu(PK(T, b));
+    const signed char* sm = small + (size_t)blockIdx.y * N;
+    u64* p = out + ((size_t)blockIdx.y * limbs + b) * N;
+    const u64 q = R.q;
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
+                               [&](int e) { const int v = sm[e]; return v >= 0 ? (u64)v : q - (u64)(-v); },
+                               [&](int e, u64 v) { p[e] = v; });
+}
+// ciphertext y of the batch: c1 = the uniform mask (k_sample SAMPLE_UNIFORM of stream sid + y sid_step),
+// c0 = e - c1 s + m (k_encrypt mode 0)
+__global__ void k_encrypt_sym(DevTables T, PrfKey K, u64 sid, u64 sid_step, u64* const* cts, const u64* s,
+                              const u64* eb, const u64* const* pts, int l) {
+    const int N = T.N;
+    const size_t S = (size_t)l * N;
+    sid += blockIdx.y * sid_step;
+    u64* c0 = cts[blockIdx.y];
+    u64* c1 = c0 + S;
+    const u64* e = eb + blockIdx.y * S;
+    const u64* m = pts[blockIdx.y];
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const PrimeK& P = PK(T, (int)(idx / N));
+        const u64 q = P.q;
+        u64 hi, lo;
+        prf128(K, sid, (uint32_t)idx, hi, lo);
+        const u64 a = reduce128(lo, hi, P);
+        c1[idx] = a;
+        c0[idx] = addmod(submod(e[idx], mulmod(a, s[idx], P), q), m[idx], q);
+    }
+}
+hipError_t launch_encrypt_sym_batch(const DevTables& T, const PrfKey& K, u64 sid_mask, u64 sid_err, u64 sid_step,
+                                    u64* const* cts_dev, const u64* s, const u64* const* pts_dev, int count, int l,
+                                    signed char* small, u64* eb, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sample_small, dim3((T.N + 255) / 256, count), dim3(256), 0, st, (int)SAMPLE_CBD, K, sid_err,
+                       sid_step, T.N, small);
+    FHS_DISPATCH_LOGN(T.logN, {
+        hipLaunchKernelGGL((k_ntt_fwd_small<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T,
+                           static_cast<const signed char*>(small), eb, l);
+    });
+    const int g1 = eltwise_grid((size_t)l * T.N) / count, gx = g1 > 0 ? g1 : 1;
+    hipLaunchKernelGGL(k_encrypt_sym, dim3(gx, count), dim3(256), 0, st, T, K, sid_mask, sid_step, cts_dev, s,
+                       static_cast<const u64*>(eb), pts_dev, l);
+    return hipGetLastError();
+}
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
                                   const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st) {
     hipLaunchKernelGGL(k_encrypt, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, mode, c0, c1, s_or_pk0,
