@@ -2118,10 +2118,15 @@ static hipError_t readback_buf(fhs_context* c, size_t bytes, double** out) {
 // composed exactly from all its limbs (decode_compose) and decoded on its own.  FHESPEAR_DECODE_HOST_FFT=1
 // runs the slot FFT on the host instead (decode_slots: the same operations, so the same doubles; A/B and
 // test knob).
-static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, int count, int nslots, double* re_im) {
+// cts non-null (with sk): the items are ciphertexts, decrypted straight into the INTT's buffer
+// (fhs_decrypt_decode_batch) instead of plaintexts copied there
+static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, int count, int nslots, double* re_im,
+                              const fhs_ciphertext* const* cts = nullptr, fhs_secret_key* sk = nullptr) {
     const size_t N = c->N, n = N / 2;
-    if (!pts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > n)
+    if ((!pts && !cts) || (cts && !sk) || !re_im || count < 0 || nslots < 1 || (size_t)nslots > n)
         return fail(FHS_ERR_INVALID, "decode: bad arguments");
+    auto lv = [&](int i) { return cts ? cts[i]->l : pts[i]->l; };
+    auto scl = [&](int i) { return cts ? cts[i]->scale : pts[i]->scale; };
     if (count == 0) return FHS_OK;
     static const bool full = getenv("FHESPEAR_DECODE_FULL") != nullptr;       // A/B and test knobs
     static const bool host_crt = getenv("FHESPEAR_DECODE_HOST_CRT") != nullptr;
@@ -2129,8 +2134,8 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     std::vector<int> fast(count, 0), kks(count, 0);
     size_t tmp_words = 0, vt_words = 0;
     for (int i = 0; i < count; ++i) {
-        if (!pts[i]) return fail(FHS_ERR_INVALID, "decode: null plaintext");
-        const int l = pts[i]->l, k = full ? l : decode_limbs(c, pts[i]->scale, l);
+        if (cts ? !cts[i] : !pts[i]) return fail(FHS_ERR_INVALID, "decode: null plaintext or ciphertext");
+        const int l = lv(i), k = full ? l : decode_limbs(c, scl(i), l);
         kks[i] = std::min(l, k + 1);
         fast[i] = kks[i] < l && kks[i] <= fhs::kCrtMaxL && !host_crt;
         if (fast[i]) {
@@ -2157,14 +2162,15 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     unsigned* dflag = reinterpret_cast<unsigned*>(aux + count + vt_words);
     std::vector<uint64_t> head((size_t)count + vt_words, 0);   // scales and vtabs: one staged copy
     for (int i = 0; i < count; ++i) {
-        std::memcpy(&head[i], &pts[i]->scale, 8);
+        const double sc = scl(i);
+        std::memcpy(&head[i], &sc, 8);
         hflag[i] = 0;
     }
     size_t vo = (size_t)count;
     std::vector<size_t> vt_at(count, 0);
     for (int i = 0; i < count; ++i) {
         if (!fast[i]) continue;
-        const int kk = kks[i], nx = pts[i]->l - kk;
+        const int kk = kks[i], nx = lv(i) - kk;
         crt_consts(c, kk, Ks[i]);
         vt_at[i] = vo;
         for (int x = 0; x < nx; ++x, vo += fhs::kCrtVtabWords) {
@@ -2190,15 +2196,16 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     bool one_l = true;
     for (int i = 0; i < count; ++i) {
         if (!fast[i]) continue;
-        one_l &= lf < 0 || pts[i]->l == lf;
-        lf = pts[i]->l;
+        one_l &= lf < 0 || lv(i) == lf;
+        lf = lv(i);
         ++nf;
     }
     size_t to = 0;
     for (int i = 0; e == hipSuccess && i < count; ++i) {
         if (!fast[i]) continue;
-        const int l = pts[i]->l;
-        e = hipMemcpyAsync(tmp + to, pts[i]->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
+        const int l = lv(i);
+        e = cts ? fhs::launch_decrypt(c->T, cts[i]->d, cts[i]->ncomp, sk->s, tmp + to, l, c->st)
+                : hipMemcpyAsync(tmp + to, pts[i]->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
         if (e == hipSuccess && !one_l) e = fhs::launch_ntt_inv(c->T, tmp + to, l, l, 1, 0, c->st);
         to += (size_t)l * N;
     }
@@ -2206,7 +2213,7 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     to = 0;
     for (int i = 0; e == hipSuccess && i < count; ++i) {
         if (!fast[i]) continue;
-        const int l = pts[i]->l, kk = kks[i], nx = l - kk;
+        const int l = lv(i), kk = kks[i], nx = l - kk;
         uint64_t* t = tmp + to;
         e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
                                     t + (size_t)kk * N, nx, aux + vt_at[i], dflag + i);
@@ -2226,7 +2233,14 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     std::vector<double> m;
     for (int i = 0; st == FHS_OK && i < count; ++i) {
         if (fast[i] && hflag[i] == 0) continue;
-        st = decode_compose(c, pts[i], pts[i]->l, m);   // exact: all limbs
+        if (cts) {   // exact: all limbs, from the decrypted plaintext
+            fhs_plaintext* pt = nullptr;
+            st = fhs_decrypt(c, sk, cts[i], &pt);
+            if (st == FHS_OK) st = decode_compose(c, pt, pt->l, m);
+            if (pt) fhs_plaintext_destroy(pt);
+        } else {
+            st = decode_compose(c, pts[i], pts[i]->l, m);   // exact: all limbs
+        }
         if (st != FHS_OK) break;
         double* slot = rb + (size_t)i * per_out;
         if (host_fft) {
@@ -2245,7 +2259,7 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     for (int i = 0; st == FHS_OK && i < count; ++i) {
         double* out = re_im + (size_t)i * 2 * nslots;
         if (host_fft)
-            decode_slots(c, rb + (size_t)i * N, pts[i]->scale, (size_t)nslots, out);
+            decode_slots(c, rb + (size_t)i * N, scl(i), (size_t)nslots, out);
         else
             std::memcpy(out, rb + (size_t)i * per_out, 8 * per_out);
     }
@@ -2261,6 +2275,13 @@ extern "C" fhs_status fhs_decode(fhs_context* c, const fhs_plaintext* pt, double
     ENTER(c);
     if (!pt || !re_im) return fail(FHS_ERR_INVALID, "decode: null argument");
     return decode_many(c, &pt, 1, (int)(c->N / 2), re_im);
+}
+extern "C" fhs_status fhs_decrypt_decode_batch(fhs_context* c, fhs_secret_key* sk, const fhs_ciphertext* const* cts,
+                                               int count, int nslots, double* re_im) {
+    ENTER(c);
+    if (!sk || !cts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > c->N / 2)
+        return fail(FHS_ERR_INVALID, "decrypt_decode_batch: bad arguments");
+    return decode_many(c, nullptr, count, nslots, re_im, cts, sk);
 }
 // Client-side batch (the client-aided block decrypts 2-3 outputs per stage): decode_many over all of
 // them, one synchronisation, only the first `nslots` slots of each back to the host.
@@ -2293,37 +2314,26 @@ extern "C" fhs_status fhs_encrypt_symmetric(fhs_context* c, fhs_secret_key* sk, 
     *out = ct;
     return FHS_OK;
 }
-extern "C" fhs_status fhs_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key* sk, const fhs_plaintext* const* pts,
-                                                  int count, fhs_ciphertext** outs) {
-    ENTER(c);
-    if (!sk || !pts || !outs || count < 0) return fail(FHS_ERR_INVALID, "encrypt_batch: bad arguments");
-    for (int i = 0; i < count; ++i)
-        if (!pts[i]) return fail(FHS_ERR_INVALID, "encrypt_batch: null plaintext");
-    bool same = count > 0;
-    for (int i = 1; i < count; ++i) same &= pts[i]->l == pts[0]->l;
-    if (!same) {   // mixed levels: one at a time (the same counters in the same order)
-        for (int i = 0; i < count; ++i) {
-            const fhs_status s = fhs_encrypt_symmetric(c, sk, pts[i], &outs[i]);
-            if (s != FHS_OK) return s;
-        }
-        return FHS_OK;
-    }
+// `count` symmetric encryptions at l limbs into new ciphertexts outs[i] (chain index ci, scale scales[i]):
+// of the plaintexts pts[i], or (pts null) of the rounded message coefficients `coef` already in HBM
+// (count x N doubles, launch_encode_coef) -- encode and encrypt fused.  Counters as `count` calls.
+static fhs_status encrypt_sym_core(fhs_context* c, fhs_secret_key* sk, int count, int l, int ci, const double* scales,
+                                   const fhs_plaintext* const* pts, const double* coef, fhs_ciphertext** outs) {
     BatchOutT<fhs_ciphertext> bo(outs, count);
-    const int l = pts[0]->l;
     const size_t S = (size_t)l * c->N;
     for (int i = 0; i < count; ++i) {
         fhs_ciphertext* ct;
-        fhs_status s = new_ct(c, 2, pts[i]->ci, pts[i]->scale, &ct);
+        fhs_status s = new_ct(c, 2, ci, scales[i], &ct);
         if (s != FHS_OK) return s;
         outs[i] = ct;
     }
     const uint64_t ctr0 = sk->ctr;
     sk->ctr += (uint64_t)count;
     const uint64_t step = stream_id(0, 1, 0);   // consecutive counters: stream ids 2^16 apart
-    std::vector<uint64_t*> ptrs(2 * (size_t)count);
+    std::vector<uint64_t*> ptrs(2 * (size_t)count, nullptr);
     for (int i = 0; i < count; ++i) {
         ptrs[i] = outs[i]->d;
-        ptrs[count + i] = pts[i]->d;
+        if (pts) ptrs[count + i] = pts[i]->d;
     }
     uint64_t *eb = nullptr, *dptrs = nullptr, *small = nullptr;
     const size_t small_b = ((size_t)c->N * count + 7) & ~(size_t)7;
@@ -2334,12 +2344,65 @@ extern "C" fhs_status fhs_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key
     if (e == hipSuccess)
         e = fhs::launch_encrypt_sym_batch(c->T, sk->key, stream_id(ST_ENC_SYM, ctr0, 0), stream_id(ST_ENC_SYM, ctr0, 1),
                                           step, reinterpret_cast<fhs::u64* const*>(dptrs), sk->s,
-                                          reinterpret_cast<const fhs::u64* const*>(dptrs + count), count, l,
-                                          reinterpret_cast<signed char*>(small), eb, c->st);
+                                          pts ? reinterpret_cast<const fhs::u64* const*>(dptrs + count) : nullptr,
+                                          count, l, reinterpret_cast<signed char*>(small), eb, c->st, coef);
     if (small) dfree(c, small, small_b);
     if (dptrs) dfree(c, dptrs, 16 * (size_t)count);
     dfree(c, eb, 8 * S * count);
     return bo.keep(e == hipSuccess ? FHS_OK : hip_fail(e, "encrypt"));
+}
+extern "C" fhs_status fhs_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key* sk, const fhs_plaintext* const* pts,
+                                                  int count, fhs_ciphertext** outs) {
+    ENTER(c);
+    if (!sk || !pts || !outs || count < 0) return fail(FHS_ERR_INVALID, "encrypt_batch: bad arguments");
+    for (int i = 0; i < count; ++i)
+        if (!pts[i]) return fail(FHS_ERR_INVALID, "encrypt_batch: null plaintext");
+    bool same = count > 0;
+    for (int i = 1; i < count; ++i) same &= pts[i]->l == pts[0]->l && pts[i]->ci == pts[0]->ci;
+    if (!same) {   // mixed levels: one at a time (the same counters in the same order)
+        for (int i = 0; i < count; ++i) {
+            const fhs_status s = fhs_encrypt_symmetric(c, sk, pts[i], &outs[i]);
+            if (s != FHS_OK) return s;
+        }
+        return FHS_OK;
+    }
+    std::vector<double> scales(count);
+    for (int i = 0; i < count; ++i) scales[i] = pts[i]->scale;
+    return encrypt_sym_core(c, sk, count, pts[0]->l, pts[0]->ci, scales.data(), pts, nullptr, outs);
+}
+// Extension (the client's encrypt_replicated of a stage's inputs, bg:53-58 / 124-127, in one pass):
+// encode `count` vectors of n values (real, or interleaved re/im) at `scale` and chain index ci and encrypt
+// them with sk -- limb for limb fhs_encode[_real]_batch followed by fhs_encrypt_symmetric_batch, without
+// the plaintexts: the message's rounded coefficients go into the error's NTT.
+extern "C" fhs_status fhs_encode_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key* sk, const double* values,
+                                                         size_t count, size_t n, int is_real, double scale, int ci,
+                                                         fhs_ciphertext** outs) {
+    ENTER(c);
+    if (!sk || !outs || (!values && count && n)) return fail(FHS_ERR_INVALID, "encode_encrypt: null argument");
+    fhs_status st = encode_checks(c, n, scale, ci);
+    if (st != FHS_OK) return st;
+    if (count == 0) return FHS_OK;
+    if (count > 4096) return fail(FHS_ERR_INVALID, "encode_encrypt: at most 4096 vectors per call");
+    const size_t stride = is_real ? n : 2 * n, N = c->N;
+    const int l = c->L0 + 1 - ci;
+    uint64_t *dvals = nullptr, *coef = nullptr;
+    const size_t vb = std::max<size_t>(8, 8 * count * stride), cb = 8 * count * N;
+    HIPCHK(dalloc(c, &dvals, vb), "encode_encrypt");
+    hipError_t e = dalloc(c, &coef, cb);
+    if (e == hipSuccess && stride) e = stage_h2d(c, dvals, values, 8 * count * stride);
+    if (e == hipSuccess)
+        e = fhs::launch_encode_coef(c->T, reinterpret_cast<const double*>(dvals), (int)count, n, stride, is_real != 0,
+                                    scale, reinterpret_cast<double*>(coef), c->st);
+    if (e == hipSuccess) {
+        std::vector<double> scales(count, scale);
+        st = encrypt_sym_core(c, sk, (int)count, l, ci, scales.data(), nullptr, reinterpret_cast<const double*>(coef),
+                              outs);
+    } else {
+        st = hip_fail(e, "encode_encrypt");
+    }
+    if (coef) dfree(c, coef, cb);
+    dfree(c, dvals, vb);
+    return st;
 }
 extern "C" fhs_status fhs_encrypt_asymmetric(fhs_context* c, fhs_public_key* pk, const fhs_plaintext* pt,
                                              fhs_ciphertext** out) {

@@ -145,7 +145,11 @@ hipError_t launch_galois_perm(const DevTables& T, const u64* in, u64* out, int l
 // Scratch: small (count x N bytes), eb (count x l x N words).
 hipError_t launch_encrypt_sym_batch(const DevTables& T, const ::PrfKey& K, u64 sid_mask, u64 sid_err, u64 sid_step,
                                     u64* const* cts_dev, const u64* s, const u64* const* pts_dev, int count, int l,
-                                    signed char* small, u64* eb, hipStream_t st);
+                                    signed char* small, u64* eb, hipStream_t st, const double* coef = nullptr);
+// coef (count x N rounded message coefficients, launch_encode_coef) instead of pts_dev (null): encode and
+// encrypt fused -- the message enters the error's NTT, the same limbs as encoding then encrypting.
+hipError_t launch_encode_coef(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
+                              double scale, double* coef, hipStream_t st);
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
                                   const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st);
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);

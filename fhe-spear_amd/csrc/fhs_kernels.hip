@@ -1961,6 +1961,27 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_small(DevTables
                                [&](int e) { const int v = sm[e]; return v >= 0 ? (u64)v : q - (u64)(-v); },
                                [&](int e, u64 v) { p[e] = v; });
 }
+// encode + encrypt fused: NTT(m + e) of the rounded message coefficients (coef, doubles; k_encode's
+// coef_out, reduced per limb by dbl_mod as k_ntt_fwd_from_dbl does) plus the small error -- the NTT is
+// linear and its outputs canonical, so the limbs equal NTT(m) + NTT(e) mod q, i.e. encode then encrypt
+template <int LOGN>
+__global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_msg_err(DevTables T, const double* coef,
+                                                                        const signed char* small, u64* out, int limbs) {
+    constexpr int N = 1 << LOGN;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    const int b = blockIdx.x;
+    const RedU R = redu(PK(T, b));
+    const double* cf = coef + (size_t)blockIdx.y * N;
+    const signed char* sm = small + (size_t)blockIdx.y * N;
+    u64* p = out + ((size_t)blockIdx.y * limbs + b) * N;
+    const u64 q = R.q;
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
+                               [&](int e) {   // < 2q: inside the forward NTT's input bound
+                                   const int v = sm[e];
+                                   return dbl_mod(T, cf[e], b) + (v >= 0 ? (u64)v : q - (u64)(-v));
+                               },
+                               [&](int e, u64 v) { p[e] = v; });
+}
 // ciphertext y of the batch: c1 = the uniform mask (k_sample SAMPLE_UNIFORM of stream sid + y sid_step),
 // c0 = e - c1 s + m (k_encrypt mode 0)
 __global__ void k_encrypt_sym(DevTables T, PrfKey K, u64 sid, u64 sid_step, u64* const* cts, const u64* s,
@@ -1971,7 +1992,7 @@ __global__ void k_encrypt_sym(DevTables T, PrfKey K, u64 sid, u64 sid_step, u64*
     u64* c0 = cts[blockIdx.y];
     u64* c1 = c0 + S;
     const u64* e = eb + blockIdx.y * S;
-    const u64* m = pts[blockIdx.y];
+    const u64* m = pts ? pts[blockIdx.y] : nullptr;   // null: the message is already inside eb
     for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
         const PrimeK& P = PK(T, (int)(idx / N));
         const u64 q = P.q;
@@ -1979,18 +2000,23 @@ __global__ void k_encrypt_sym(DevTables T, PrfKey K, u64 sid, u64 sid_step, u64*
         prf128(K, sid, (uint32_t)idx, hi, lo);
         const u64 a = reduce128(lo, hi, P);
         c1[idx] = a;
-        c0[idx] = addmod(submod(e[idx], mulmod(a, s[idx], P), q), m[idx], q);
+        const u64 c = submod(e[idx], mulmod(a, s[idx], P), q);
+        c0[idx] = m ? addmod(c, m[idx], q) : c;
     }
 }
 hipError_t launch_encrypt_sym_batch(const DevTables& T, const PrfKey& K, u64 sid_mask, u64 sid_err, u64 sid_step,
                                     u64* const* cts_dev, const u64* s, const u64* const* pts_dev, int count, int l,
-                                    signed char* small, u64* eb, hipStream_t st) {
+                                    signed char* small, u64* eb, hipStream_t st, const double* coef) {
     if (count <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_sample_small, dim3((T.N + 255) / 256, count), dim3(256), 0, st, (int)SAMPLE_CBD, K, sid_err,
                        sid_step, T.N, small);
     FHS_DISPATCH_LOGN(T.logN, {
-        hipLaunchKernelGGL((k_ntt_fwd_small<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T,
-                           static_cast<const signed char*>(small), eb, l);
+        if (coef)
+            hipLaunchKernelGGL((k_ntt_fwd_msg_err<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T, coef,
+                               static_cast<const signed char*>(small), eb, l);
+        else
+            hipLaunchKernelGGL((k_ntt_fwd_small<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T,
+                               static_cast<const signed char*>(small), eb, l);
     });
     const int g1 = eltwise_grid((size_t)l * T.N) / count, gx = g1 > 0 ? g1 : 1;
     hipLaunchKernelGGL(k_encrypt_sym, dim3(gx, count), dim3(256), 0, st, T, K, sid_mask, sid_step, cts_dev, s,
@@ -2109,7 +2135,7 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
     const int tid = threadIdx.x;
     const double* src = vals + (size_t)blockIdx.x * stride;
     const double2* W = reinterpret_cast<const double2*>(T.enc_w);
-    u64* out = outs[blockIdx.x];
+    u64* out = outs ? outs[blockIdx.x] : nullptr;   // null: coefficients to coef_out only
     double* dout = coef_out ? coef_out + (size_t)blockIdx.x * N : nullptr;
     if constexpr (!SPLIT) {
         for (int j = tid; j < H; j += TH) {
@@ -2271,6 +2297,16 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_from_dbl(DevTab
                                [&](int e) { return dbl_mod(T, cf[e], b); }, [&](int e, u64 v) { p[e] = v; });
 }
 
+hipError_t launch_encode_coef(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
+                              double scale, double* coef, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    FHS_DISPATCH_LOGN(T.logN, {
+        constexpr int TH = ((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024;
+        hipLaunchKernelGGL((k_encode<LOGN>), dim3(count), dim3(TH), 0, st, T, vals, n, stride, is_real ? 1 : 0, scale,
+                           static_cast<u64* const*>(nullptr), 0, coef);
+    });
+    return hipGetLastError();
+}
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
                          double scale, u64* const* outs_dev, int l, hipStream_t st, double* coef_scratch) {
     if (count <= 0) return hipSuccess;

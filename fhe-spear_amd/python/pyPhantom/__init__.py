@@ -127,6 +127,9 @@ _SIGS = {
     "fhs_decode_batch": (C.c_int, [_vp, _vp, C.c_int, C.c_int, _dblp]),
     "fhs_encrypt_symmetric": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_encrypt_symmetric_batch": (C.c_int, [_vp, _vp, _vp, C.c_int, _vp]),
+    "fhs_encode_encrypt_symmetric_batch": (C.c_int, [_vp, _vp, _dblp, C.c_size_t, C.c_size_t, C.c_int, C.c_double,
+                                                     C.c_int, _vp]),
+    "fhs_decrypt_decode_batch": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, _dblp]),
     "fhs_encrypt_asymmetric": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_decrypt": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
     "fhs_add": (C.c_int, [_vp, _vp, _vp, C.POINTER(_vp)]),
@@ -598,6 +601,34 @@ class secret_key:
         outs = (_vp * n)()
         _check(_lib.fhs_encrypt_symmetric_batch(ctx._h, self._h, ins, n, outs), "encrypt_symmetric_batch")
         return [ciphertext(ctx, _vp(outs[i])) for i in range(n)]
+
+    def encode_encrypt_batch(self, ctx, mat, scale, chain_index=1):
+        """Extension: one ciphertext per row of `mat` (real rows: encode_double_vector_batch, complex rows:
+        encode_complex_vector_batch) encrypted with this key -- the same ciphertexts as encoding then
+        encrypt_symmetric_batch, in one pass without plaintexts (fhs_encode_encrypt_symmetric_batch)."""
+        cplx = np.iscomplexobj(mat)
+        m = np.ascontiguousarray(np.asarray(mat, dtype=np.complex128 if cplx else np.float64))
+        if m.ndim != 2:
+            raise ValueError("encode_encrypt_batch expects a 2-D array (count, values)")
+        count, n = m.shape
+        if count == 0:
+            return []
+        outs = (_vp * count)()
+        _check(_lib.fhs_encode_encrypt_symmetric_batch(ctx._h, self._h, m.ctypes.data_as(_dblp), count, n,
+                                                       0 if cplx else 1, float(scale), int(chain_index), outs),
+               "encode_encrypt_batch")
+        return [ciphertext(ctx, _vp(outs[i])) for i in range(count)]
+
+    def decrypt_decode_batch(self, ctx, cts, nslots=None):
+        """Extension: decrypt each ciphertext and decode its first `nslots` slots (default all) -- the
+        values of decrypt + ckks_encoder.decode_batch, without plaintexts (fhs_decrypt_decode_batch);
+        complex array [len(cts), nslots]."""
+        n = ctx.N // 2 if nslots is None else int(nslots)
+        out = np.empty((len(cts), n, 2), dtype=np.float64)
+        hs = (_vp * max(1, len(cts)))(*[c._h for c in cts])
+        _check(_lib.fhs_decrypt_decode_batch(ctx._h, self._h, hs, len(cts), n, out.ctypes.data_as(_dblp)),
+               "decrypt_decode_batch")
+        return out[..., 0] + 1j * out[..., 1]
 
     def decrypt(self, ctx, ct):
         return _pt(ctx, _lib.fhs_decrypt, self._h, ct._h, what="decrypt")

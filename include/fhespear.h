@@ -149,6 +149,16 @@ fhs_status fhs_encrypt_symmetric(fhs_context* ctx, fhs_secret_key* sk, const fhs
  * counter); the samplers and NTTs run once over the whole batch */
 fhs_status fhs_encrypt_symmetric_batch(fhs_context* ctx, fhs_secret_key* sk, const fhs_plaintext* const* pts, int count,
                                        fhs_ciphertext** out_array);
+/* Extension: encode `count` vectors of n values (is_real: n doubles each; else n interleaved (re, im)) at
+ * `scale` / `chain_index` and encrypt them with sk in one pass -- the same ciphertexts as
+ * fhs_encode[_real]_batch + fhs_encrypt_symmetric_batch (no plaintext objects; count <= 4096) */
+fhs_status fhs_encode_encrypt_symmetric_batch(fhs_context* ctx, fhs_secret_key* sk, const double* values, size_t count,
+                                              size_t n, int is_real, double scale, int chain_index,
+                                              fhs_ciphertext** out_array);
+/* Extension: decrypt `count` ciphertexts with sk and decode the first `nslots` slots of each (re_im_out =
+ * count x nslots x (re, im)) -- the doubles of fhs_decrypt + fhs_decode_batch, without the plaintexts */
+fhs_status fhs_decrypt_decode_batch(fhs_context* ctx, fhs_secret_key* sk, const fhs_ciphertext* const* cts, int count,
+                                    int nslots, double* re_im_out);
 fhs_status fhs_encrypt_asymmetric(fhs_context* ctx, fhs_public_key* pk, const fhs_plaintext* pt, fhs_ciphertext** out);
 fhs_status fhs_decrypt(fhs_context* ctx, fhs_secret_key* sk, const fhs_ciphertext* ct, fhs_plaintext** out);
 

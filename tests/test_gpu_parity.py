@@ -744,6 +744,36 @@ def test_encrypt_symmetric_batch_equals_single_encryptions(ph):
     assert b.encrypt_symmetric_batch(ctx, []) == []
 
 
+def test_fused_client_calls_equal_separate_calls(ph):
+    """encode_encrypt_batch (the message's rounded coefficients go into the error's NTT) gives the
+    ciphertexts of encode_*_vector_batch + encrypt_symmetric_batch, limb for limb, real and complex rows at
+    two chain indices; decrypt_decode_batch (decrypted straight into the decoder's INTT buffer) gives the
+    doubles of decrypt + decode_batch, including a ciphertext whose decryption aliases (all-limb path)."""
+    N, L0, P = 2048, 6, 2
+    ctx, _, primes = make_ctx(ph, N, L0, P, seed=51)
+    a, b = ph.secret_key(ctx, seed=52), ph.secret_key(ctx, seed=52)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(53)
+    real = rng.normal(0, 1, (3, N // 2))
+    cplx = rng.normal(0, 1, (2, 100)) + 1j * rng.normal(0, 1, (2, 100))
+    for rows, ci in ((real, 1), (cplx, 1), (real[:1], 3), (cplx, 2)):
+        batch = enc.encode_complex_vector_batch if np.iscomplexobj(rows) else enc.encode_double_vector_batch
+        want = a.encrypt_symmetric_batch(ctx, batch(ctx, rows, 2.0 ** 40, ci))
+        got = b.encode_encrypt_batch(ctx, rows, 2.0 ** 40, ci)
+        assert len(got) == len(want)
+        for g, w in zip(got, want):
+            assert g.chain_index() == w.chain_index() and g.scale() == w.scale()
+            assert np.array_equal(g.to_numpy(), w.to_numpy())
+    cts = a.encode_encrypt_batch(ctx, real, 2.0 ** 40) + a.encode_encrypt_batch(ctx, cplx, 2.0 ** 40, 2)[:1]
+    o = oracle_for(primes, N, P)
+    cts.append(ph.ciphertext_from_numpy(ctx, np.stack([rand_pt(o, rng, L0), rand_pt(o, rng, L0)]), 1, 2.0 ** 40))
+    for group in (cts[:3], cts[3:], cts):
+        for n in (N // 2, 64):
+            want = enc.decode_batch(ctx, [a.decrypt(ctx, c) for c in group], n)
+            got = a.decrypt_decode_batch(ctx, group, n)
+            assert np.array_equal(got, want), n
+
+
 def test_decode_batch_equals_single_decodes(ph):
     """fhs_decode_batch (the client's decrypt_vec of a block stage in one synchronisation) returns the
     same doubles as fhs_decode one plaintext at a time: real and complex encodings at two levels, and a

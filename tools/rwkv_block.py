@@ -180,17 +180,19 @@ class Server:
     def decrypt_vec_complex(self, ct, n):
         return np.array(self.encoder.decode_complex_vector(self.ctx, self.sk.decrypt(self.ctx, ct)))[:n]
 
-    # the client's calls of one stage batched: one encode upload for all its inputs, one synchronisation
-    # for all its decodes (pyPhantom encode_*_batch, decode_batch) -- the same values as one at a time
+    # the client's calls of one stage batched: encode + encrypt of all its inputs in one library pass, decrypt
+    # + decode of all its outputs in one (one synchronisation) -- the same values as one at a time
     def encrypt_replicated_batch(self, xs, cplx=False):
         reps = -(-self.slots // len(xs[0]))
         rows = np.stack([np.tile(np.asarray(x), reps)[:self.slots] for x in xs])
-        enc = self.encoder.encode_complex_vector_batch if cplx else self.encoder.encode_double_vector_batch
-        return self.sk.encrypt_symmetric_batch(self.ctx, enc(self.ctx, rows, self.scale))
+        rows = rows.astype(np.complex128) if cplx else rows.astype(np.float64)
+        # encode + encrypt_symmetric of each row (bg:53-58) in one library pass: the same ciphertexts
+        return self.sk.encode_encrypt_batch(self.ctx, rows, self.scale)
 
     def decrypt_vecs(self, cts, n):
         """complex slots [len(cts), n] (real parts for real-packed outputs)"""
-        return self.encoder.decode_batch(self.ctx, [self.sk.decrypt(self.ctx, c) for c in cts], n)
+        # decrypt + decode_complex_vector of each (bg:784-892's decrypt_vec) in one library pass: the same doubles
+        return self.sk.decrypt_decode_batch(self.ctx, cts, n)
 
     # bg:361-432
     def encode_real(self, M, rows=None):
