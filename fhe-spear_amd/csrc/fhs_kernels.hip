@@ -1961,6 +1961,7 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_small(DevTables
                                [&](int e) { const int v = sm[e]; return v >= 0 ? (u64)v : q - (u64)(-v); },
                                [&](int e, u64 v) { p[e] = v; });
 }
+__device__ __forceinline__ u64 dbl_mod(const DevTables& T, double d, int i);   // below, with the encoder
 // encode + encrypt fused: NTT(m + e) of the rounded message coefficients (coef, doubles; k_encode's
 // coef_out, reduced per limb by dbl_mod as k_ntt_fwd_from_dbl does) plus the small error -- the NTT is
 // linear and its outputs canonical, so the limbs equal NTT(m) + NTT(e) mod q, i.e. encode then encrypt
