@@ -244,7 +244,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     os.environ.setdefault("FHESPEAR_DEVICE", str(local))
     dist = None
-    if world > 1:
+    # FHESPEAR_BENCH_DIST=1 under torchrun at world 1: the multi-rank step (RCCL gather to rank 0) on one
+    # GPU, to time its exchange ordering where no second GPU exists
+    if world > 1 or (env_world is not None and os.environ.get("FHESPEAR_BENCH_DIST") == "1"):
         import torch
         import torch.distributed as dist
         if os.environ.get("FHESPEAR_DIST_BACKEND", "nccl") == "gloo":
@@ -293,18 +295,24 @@ def main():
         import fhespear_dist
 
     gathered = [None]
+    SYNC_GATHER = os.environ.get("FHESPEAR_BENCH_SYNC_GATHER") == "1"
 
     def step():
         baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
         y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
         if dist is not None:     # cfg4: output ciphertexts to rank 0 over RCCL (xGMI)
-            # the previous step's gather (torch/RCCL stream) must have read the buffer before the
-            # library's stream overwrites it; it finished long before this step's kernels did
-            torch.cuda.current_stream().synchronize()
-            ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
-            if dist.get_backend() == "gloo":
+            if dist.get_backend() == "gloo":   # rehearsal: host-staged
+                ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
                 gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf.cpu(), world, rank)
+            elif SYNC_GATHER:   # round 1-3 ordering (A/B knob): host waits for the step, then for the gather
+                torch.cuda.current_stream().synchronize()
+                ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
+                gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
             else:
+                # device-side ordering only (fhespear_dist.to_buffer): the copy waits on the library stream
+                # for torch's pending work on the buffer (the previous step's gather), RCCL's gather waits for
+                # the copy -- the host never blocks, so it enqueues the next step while this one runs
+                fhespear_dist.to_buffer(ph, ctx, y, gather_buf)
                 gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
         return y
 

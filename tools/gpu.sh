@@ -13,6 +13,7 @@
 #                           -> OUT/pmc_traffic_<config>.json, OUT/pmc_valu_<config>.json
 #   rehearse=N[:bench args] N ranks sharing this one GPU (gloo, host-staged exchange; timings
 #                           meaningless): bench.py --gpus N self-launches them -> OUT/rehearse_nN.json
+#   dist1[=NAME[:ENV=v,..]] matvec bench at world 1 under torchrun with the RCCL gather step -> OUT/NAME.json
 #   py=SCRIPT[:args]        python SCRIPT args                                  -> OUT/py_<name>.log
 #   ptrace=SCRIPT[:args]    the same under rocprofv3 --kernel-trace --stats      -> OUT/ptrace_<name>/
 set -o pipefail
@@ -65,6 +66,17 @@ for step in "$@"; do
         python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" \
             "$OUT/pmc_write/run_counter_collection.csv" 7 "$OUT/pmc_traffic_$cfg.json" || exit 1
         python3 tools/pmc_valu.py "$OUT/pmc_valu/run_counter_collection.csv" 7 "$OUT/pmc_valu_$cfg.json" || exit 1 ;;
+    dist1)
+        # the multi-rank step (RCCL gather, device-side stream ordering) at world 1 on this one GPU
+        v=${arg%%:*}
+        v=${v:-dist1}
+        envs=""
+        [ "$v" != "$arg" ] && [ -n "$arg" ] && envs=$(echo "${arg#*:}" | tr ',' ' ')
+        env FHESPEAR_BENCH_DIST=1 $envs timeout -k 10 400 python -m torch.distributed.run --nnodes 1 \
+            --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 20 --warmup 3 $MV \
+            > "$OUT/$v.log" 2>&1 || fail dist1 "$OUT/$v.log"
+        grep '^{' "$OUT/$v.log" | tail -1 > "$OUT/$v.json"
+        python3 tools/show_bench.py "$OUT/$v.json" "$v" ;;
     rehearse)
         n=${arg%%:*}
         a=""
