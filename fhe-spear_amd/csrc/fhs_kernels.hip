@@ -34,13 +34,15 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_INNER_VEC 2        // consecutive coefficients per lane in k_bsgs_inner (16-byte loads)
 #define FHS_MODDOWN_HALF 1     // k_moddown_h: half-limb LDS
 #define FHS_INTT_HALF 1        // k_ks_intt_h: half-limb LDS inverse NTT
-#ifndef FHS_MODUPH_CH
 #ifndef FHS_MODUP_QUADPAIR
 #define FHS_MODUP_QUADPAIR 1   // k_modup_h block decode: 1 = xcd_quadpair (inputs read by 4 XCDs), 0 = xcd_tinner
 #endif
+#ifndef FHS_MODUPH_CH
 #define FHS_MODUPH_CH 2        // k_modup_h: coefficient pairs per conversion chunk
 #endif
+#ifndef FHS_MODUPH_RL
 #define FHS_MODUPH_RL 3        // k_modup_h: radix (log2) of the NTT register passes
+#endif
 #define FHS_MODUP_CH 4         // k_modup (full-limb form): coefficients per conversion chunk
 #define FHS_MODUP_RL 4         // k_modup (full-limb form): radix (log2) of the NTT register passes
 #define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
