@@ -346,6 +346,7 @@ struct fhs_context {
     hipEvent_t ring_ev[kRingSegs] = {};
     uint64_t ring_waits = 0, ring_blocked = 0;   // segment re-entries; of those, the ones that had to wait
     fhs::Stager stager{};
+    std::map<std::pair<int, int>, std::vector<uint64_t>> crt_cache;   // decoder tables per (kk, l) (crt_tables)
     // pinned, grow-only: the decoder's slots (and flags) come back through it
     double* readback = nullptr;
     size_t readback_bytes = 0;
@@ -2007,6 +2008,34 @@ static void crt_consts(const fhs_context* c, int l, fhs::CrtConsts& K) {
 }
 // INTT of the first lv limbs and the centred CRT composition of the first k on the GPU, checked against
 // limbs k..lv-1 (*exact = every coefficient matched them); N doubles to the host
+// The composition constants of the first kk limbs and the check tables of limbs kk..l-1 ([CrtConsts as
+// words][l - kk vtabs of kCrtVtabWords]), built once per (kk, l) and kept in the context: a client decodes
+// the same few levels over and over
+static const std::vector<uint64_t>& crt_tables(fhs_context* c, int kk, int l) {
+    std::vector<uint64_t>& tab = c->crt_cache[std::make_pair(kk, l)];
+    if (!tab.empty()) return tab;
+    constexpr size_t KW = sizeof(fhs::CrtConsts) / 8;
+    static_assert(sizeof(fhs::CrtConsts) % 8 == 0, "CrtConsts packs into words");
+    fhs::CrtConsts K;
+    crt_consts(c, kk, K);
+    tab.assign(KW + (size_t)(l - kk) * fhs::kCrtVtabWords, 0);
+    std::memcpy(tab.data(), &K, sizeof(K));
+    for (int x = 0; x < l - kk; ++x) {
+        uint64_t* v = tab.data() + KW + (size_t)x * fhs::kCrtVtabWords;
+        const uint64_t q = c->q[kk + x];
+        const hu128 R = (~(hu128)0) / q;
+        v[0] = q;
+        v[1] = (uint64_t)R;
+        v[2] = (uint64_t)(R >> 64);
+        const uint64_t t64 = (uint64_t)((((hu128)1) << 64) % q);
+        uint64_t pw = 1 % q;
+        for (int w = 0; w < K.W; ++w) {
+            v[3 + w] = pw;
+            pw = h_mulmod(pw, t64, q);
+        }
+    }
+    return tab;
+}
 static fhs_status decode_coeffs_dev(fhs_context* c, const fhs_plaintext* pt, int k, int lv, std::vector<double>& m,
                                     bool* exact) {
     const size_t N = c->N, bytes = 8ull * lv * N;
@@ -2143,89 +2172,93 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
             vt_words += (size_t)(l - kks[i]) * fhs::kCrtVtabWords;
         }
     }
-    // aux: the scales (count doubles), every fast plaintext's vtab, then the count check flags
-    const size_t aux_words = (size_t)count + vt_words + ((size_t)count + 1) / 2;
-    HostTrace ht;
-    const size_t per_out = host_fft ? N : 2 * (size_t)nslots;   // doubles back per plaintext
-    const size_t dbl_b = 8 * N * count, spec_b = 16 * n * count, dout_b = 16 * (size_t)nslots * count;
-    uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr, *spec = nullptr, *dout = nullptr;
-    double* rb = nullptr;
-    std::vector<fhs::CrtConsts> Ks(count);
-    hipError_t e = readback_buf(c, 8 * per_out * count + 4 * (size_t)count, &rb);
-    if (e == hipSuccess && tmp_words) e = dalloc(c, &tmp, 8 * tmp_words);
-    if (e == hipSuccess) e = dalloc(c, &dbl, dbl_b);
-    if (e == hipSuccess) e = dalloc(c, &aux, 8 * aux_words);
-    if (e == hipSuccess) e = dalloc(c, &spec, spec_b);
-    if (e == hipSuccess) e = dalloc(c, &dout, dout_b);
-    unsigned* hflag = reinterpret_cast<unsigned*>(rb + per_out * count);
-    double* dscales = reinterpret_cast<double*>(aux);
-    unsigned* dflag = reinterpret_cast<unsigned*>(aux + count + vt_words);
-    std::vector<uint64_t> head((size_t)count + vt_words, 0);   // scales and vtabs: one staged copy
-    for (int i = 0; i < count; ++i) {
-        const double sc = scl(i);
-        std::memcpy(&head[i], &sc, 8);
-        hflag[i] = 0;
-    }
-    size_t vo = (size_t)count;
-    std::vector<size_t> vt_at(count, 0);
-    for (int i = 0; i < count; ++i) {
-        if (!fast[i]) continue;
-        const int kk = kks[i], nx = lv(i) - kk;
-        crt_consts(c, kk, Ks[i]);
-        vt_at[i] = vo;
-        for (int x = 0; x < nx; ++x, vo += fhs::kCrtVtabWords) {
-            uint64_t* v = head.data() + vo;
-            const uint64_t q = c->q[kk + x];
-            const hu128 R = (~(hu128)0) / q;
-            v[0] = q;
-            v[1] = (uint64_t)R;
-            v[2] = (uint64_t)(R >> 64);
-            const uint64_t t64 = (uint64_t)((((hu128)1) << 64) % q);
-            uint64_t pw = 1 % q;
-            for (int w = 0; w < Ks[i].W; ++w) {
-                v[3 + w] = pw;
-                pw = h_mulmod(pw, t64, q);
-            }
-        }
-    }
-    if (e == hipSuccess) e = stage_h2d(c, aux, head.data(), 8 * head.size());
-    if (e == hipSuccess) e = hipMemsetAsync(dflag, 0, 4 * (size_t)count, c->st);
-    // coefficient form: the fast plaintexts copied side by side; one INTT launch over all of them when
-    // they share a level (the usual client batch), else one per plaintext
-    int lf = -1, nf = 0;
-    bool one_l = true;
+    // aux (one staged copy up to the flags): the scales, every fast item's check table (vtab), its
+    // composition job (fhs::CrtJob), the ciphertext pointers (cts), the zeroed check flags, then the slots;
+    // flags and slots come back in one copy
+    constexpr size_t JW = sizeof(fhs::CrtJob) / 8;
+    static_assert(sizeof(fhs::CrtJob) % 8 == 0, "CrtJob packs into words");
+    int nf = 0, lf = -1, max_nx = 0;
+    bool one_l = true, one_nc = true;
     for (int i = 0; i < count; ++i) {
         if (!fast[i]) continue;
         one_l &= lf < 0 || lv(i) == lf;
+        one_nc &= !cts || cts[i]->ncomp == cts[0]->ncomp;
         lf = lv(i);
+        max_nx = std::max(max_nx, lv(i) - kks[i]);
         ++nf;
     }
-    size_t to = 0;
-    for (int i = 0; e == hipSuccess && i < count; ++i) {
-        if (!fast[i]) continue;
-        const int l = lv(i);
-        e = cts ? fhs::launch_decrypt(c->T, cts[i]->d, cts[i]->ncomp, sk->s, tmp + to, l, c->st)
-                : hipMemcpyAsync(tmp + to, pts[i]->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
-        if (e == hipSuccess && !one_l) e = fhs::launch_ntt_inv(c->T, tmp + to, l, l, 1, 0, c->st);
-        to += (size_t)l * N;
+    const size_t FW = ((size_t)count + 1) / 2, J0 = (size_t)count + vt_words, P0 = J0 + (size_t)nf * JW,
+                 A0 = P0 + (cts ? (size_t)count : 0);
+    const size_t slot_words = host_fft ? 0 : 2 * (size_t)nslots * count;
+    const size_t aux_words = A0 + FW + slot_words;
+    HostTrace ht;
+    const size_t per_out = host_fft ? N : 2 * (size_t)nslots;   // doubles back per item
+    const size_t dbl_b = 8 * N * count, spec_b = 16 * n * count;
+    uint64_t *tmp = nullptr, *dbl = nullptr, *aux = nullptr, *spec = nullptr;
+    double* rb = nullptr;
+    hipError_t e = readback_buf(c, 8 * (FW + per_out * count), &rb);
+    if (e == hipSuccess && tmp_words) e = dalloc(c, &tmp, 8 * tmp_words);
+    if (e == hipSuccess) e = dalloc(c, &dbl, dbl_b);
+    if (e == hipSuccess) e = dalloc(c, &aux, 8 * aux_words);
+    if (e == hipSuccess && !host_fft) e = dalloc(c, &spec, spec_b);
+    const unsigned* hflag = reinterpret_cast<const unsigned*>(rb);
+    double* rslots = rb + FW;
+    const double* dscales = reinterpret_cast<const double*>(aux);
+    unsigned* dflag = reinterpret_cast<unsigned*>(aux + A0);
+    uint64_t* dout = aux + A0 + FW;
+    std::vector<uint64_t> head(A0 + FW, 0);
+    for (int i = 0; i < count; ++i) {
+        const double sc = scl(i);
+        std::memcpy(&head[i], &sc, 8);
     }
-    if (e == hipSuccess && nf > 0 && one_l) e = fhs::launch_ntt_inv(c->T, tmp, lf, lf, nf, (size_t)lf * N, c->st);
-    to = 0;
-    for (int i = 0; e == hipSuccess && i < count; ++i) {
+    size_t vo = (size_t)count, jo = J0, to = 0;
+    for (int i = 0; i < count; ++i) {
         if (!fast[i]) continue;
         const int l = lv(i), kk = kks[i], nx = l - kk;
-        uint64_t* t = tmp + to;
-        e = fhs::launch_crt_compose(Ks[i], t, reinterpret_cast<double*>(dbl) + (size_t)i * N, (int)N, c->st,
-                                    t + (size_t)kk * N, nx, aux + vt_at[i], dflag + i);
+        const std::vector<uint64_t>& tab = crt_tables(c, kk, l);   // [CrtConsts][nx vtabs], cached per (kk, l)
+        fhs::CrtJob J{};
+        std::memcpy(&J.K, tab.data(), sizeof(fhs::CrtConsts));
+        std::memcpy(head.data() + vo, tab.data() + sizeof(fhs::CrtConsts) / 8, 8 * (size_t)nx * fhs::kCrtVtabWords);
+        J.limbs = tmp + to;
+        J.out = reinterpret_cast<double*>(dbl) + (size_t)i * N;
+        J.extra = tmp + to + (size_t)kk * N;
+        J.vtab = aux + vo;
+        J.flag = dflag + i;
+        J.nx = nx;
+        std::memcpy(head.data() + jo, &J, sizeof(J));
+        vo += (size_t)nx * fhs::kCrtVtabWords;
+        jo += JW;
         to += (size_t)l * N;
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(hflag, dflag, 4 * (size_t)count, hipMemcpyDeviceToHost, c->st);
-    // the slots of every plaintext (a slow one's are recomputed below)
+    if (cts)
+        for (int i = 0; i < count; ++i) head[P0 + i] = reinterpret_cast<uint64_t>(cts[i]->d);
+    if (e == hipSuccess) e = stage_h2d(c, aux, head.data(), 8 * head.size());
+    // coefficient form: the fast items side by side (decrypted there, or copied), one INTT launch over all
+    // of them when they share a level (the usual client batch), else one per item
+    if (cts && nf == count && one_l && one_nc) {
+        if (e == hipSuccess)
+            e = fhs::launch_decrypt_many(c->T, reinterpret_cast<const fhs::u64* const*>(aux + P0), count, cts[0]->ncomp,
+                                         sk->s, tmp, (size_t)lf * N, lf, c->st);
+    } else {
+        to = 0;
+        for (int i = 0; e == hipSuccess && i < count; ++i) {
+            if (!fast[i]) continue;
+            const int l = lv(i);
+            e = cts ? fhs::launch_decrypt(c->T, cts[i]->d, cts[i]->ncomp, sk->s, tmp + to, l, c->st)
+                    : hipMemcpyAsync(tmp + to, pts[i]->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
+            if (e == hipSuccess && !one_l) e = fhs::launch_ntt_inv(c->T, tmp + to, l, l, 1, 0, c->st);
+            to += (size_t)l * N;
+        }
+    }
+    if (e == hipSuccess && nf > 0 && one_l) e = fhs::launch_ntt_inv(c->T, tmp, lf, lf, nf, (size_t)lf * N, c->st);
+    if (e == hipSuccess && nf > 0)
+        e = fhs::launch_crt_compose_jobs(reinterpret_cast<const fhs::CrtJob*>(aux + J0), nf, max_nx, (int)N, c->st);
+    // the slots of every item (a slow one's are recomputed below), then flags + slots in one copy back
     if (e == hipSuccess && !host_fft)
         e = fhs::launch_decode_slots(c->T, reinterpret_cast<const double*>(dbl), dscales, count,
                                      reinterpret_cast<double*>(spec), nslots, reinterpret_cast<double*>(dout), c->st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(rb, host_fft ? (void*)dbl : (void*)dout, 8 * per_out * count, hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(rb, dflag, 8 * (FW + slot_words), hipMemcpyDeviceToHost, c->st);
+    if (e == hipSuccess && host_fft) e = hipMemcpyAsync(rslots, dbl, 8 * per_out * count, hipMemcpyDeviceToHost, c->st);
     ht.mark("decode: enqueue");
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);
     ht.mark("decode: gpu");
@@ -2242,7 +2275,7 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
             st = decode_compose(c, pts[i], pts[i]->l, m);   // exact: all limbs
         }
         if (st != FHS_OK) break;
-        double* slot = rb + (size_t)i * per_out;
+        double* slot = rslots + (size_t)i * per_out;
         if (host_fft) {
             std::copy(m.begin(), m.end(), slot);
             continue;
@@ -2259,12 +2292,11 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     for (int i = 0; st == FHS_OK && i < count; ++i) {
         double* out = re_im + (size_t)i * 2 * nslots;
         if (host_fft)
-            decode_slots(c, rb + (size_t)i * N, scl(i), (size_t)nslots, out);
+            decode_slots(c, rslots + (size_t)i * N, scl(i), (size_t)nslots, out);
         else
-            std::memcpy(out, rb + (size_t)i * per_out, 8 * per_out);
+            std::memcpy(out, rslots + (size_t)i * per_out, 8 * per_out);
     }
     ht.mark("decode: slots");
-    if (dout) dfree(c, dout, dout_b);
     if (spec) dfree(c, spec, spec_b);
     if (aux) dfree(c, aux, 8 * aux_words);
     if (dbl) dfree(c, dbl, dbl_b);

@@ -153,6 +153,9 @@ hipError_t launch_encode_coef(const DevTables& T, const double* vals, int count,
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
                                   const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st);
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);
+// `count` ciphertexts (device pointer array; each ncomp components at l limbs) decrypted to out + i out_stride
+hipError_t launch_decrypt_many(const DevTables& T, const u64* const* cts_dev, int count, int ncomp, const u64* s, u64* out,
+                               size_t out_stride, int l, hipStream_t st);
 hipError_t launch_diag_gather(const double* M1, const double* M2, int D, int G, int n, int k0, int rows, int trans,
                               double* out, hipStream_t st);
 // CKKS decode of `count` centred coefficient vectors (m: count x N doubles in HBM) to their first nslots
@@ -181,6 +184,17 @@ hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out,
                               const u64* extra = nullptr, int nx = 0, const u64* vtab = nullptr,
                               unsigned* flag = nullptr);
 constexpr int kCrtVtabWords = 3 + kCrtMaxL + 1;   // per extra limb in vtab
+// one composition of a batch (launch_crt_compose_jobs): the arguments of launch_crt_compose in HBM
+struct CrtJob {
+    CrtConsts K;
+    const u64* limbs;
+    double* out;
+    const u64* extra;
+    const u64* vtab;
+    unsigned* flag;
+    int nx, pad;
+};
+hipError_t launch_crt_compose_jobs(const CrtJob* jobs_dev, int count, int max_nx, int N, hipStream_t st);
 
 // per-limb constants for k_scalar (value mod q_i and its Shoup companion)
 constexpr int kMaxScalarLimbs = 64;

@@ -2049,6 +2049,31 @@ __global__ void k_decrypt(DevTables T, const u64* ct, int ncomp, const u64* s, u
         out[idx] = v;
     }
 }
+// ciphertext blockIdx.y of cts (device pointer array, all with ncomp components at l limbs) -> out + y out_stride
+__global__ void k_decrypt_many(DevTables T, const u64* const* cts, int ncomp, const u64* s, u64* out, size_t out_stride,
+                               int l) {
+    const int N = T.N;
+    const size_t S = (size_t)l * N;
+    const u64* ct = cts[blockIdx.y];
+    u64* o = out + blockIdx.y * out_stride;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const PrimeK& P = PK(T, (int)(idx / N));
+        const u64 sv = s[idx];
+        u64 v = ct[idx], sp = sv;
+        for (int k = 1; k < ncomp; ++k) {
+            v = addmod(v, mulmod(ct[k * S + idx], sp, P), P.q);
+            sp = mulmod(sp, sv, P);
+        }
+        o[idx] = v;
+    }
+}
+hipError_t launch_decrypt_many(const DevTables& T, const u64* const* cts_dev, int count, int ncomp, const u64* s, u64* out,
+                               size_t out_stride, int l, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    const int g1 = eltwise_grid((size_t)l * T.N) / count, gx = g1 > 0 ? g1 : 1;
+    hipLaunchKernelGGL(k_decrypt_many, dim3(gx, count), dim3(256), 0, st, T, cts_dev, ncomp, s, out, out_stride, l);
+    return hipGetLastError();
+}
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st) {
     hipLaunchKernelGGL(k_decrypt, dim3(eltwise_grid((size_t)l * T.N)), dim3(256), 0, st, T, ct, ncomp, s, out, l);
     return hipGetLastError();
@@ -2367,8 +2392,9 @@ hipError_t launch_encode_reduce(const DevTables& T, const double* coef, int coun
 
 // ============================================================================ decode: centred CRT
 constexpr int kCrtCheckPer = 4;   // extra limbs checked per grid row
-__global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double* __restrict__ out, int N,
-                              const u64* __restrict__ extra, int nx, const u64* __restrict__ vtab, unsigned* flag) {
+__device__ __forceinline__ void crt_compose_body(const CrtConsts& K, const u64* __restrict__ limbs, double* __restrict__ out,
+                                                 int N, const u64* __restrict__ extra, int nx,
+                                                 const u64* __restrict__ vtab, unsigned* flag) {
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
     if (n >= N) return;
     const int l = K.l, W = K.W;
@@ -2446,6 +2472,22 @@ __global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double
         bad |= r != extra[(size_t)e * N + n];
     }
     if (bad) atomicOr(flag, 1u);
+}
+__global__ void k_crt_compose(CrtConsts K, const u64* __restrict__ limbs, double* __restrict__ out, int N,
+                              const u64* __restrict__ extra, int nx, const u64* __restrict__ vtab, unsigned* flag) {
+    crt_compose_body(K, limbs, out, N, extra, nx, vtab, flag);
+}
+// a batch of compositions (one decode call's plaintexts): job blockIdx.z, its check rows up to its own nx
+__global__ void k_crt_compose_jobs(const CrtJob* __restrict__ jobs, int N) {
+    const CrtJob& J = jobs[blockIdx.z];
+    if (blockIdx.y > 0 && (int)blockIdx.y * kCrtCheckPer >= J.nx) return;
+    crt_compose_body(J.K, J.limbs, J.out, N, J.extra, J.nx, J.vtab, J.flag);
+}
+hipError_t launch_crt_compose_jobs(const CrtJob* jobs_dev, int count, int max_nx, int N, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    const int rows = max_nx > 0 ? (max_nx + kCrtCheckPer - 1) / kCrtCheckPer : 1;
+    hipLaunchKernelGGL(k_crt_compose_jobs, dim3((N + 255) / 256, rows, count), dim3(256), 0, st, jobs_dev, N);
+    return hipGetLastError();
 }
 hipError_t launch_crt_compose(const CrtConsts& K, const u64* limbs, double* out, int N, hipStream_t st, const u64* extra,
                               int nx, const u64* vtab, unsigned* flag) {
