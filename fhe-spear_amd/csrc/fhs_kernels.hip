@@ -126,6 +126,12 @@ __device__ __forceinline__ int galois_src(int e, u64 elt, int logN) {
     return (int)(__brev((unsigned)((e2 - 1) >> 1)) >> (32 - logN));
 }
 
+// The forward NTT may skip Harvey's conditional subtraction (RedU::lazy: q (4 + 2 log N) < 2^64).  Every
+// prime of a B59 context is below 2^59, so for N <= 16384 that holds for all of them: the kernels'
+// B59 instantiations drop the non-lazy code at compile time (same values -- lazy is true at run time too)
+template <int LOGN, bool B59>
+__device__ __forceinline__ bool lazy_of(const RedU& R) { return (B59 && LOGN <= 14) || R.lazy; }
+
 template <int LOGN>
 constexpr size_t lds_bytes() { return (size_t)((1 << LOGN) + (1 << LOGN) / 16) * 8; }
 
@@ -786,7 +792,7 @@ __device__ __forceinline__ void modup_convert3x(const u64* yb, const u64* xt, co
                                       // so any congruent 64-bit value will do (no final fold)
             x[k] = B59 ? convert3x_b59(V[0][k], V[1][k], V[2][k], e1, e2, c3, R.d, k < 2)
                        : convert3x_value(V[0][k], V[1][k], V[2][k], e1, e2, c3, R.b, R.d);
-        fwd_quad_first2<TH>(x, w4, m, R.lazy, lds, tid, ch, hi);
+        fwd_quad_first2<TH>(x, w4, m, lazy_of<LOGN, B59>(R), lds, tid, ch, hi);
     }
 }
 
@@ -919,14 +925,14 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
         __syncthreads();
         // the radix-4 conversion (modup_convert3x, FHS_MODUP_R4) did each half's local stage 0 already
         constexpr int S0 = DP == 3 ? 1 : 0;
-        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0>(lds, tid, tw, m, R.lazy, 1 + h);
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0>(lds, tid, tw, m, lazy_of<LOGN, B59>(R), 1 + h);
         // buffer stores: per-lane offset tid, the half / row offset in soffset.  The extended limbs feed only
         // the key inner products, whose split-30 sums take any value < 2^60: lazy outputs are folded once
         // (pm_fold_lt60), without fwd_canon's final subtraction.  The wave-uniform lazy choice is made once
         // per sweep, outside the unrolled loop, so its 16 LDS reads issue together (a choice per element
         // split the loop into blocks, each waiting for its own read)
         const __amdgpu_buffer_rsrc_t ro = brsrc(o, N * 8);
-        if (R.lazy) {
+        if (lazy_of<LOGN, B59>(R)) {
 #pragma unroll
             for (int c = 0; c < 16; ++c)
                 bstore64_aux<FHS_MODUP_STORE_AUX>(pm_fold_lt60(lds[row_pad<TH>(tid, c)], R), ro, tid * 8,
@@ -1231,7 +1237,7 @@ __device__ __forceinline__ void moddown_convert3x(const u64* y, const u64* xt, c
         for (int k = 0; k < 4; ++k)   // B59: upper half unfolded, as modup_convert3x
             x[k] = B59 ? convert3x_b59(v[0][k], v[1][k], v[2][k], e1, e2, 0, R.d, k < 2)
                        : convert3x_value(v[0][k], v[1][k], v[2][k], e1, e2, 0, R.b, R.d);
-        fwd_quad_first2<TH>(x, w4, R.q, R.lazy, lds, tid, ch, hi);
+        fwd_quad_first2<TH>(x, w4, R.q, lazy_of<LOGN, B59>(R), lds, tid, ch, hi);
     }
 }
 
@@ -1291,7 +1297,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             }
             if (T.ks_seal) x[z] = submod(csub(x[z], q), halfq, q);   // SEAL rounding: - floor(p/2) mod q_i
         }
-        fwd_quad_first2<TH>(x, w4, q, RU.lazy, lds, tid, ch, hi);
+        fwd_quad_first2<TH>(x, w4, q, lazy_of<LOGN, B59>(RU), lds, tid, ch, hi);
     }
     }
     const u64 pinv = T.md_pinv[2 * i], pinv_s = T.md_pinv[2 * i + 1];
@@ -1307,7 +1313,7 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
         }
         __syncthreads();
-        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, 1>(lds, tid, tw, q, RU.lazy, 1 + h);
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, 1>(lds, tid, tw, q, lazy_of<LOGN, B59>(RU), 1 + h);
         // outputs in batches of 4 whose accumulator (and rotated c0) loads are issued together, with
         // the add / no-add choice outside the loop (one latency per batch, not one per coefficient);
         // buffer loads / stores with the row offsets in soffset
