@@ -1,4 +1,5 @@
 set -o pipefail
+export FHESPEAR_PARITY_RNG=1   # deterministic encryption randomness: the digests are comparable across runs
 mkdir -p gpurun_out/r04y
 A="--N 32768 --L0 36 --P 3 --D 2048 --F 4096 --blocks 2"
 FFN_DIGEST=1 timeout -k 10 300 python tools/ffn_block.py $A > gpurun_out/r04y/ffn_world1.log 2>&1 &&
