@@ -57,10 +57,8 @@ def summarise(rows, steps):
     cuts = [i for i, (_, _, n) in enumerate(rows) if bare(n) == "k_bsgs_inner"]
     if len(cuts) < steps + 1:
         raise SystemExit(f"only {len(cuts)} k_bsgs_inner dispatches for {steps} timed steps")
-    # step s spans from the dispatch after the previous step's k_bsgs_inner's giant tail ... simplest exact
-    # cut: a step's kernels are those between consecutive k_bsgs_inner dispatches, shifted so the baby-step
-    # key switch (before k_bsgs_inner) belongs to its own step: step k = (cut[k-1], cut[k]] minus the giant
-    # tail of step k-1, i.e. [first dispatch after step k-1's rescale, cut[k]] + giant tail of step k.
+    # a step runs its baby-step key switch, then k_bsgs_inner, then its giant steps and the rescale: step k
+    # spans from the dispatch after the previous rescale to the first rescale after its k_bsgs_inner
     resc = [i for i, (_, _, n) in enumerate(rows) if family(n) == "rescale"]
     bounds = []
     for c in cuts[-steps:]:
