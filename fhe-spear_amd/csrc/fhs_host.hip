@@ -940,9 +940,12 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
     bool b59 = T.modup_dp == 3;
     for (int i = 0; i < K && b59; ++i) b59 = b59_prime(c->q[i]);
     T.conv_b59 = b59;
+    bool all59 = true;
+    for (int i = 0; i < K && all59; ++i) all59 = b59_prime(c->q[i]);
+    T.all_b59 = all59;
     // the B59 kernels compile the forward NTT's lazy mode in for N <= 16384 (fhs_kernels.hip lazy_of): every
     // prime must carry the lazy bit there, which q < 2^59 implies -- checked, not assumed
-    for (int i = 0; i < K && b59 && c->logN <= 14; ++i)
+    for (int i = 0; i < K && (b59 || all59) && c->logN <= 14; ++i)
         if (!((pk[i].pm >> 7) & 1))
             return fail(FHS_ERR_INVALID, "context: a 59-bit prime without the lazy NTT bound (internal)");
     HIPCHK(up(pk.data(), sizeof(PrimeK) * K, &T.primes), "tables");

@@ -43,6 +43,8 @@ struct DevTables {
     int max_qbits;            // bits of the largest prime (<= 59: split-30 high halves < 2^29, fewer folds)
     int md_xform;             // ModDown converts from the X form (P = 3 special primes < 2^59, modup_dp == 3)
     int conv_b59;             // every prime is 2^59 - d with d < 2^27: the X-form conversions use convert3x_b59
+    int all_b59;              // every prime is 2^59 - d with d < 2^27 (any digit shape): the one-limb-digit ModUp
+                              // and its ModDown take their B59 instantiations (compile-time lazy NTT, folded stores)
     int modup_dp;             // ModUp conversion compiled for this shape: 3 (P = 3, all targets pseudo-
                               // Mersenne with 2^60 mod m < 2^30: modup_convert3x only, at levels
                               // l % 3 == 0), 1 (P = 1:

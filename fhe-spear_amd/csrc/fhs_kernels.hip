@@ -970,7 +970,10 @@ static void launch_modup(const DevTables& T, const u64* const* uniq, const u64* 
     else if (modup_xform(T, l))   // every digit of this level full (3 limbs), X form (launch_centered)
         hipLaunchKernelGGL((k_modup_h<LOGN, 3, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else if (T.modup_dp == 1)
-        hipLaunchKernelGGL((k_modup_h<LOGN, 1, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+        if (T.all_b59)   // SEAL's 59-bit chains: compile-time lazy NTT and folded stores
+            hipLaunchKernelGGL((k_modup_h<LOGN, 1, true>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
+        else
+            hipLaunchKernelGGL((k_modup_h<LOGN, 1, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
     else
         hipLaunchKernelGGL((k_modup_h<LOGN, 0, false>), g, b, 0, st, T, uniq, acoef, vcnt, ext, l, U);
 }
@@ -1486,6 +1489,10 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
                 hipLaunchKernelGGL((k_moddown_h<LOGN, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc,
                                    ycoef, l, R);
             } else {
+                if (T.all_b59)
+                    hipLaunchKernelGGL((k_moddown_h<LOGN, false, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
+                                       it, acc, ycoef, l, R);
+                else
                 hipLaunchKernelGGL((k_moddown_h<LOGN, false>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it,
                                    acc, ycoef, l, R);
             }
