@@ -2129,24 +2129,57 @@ __global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64*
 // per vector: z_j is scattered to LDS slot rev(s_j) (bit-reversed input), a radix-2 DIT FFT runs in
 // LDS (f64), then each coefficient is scaled, rounded (half away from zero, as the host decoder's
 // inverse) and reduced exactly mod every limb's prime.  The NTT follows (k_ntt_fwd_ptrs).
-template <int LOGN>
-__device__ __forceinline__ void enc_fft_stages(double2* a, int tid, int TH, int n_pts, int log_pts, const double2* W,
-                                               int logh) {
-    // radix-2 DIT over n_pts = 2^log_pts points in LDS, bit-reversed in, natural out; twiddles of
-    // the full 2^logh-point transform (a sub-FFT uses the same ones)
-    for (int s = 0; s < log_pts; ++s) {
+// radix-2 DIT over n_pts = 2^log_pts points in LDS, bit-reversed in, natural out; twiddles of the full
+// 2^logh-point transform (a sub-FFT uses the same ones).  Stages go in pairs through registers (each
+// thread takes the quad i0, i0 + h, i0 + 2h, i0 + 3h and applies stage s then s + 1 to it -- the same
+// butterflies in the same order, half the LDS round trips and barriers); an odd last stage alone.
+// bf(x, y, w): x, y <- x + w y, x - w y.
+template <class BF>
+__device__ __forceinline__ void fft_dit_stages(double2* a, int tid, int TH, int n_pts, int log_pts, const double2* W,
+                                               int logh, BF bf) {
+    int s = 0;
+    for (; s + 1 < log_pts; s += 2) {
         const int half = 1 << s;
-        for (int b = tid; b < n_pts / 2; b += TH) {
-            const int k = b & (half - 1);
-            const int i = ((b >> s) << (s + 1)) + k, j = i + half;
+        for (int g = tid; g < n_pts / 4; g += TH) {
+            const int k = g & (half - 1);
+            const int i0 = ((g >> s) << (s + 2)) + k;
+            double2 x0 = a[i0], x1 = a[i0 + half], x2 = a[i0 + 2 * half], x3 = a[i0 + 3 * half];
             const double2 w = W[(size_t)k << (logh - 1 - s)];
-            const double2 x = a[i], y = a[j];
-            const double2 t = {y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x};
-            a[i] = double2{x.x + t.x, x.y + t.y};
-            a[j] = double2{x.x - t.x, x.y - t.y};
+            bf(x0, x1, w);
+            bf(x2, x3, w);
+            bf(x0, x2, W[(size_t)k << (logh - 2 - s)]);
+            bf(x1, x3, W[(size_t)(k + half) << (logh - 2 - s)]);
+            a[i0] = x0;
+            a[i0 + half] = x1;
+            a[i0 + 2 * half] = x2;
+            a[i0 + 3 * half] = x3;
         }
         __syncthreads();
     }
+    if (s < log_pts) {
+        const int half = 1 << s;
+        for (int b = tid; b < n_pts / 2; b += TH) {
+            const int k = b & (half - 1);
+            const int i = ((b >> s) << (s + 1)) + k;
+            double2 x = a[i], y = a[i + half];
+            bf(x, y, W[(size_t)k << (logh - 1 - s)]);
+            a[i] = x;
+            a[i + half] = y;
+        }
+        __syncthreads();
+    }
+}
+struct FftBfly {   // the encoder's butterfly (contraction as the compiler likes)
+    __device__ __forceinline__ void operator()(double2& x, double2& y, const double2 w) const {
+        const double2 t = {y.x * w.x - y.y * w.y, y.x * w.y + y.y * w.x};
+        y = double2{x.x - t.x, x.y - t.y};
+        x = double2{x.x + t.x, x.y + t.y};
+    }
+};
+template <int LOGN>
+__device__ __forceinline__ void enc_fft_stages(double2* a, int tid, int TH, int n_pts, int log_pts, const double2* W,
+                                               int logh) {
+    fft_dit_stages(a, tid, TH, n_pts, log_pts, W, logh, FftBfly{});
 }
 template <int LOGN>
 __device__ __forceinline__ void enc_finish(const DevTables& T, double2 v, int k, double scale, u64* out, int l,
@@ -2221,22 +2254,17 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
 // ---- decoder FFT (launch_decode_slots).  fp contraction is off throughout: the host decoder's
 // fft_inplace / decode_slots evaluate these products and sums unfused (x86-64 without FMA), and the GPU
 // must round the same way to give the same doubles.
+struct DecBfly {   // the host decoder's butterfly, unfused (decode_slots / fft_inplace round the same way)
+    __device__ __forceinline__ void operator()(double2& x, double2& y, const double2 w) const {
+#pragma clang fp contract(off)
+        const double vr = y.x * w.x - y.y * w.y, vi = y.x * w.y + y.y * w.x;
+        y = double2{x.x - vr, x.y - vi};
+        x = double2{x.x + vr, x.y + vi};
+    }
+};
 __device__ __forceinline__ void dec_fft_stages(double2* a, int tid, int TH, int n_pts, int log_pts, const double2* W,
                                                int logh) {
-#pragma clang fp contract(off)
-    for (int s = 0; s < log_pts; ++s) {   // DIT, bit-reversed in, natural out (fft_inplace's stage order)
-        const int half = 1 << s;
-        for (int b = tid; b < n_pts / 2; b += TH) {
-            const int k = b & (half - 1);
-            const int i = ((b >> s) << (s + 1)) + k, j = i + half;
-            const double2 w = W[(size_t)k << (logh - 1 - s)];
-            const double2 u = a[i], v = a[j];
-            const double vr = v.x * w.x - v.y * w.y, vi = v.x * w.y + v.y * w.x;
-            a[j] = double2{u.x - vr, u.y - vi};
-            a[i] = double2{u.x + vr, u.y + vi};
-        }
-        __syncthreads();
-    }
+    fft_dit_stages(a, tid, TH, n_pts, log_pts, W, logh, DecBfly{});
 }
 template <int LOGN>
 constexpr int dec_threads() {
