@@ -113,3 +113,10 @@ def test_bench_rejects_a_world_size_other_than_gpus():
                        text=True, timeout=120)
     assert r.returncode == 2
     assert "WORLD_SIZE=3" in r.stderr
+
+
+def test_gpu_scripts_parse():
+    """The GPU-box scripts (tools/gpu.sh and the rehearsal scripts) are at least valid bash."""
+    for f in sorted((REPO / "tools").glob("*.sh")) + sorted((REPO / "tools" / "debug").glob("*.sh")):
+        r = subprocess.run(["bash", "-n", str(f)], capture_output=True, text=True)
+        assert r.returncode == 0, (f.name, r.stderr)
