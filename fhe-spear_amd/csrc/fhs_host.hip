@@ -573,6 +573,16 @@ static size_t pt_bytes(const fhs_plaintext* pt) { return 8ull * pt->l * pt->ctx-
 static std::mutex g_ev_mu;
 static std::map<int, std::vector<hipEvent_t>> g_ev_free;
 static std::unordered_map<hipEvent_t, int> g_ev_dev;
+// events belong to the device current at creation: create on `dev`, whatever the calling thread has
+// current (one thread may drive contexts on two GPUs), and leave the caller's current device as it was
+static hipError_t ev_create_on(int dev, hipEvent_t* e) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) cur = -1;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return hipErrorInvalidDevice;
+    hipError_t r = hipEventCreate(e);
+    if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+    return r;
+}
 static hipEvent_t ev_get(int dev) {
     {
         std::lock_guard<std::mutex> lk(g_ev_mu);
@@ -584,7 +594,7 @@ static hipEvent_t ev_get(int dev) {
         }
     }
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (ev_create_on(dev, &e) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(g_ev_mu);
     g_ev_dev[e] = dev;
     return e;
@@ -608,7 +618,7 @@ static void ev_reserve(int dev, size_t n) {
     }
     for (size_t k = 0; k < n; ++k) {
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess) break;
+        if (ev_create_on(dev, &e) != hipSuccess) break;
         made.push_back(e);
     }
     std::lock_guard<std::mutex> lk(g_ev_mu);
@@ -1114,7 +1124,18 @@ static uint64_t stream_id(uint64_t kind, uint64_t a, uint64_t b) { return (kind 
 // counter starts at a fresh random offset and each public key's mask key has 256 fresh random bits
 // mixed in: a secret key recreated from the same 32 key bytes (another process, another context) never
 // repeats an encryption mask, which would reveal the difference of the two messages.
-static bool parity_rng() { return getenv("FHESPEAR_PARITY_RNG") != nullptr; }
+// Only the exact value "1" enables it (0, empty or anything else leaves the secure default), and the
+// first use in a process says so on stderr: ciphertexts made in this mode reuse mask streams across
+// processes and must never leave a test.
+static bool parity_rng() {
+    const char* v = getenv("FHESPEAR_PARITY_RNG");
+    if (!v || strcmp(v, "1") != 0) return false;
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+        fprintf(stderr, "[fhespear] FHESPEAR_PARITY_RNG=1: deterministic encryption randomness (parity tests "
+                        "only; never for real data)\n");
+    return true;
+}
 enum { ST_SECRET = 1, ST_PUBKEY = 2, ST_RELIN = 3, ST_GALOIS = 4, ST_ENC_SYM = 5, ST_ENC_ASYM = 6, ST_PK_RNG = 7 };
 
 // sample a small polynomial (ternary/CBD) over `limbs` primes and NTT it
@@ -1519,6 +1540,10 @@ struct BatchOutT {
     }
 };
 using BatchOut = BatchOutT<fhs_plaintext>;
+// Largest batch one launch takes (its item count is a grid dimension of the sampler, NTT, combine, decrypt
+// and CRT kernels, and its scratch is count x l x N words); bigger batches are processed in chunks of this
+// many items, with the same results as one call per item
+static constexpr int kMaxBatch = 4096;
 extern "C" fhs_status fhs_ciphertext_info(const fhs_ciphertext* ct, int* ncomp, int* ci, int* l, double* scale) {
     if (!ct) return fail(FHS_ERR_INVALID, "null ciphertext");
     if (ncomp) *ncomp = ct->ncomp;
@@ -2321,7 +2346,12 @@ extern "C" fhs_status fhs_decrypt_decode_batch(fhs_context* c, fhs_secret_key* s
     ENTER(c);
     if (!sk || !cts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > c->N / 2)
         return fail(FHS_ERR_INVALID, "decrypt_decode_batch: bad arguments");
-    return decode_many(c, nullptr, count, nslots, re_im, cts, sk);
+    for (int i0 = 0; i0 < count; i0 += kMaxBatch) {   // grid rows and scratch bound one launch
+        const fhs_status s = decode_many(c, nullptr, std::min(kMaxBatch, count - i0), nslots,
+                                         re_im + (size_t)i0 * 2 * nslots, cts + i0, sk);
+        if (s != FHS_OK) return s;
+    }
+    return FHS_OK;
 }
 // Client-side batch (the client-aided block decrypts 2-3 outputs per stage): decode_many over all of
 // them, one synchronisation, only the first `nslots` slots of each back to the host.
@@ -2330,7 +2360,12 @@ extern "C" fhs_status fhs_decode_batch(fhs_context* c, const fhs_plaintext* cons
     ENTER(c);
     if (!pts || !re_im || count < 0 || nslots < 1 || (size_t)nslots > c->N / 2)
         return fail(FHS_ERR_INVALID, "decode_batch: bad arguments");
-    return decode_many(c, pts, count, nslots, re_im);
+    for (int i0 = 0; i0 < count; i0 += kMaxBatch) {
+        const fhs_status s = decode_many(c, pts + i0, std::min(kMaxBatch, count - i0), nslots,
+                                         re_im + (size_t)i0 * 2 * nslots);
+        if (s != FHS_OK) return s;
+    }
+    return FHS_OK;
 }
 
 // ============================================================================ encryption
@@ -2399,16 +2434,27 @@ extern "C" fhs_status fhs_encrypt_symmetric_batch(fhs_context* c, fhs_secret_key
         if (!pts[i]) return fail(FHS_ERR_INVALID, "encrypt_batch: null plaintext");
     bool same = count > 0;
     for (int i = 1; i < count; ++i) same &= pts[i]->l == pts[0]->l && pts[i]->ci == pts[0]->ci;
-    if (!same) {   // mixed levels: one at a time (the same counters in the same order)
+    if (!same) {   // mixed levels: one at a time (the same counters in the same order); a failure destroys
+                   // the ciphertexts already made, as the batched path does
+        BatchOutT<fhs_ciphertext> bo(outs, count);
         for (int i = 0; i < count; ++i) {
             const fhs_status s = fhs_encrypt_symmetric(c, sk, pts[i], &outs[i]);
             if (s != FHS_OK) return s;
         }
-        return FHS_OK;
+        return bo.keep(FHS_OK);
     }
+    // chunks of kMaxBatch (grid rows and scratch bound the launch); counters stay consecutive, so the
+    // ciphertexts are those of one call per plaintext
+    BatchOutT<fhs_ciphertext> bo(outs, count);
     std::vector<double> scales(count);
     for (int i = 0; i < count; ++i) scales[i] = pts[i]->scale;
-    return encrypt_sym_core(c, sk, count, pts[0]->l, pts[0]->ci, scales.data(), pts, nullptr, outs);
+    for (int i0 = 0; i0 < count; i0 += kMaxBatch) {
+        const int n = std::min(kMaxBatch, count - i0);
+        const fhs_status s = encrypt_sym_core(c, sk, n, pts[0]->l, pts[0]->ci, scales.data() + i0, pts + i0, nullptr,
+                                              outs + i0);
+        if (s != FHS_OK) return s;
+    }
+    return bo.keep(FHS_OK);
 }
 // Extension (the client's encrypt_replicated of a stage's inputs, bg:53-58 / 124-127, in one pass):
 // encode `count` vectors of n values (real, or interleaved re/im) at `scale` and chain index ci and encrypt
@@ -2422,7 +2468,7 @@ extern "C" fhs_status fhs_encode_encrypt_symmetric_batch(fhs_context* c, fhs_sec
     fhs_status st = encode_checks(c, n, scale, ci);
     if (st != FHS_OK) return st;
     if (count == 0) return FHS_OK;
-    if (count > 4096) return fail(FHS_ERR_INVALID, "encode_encrypt: at most 4096 vectors per call");
+    if (count > (size_t)kMaxBatch) return fail(FHS_ERR_INVALID, "encode_encrypt: at most 4096 vectors per call");
     const size_t stride = is_real ? n : 2 * n, N = c->N;
     const int l = c->L0 + 1 - ci;
     uint64_t *dvals = nullptr, *coef = nullptr;

@@ -5,6 +5,8 @@
 #   tools/gpurun_wait.sh LOG TIMEOUT 'command'
 log=$1
 lim=$2
+case "$log" in -*) echo "gpurun_wait.sh: LOG must come first (got '$log')" >&2; exit 2;; esac
+case "$lim" in ''|*[!0-9]*) echo "gpurun_wait.sh: TIMEOUT must be a number of seconds (got '$lim')" >&2; exit 2;; esac
 shift 2
 for i in $(seq 1 12); do
     /usr/local/graft/bin/gpurun --timeout "$lim" -- "$@" > "$log" 2>&1
