@@ -47,7 +47,7 @@ CONFIGS = {
     # ModUp per rotation (the default line runs it as its seal_mode leg; --config cfg2seal profiles it)
     "cfg2seal": dict(N=16384, L0=36, P=1, D=2048, mode="seal", digest="cfg2_seal",
                      workload="BSGS matvec d=2048 N=16384 L0=36 P=1, SEAL switch_key_inplace convention "
-                              "(89 non-hoisted rotations)"),
+                              "(89 rotations; the 45 baby steps share one decomposition, corrected to SEAL's)"),
     # BASELINE configs[0] shape (CPU-runnable case in the reference)
     "cfg1": dict(N=8192, L0=24, P=3, D=1024, workload="BSGS matvec d=1024 N=8192 L0=24 P=3 (62 rotations)"),
     "small": dict(N=4096, L0=6, P=3, D=256, workload="BSGS matvec d=256 N=4096 L0=6 P=3 (smoke size)"),
@@ -75,21 +75,23 @@ def bsgs_params(D):
 def algorithmic_bytes_per_matvec(name, cfg, l):
     """Unique HBM bytes kernel `name` must move for one matvec.  Rotations of one
     input share one ModUp (hoisting): the G-1 baby rotations have one input, each of the B-1
-    giant rotations its own, so a matvec runs B ModUps for its G-1 + B-1 key-switches.  In SEAL's
-    convention (cfg mode "seal") nothing is hoisted: one ModUp per rotation."""
+    giant rotations its own, so a matvec runs B ModUps for its G-1 + B-1 key-switches.  SEAL's
+    convention (cfg mode "seal") hoists the baby rotations too (round 5, SealHoist): their key products
+    also read one correction [2][E][N] per rotation."""
     N, P, D = cfg["N"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
     E, dn = l + P, (l + P - 1) // P
     w = 8 * N
     rot = (G - 1) + (B - 1)
-    modups = rot if cfg.get("mode") == "seal" else 1 + (B - 1)
+    modups = 1 + (B - 1)
+    corr = (G - 1) * 2 * E if cfg.get("mode") == "seal" else 0
     if name == "k_bsgs_inner":   # diagonals + baby steps in, B inner products out
         return w * (D * l + 2 * G * l + 2 * B * l)
     if name == "k_modup":        # digit limbs (coefficient form) in, extended limbs out
         return w * modups * (l + dn * E)
     if name == "k_ks_ip":        # extended limbs per distinct input + key b halves per rotation in (the a_j are
         # regenerated from their seeds, fhs_host.hip key_words), accumulators out
-        return w * (modups * dn * E + rot * (dn * E + 2 * E))
+        return w * (modups * dn * E + rot * (dn * E + 2 * E) + corr)
     return None
 
 
@@ -607,8 +609,12 @@ def seal_leg(args, ph, cfg):
         roof["selection"] = rule
     mvb = matvec_bytes(scfg, l)
     value = 1000.0 / med
+    hoisted, fallback = ctx.seal_hoist_stats()
     res = {"value": round(value, 3), "unit": "matvec/s", "median_ms_per_step": round(med, 3),
-           "steps": args.seal_steps, "P": 1, "dnum": L0, "hoisting": False, "workload": scfg["workload"],
+           "steps": args.seal_steps, "P": 1, "dnum": L0,
+           "hoisting": {"baby_steps": "one decomposition, per-key correction (SealHoist)" if hoisted else False,
+                        "flushes_hoisted": hoisted, "flushes_fallback": fallback},
+           "workload": scfg["workload"],
            "parity": limb_digest_check("cfg2", y.to_numpy(), "_seal"),
            "roofline": roof,
            "matvec_roofline": {"bound": "hbm", "bytes_per_matvec": mvb, "achieved": round(mvb * value / 1e9, 1),

@@ -352,6 +352,11 @@ struct fhs_context {
     size_t readback_bytes = 0;
     // grow-only scratch buffers reused across calls (stream order makes reuse safe): a large
     // allocation costs host time per GB
+    // SEAL-convention hoisting (fhs_kernels.h SealHoist): the per-(key, level) corrections [2][l+P][N],
+    // the zero flag (device word + pinned host word) and the counts of hoisted / fallback flushes
+    std::map<std::pair<const uint64_t*, int>, uint64_t*> seal_corr;
+    size_t seal_corr_bytes = 0;
+    fhs::SealHoist seal_hoist{};
     enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_ENC_PTRS, SCR_COUNT };
     uint64_t* scr[SCR_COUNT] = {};
     size_t scr_bytes[SCR_COUNT] = {};
@@ -428,7 +433,9 @@ static const uint64_t* key_akey(const fhs_context* c, const uint64_t* key) {
     auto it = c->key_a.find(key);
     return it == c->key_a.end() ? nullptr : it->second;
 }
+static void drop_seal_corr(fhs_context* c, const uint64_t* key);
 static void free_key(fhs_context* c, uint64_t* key) {
+    drop_seal_corr(c, key);
     auto it = c->key_a.find(key);
     if (it != c->key_a.end()) {
         dfree(c, it->second, 8ull * c->dnum * c->K * c->N);
@@ -684,6 +691,73 @@ static hipError_t stage_h2d(void* user, void* dst, const void* src, size_t bytes
     return hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, c->st);
 }
 
+// ---------------------------------------------------------------- SEAL-convention hoisting
+// FHESPEAR_SEAL_HOIST=0 keeps SEAL's per-rotation decomposition for every flush (A/B and test knob)
+static bool seal_hoist_enabled() {
+    const char* v = getenv("FHESPEAR_SEAL_HOIST");
+    return !v || strcmp(v, "0") != 0;
+}
+static size_t seal_corr_bytes(const fhs_context* c, int l) { return 8ull * 2 * (l + c->P) * c->N; }
+// the corrections of `key` (null: of every key), returned to the block cache in stream order
+static void drop_seal_corr(fhs_context* c, const uint64_t* key) {
+    for (auto it = c->seal_corr.begin(); it != c->seal_corr.end();) {
+        if (key && it->first.first != key) { ++it; continue; }
+        dfree(c, it->second, seal_corr_bytes(c, it->first.second));
+        c->seal_corr_bytes -= seal_corr_bytes(c, it->first.second);
+        it = c->seal_corr.erase(it);
+    }
+}
+// The correction of every rotated item of a flush (computed once per (key, level) and kept with the key),
+// and the zero-flag buffers.  Bounded: past FHESPEAR_SEAL_CORR_BYTES (default 1/16 of HBM) the cache is
+// emptied before this flush's corrections are made (a chain walks down the levels; the corrections of the
+// levels behind it go cold).
+static hipError_t seal_prepare(fhs_context* c, std::vector<KsItem>& items, int l) {
+    fhs::SealHoist& sh = c->seal_hoist;
+    hipError_t e = hipSuccess;
+    if (!sh.zflag_dev) {
+        uint64_t* z = nullptr;
+        e = dalloc(c, &z, 8);
+        if (e != hipSuccess) return e;
+        sh.zflag_dev = reinterpret_cast<unsigned*>(z);
+    }
+    if (!sh.zflag_host) {
+        void* h = nullptr;
+        e = hipHostMalloc(&h, 64, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        sh.zflag_host = static_cast<unsigned*>(h);
+    }
+    static const size_t cap = [] {
+        const char* v = getenv("FHESPEAR_SEAL_CORR_BYTES");
+        if (v) return (size_t)strtoull(v, nullptr, 10);
+        size_t fr = 0, tot = 0;
+        return hipMemGetInfo(&fr, &tot) == hipSuccess ? tot / 16 : (size_t)16 << 30;
+    }();
+    size_t need = 0;
+    for (const KsItem& it : items)
+        if (it.elt != 1 && !c->seal_corr.count({it.key, l})) need += seal_corr_bytes(c, l);
+    if (need && c->seal_corr_bytes + need > cap) drop_seal_corr(c, nullptr);
+    uint64_t* mask = nullptr;
+    for (KsItem& it : items) {
+        if (it.elt == 1) continue;
+        auto f = c->seal_corr.find({it.key, l});
+        if (f == c->seal_corr.end()) {
+            if (!mask && (e = dalloc(c, &mask, 8ull * c->K * c->N)) != hipSuccess) break;
+            uint64_t* corr = nullptr;
+            if ((e = dalloc(c, &corr, seal_corr_bytes(c, l))) != hipSuccess) break;
+            e = fhs::launch_seal_corr(c->T, it.key, it.akey, it.elt, l, mask, corr, c->st);
+            if (e != hipSuccess) {
+                dfree(c, corr, seal_corr_bytes(c, l));
+                break;
+            }
+            f = c->seal_corr.emplace(std::make_pair(it.key, l), corr).first;
+            c->seal_corr_bytes += seal_corr_bytes(c, l);
+        }
+        it.corr = f->second;
+    }
+    if (mask) dfree(c, mask, 8ull * c->K * c->N);
+    return e;
+}
+
 // ---------------------------------------------------------------- deferred rotations
 static fhs_status flush(fhs_context* c) {
     if (c->pending.empty()) return FHS_OK;
@@ -705,8 +779,19 @@ static fhs_status flush(fhs_context* c) {
     hipError_t e = scratch(c, fhs_context::SCR_KS, wsb, &ws);
     ht.mark("flush: workspace");
     if (e != hipSuccess) return hip_fail(e, "key-switch workspace");
+    fhs::SealHoist* sh = nullptr;
+    if (c->T.ks_seal && U < R && seal_hoist_enabled()) {   // SEAL convention: one ModUp per shared input
+        e = seal_prepare(c, items, l);
+        if (e == hipSuccess) sh = &c->seal_hoist;
+        else if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+            for (auto& it : items) it.corr = nullptr;   // no room for the corrections: per-rotation path
+            e = hipSuccess;
+        }
+        ht.mark("flush: seal corrections");
+        if (e != hipSuccess) return hip_fail(e, "seal corrections");
+    }
     e = fhs::launch_keyswitch(c->T, items.data(), R, reinterpret_cast<const fhs::u64* const*>(uniq.data()), U, l, ws,
-                              wsb, c->items_dev, c->stager, c->st, c->timer_mask ? &c->ktimer : nullptr);
+                              wsb, c->items_dev, c->stager, c->st, c->timer_mask ? &c->ktimer : nullptr, sh);
     ht.mark("flush: launch keyswitch");
     c->pending.clear();
     c->pending_refs.clear();
@@ -1048,6 +1133,10 @@ static void ctx_free(fhs_context* c) {
         hipStreamSynchronize(c->st);
         ctx_sync(c);
         for (void* p : c->tables) hipFree(p);
+        for (auto& kv : c->seal_corr) hipFree(kv.second);
+        c->seal_corr.clear();
+        if (c->seal_hoist.zflag_dev) hipFree(c->seal_hoist.zflag_dev);
+        if (c->seal_hoist.zflag_host) hipHostFree(c->seal_hoist.zflag_host);
         for (int k = 0; k < fhs_context::SCR_COUNT; ++k)
             if (c->scr[k]) hipFree(c->scr[k]);
         {
@@ -1427,6 +1516,14 @@ extern "C" fhs_status fhs_context_set_key_switch_mode(fhs_context* c, int mode) 
     if (mode == FHS_KS_SEAL && c->P != 1)
         return fail(FHS_ERR_INVALID, "key switch mode seal: SEAL's switch_key_inplace has one special prime (P = 1)");
     c->T.ks_seal = mode == FHS_KS_SEAL;
+    drop_seal_corr(c, nullptr);
+    return FHS_OK;
+}
+extern "C" fhs_status fhs_seal_hoist_stats(fhs_context* c, uint64_t* hoisted, uint64_t* fallback) {
+    ENTER(c);
+    if (!hoisted || !fallback) return fail(FHS_ERR_INVALID, "null argument");
+    *hoisted = c->seal_hoist.hoisted;
+    *fallback = c->seal_hoist.fallback;
     return FHS_OK;
 }
 extern "C" fhs_status fhs_context_key_switch_mode(const fhs_context* c, int* mode) {

@@ -78,7 +78,27 @@ struct KsItem {
     u64 elt;             // galois element (1 = identity)
     u64 src;             // index of `a` in the distinct-input list
     const u64* akey;     // imported key: its a_j [dnum][K][N] (null: a_j regenerated from the seeds)
+    const u64* corr;     // SEAL convention, hoisted: the item's correction [2][l+P][N] (launch_seal_corr),
+                         // added to the key inner product before ModDown; null otherwise
 };
+
+// SEAL-convention hoisting (round 5).  SEAL lifts each data limb of the *automorphed* ciphertext without
+// centring, so its extension of sigma(a) differs from sigma applied to the extension of a exactly at the
+// coefficients sigma negates: there the lift of -y is q_j - y instead of -y (mod p_t), a difference of
+// q_j whenever y != 0.  Summed through the key product that is one data-independent term per (Galois
+// element, level): corr_c[t] = NTT_t(mask_sigma) . sum_{j != t} (q_j mod p_t) key_j[c][t], so one ModUp
+// of `a` serves every rotation of it, limb for limb equal to SEAL's per-rotation decomposition -- unless a
+// digit coefficient is exactly 0 (SEAL lifts 0, not q_j): k_centered flags any zero coefficient, the
+// host reads the flag and falls back to the per-rotation decomposition.
+struct SealHoist {
+    unsigned* zflag_dev;    // set by k_centered when a digit coefficient of an input is 0
+    unsigned* zflag_host;   // pinned host word the flag is copied to
+    unsigned long long hoisted = 0, fallback = 0;   // flushes taken each way
+};
+// corr ([2][l+P][N]) of the switching key `key` (akey: explicit a_j, or null) for Galois element elt at
+// level l; mask_scratch holds K x N words
+hipError_t launch_seal_corr(const DevTables& T, const u64* key, const u64* akey, u64 elt, int l, u64* mask_scratch,
+                            u64* out, hipStream_t st);
 
 // Optional per-kernel event timer (bench.py): rec(ctx, id, begin, stream) is called around launches.
 enum KernelId { KID_BSGS_INNER = 0, KID_MODUP = 1, KID_KS_IP = 2, KID_MODDOWN = 3, KID_KS_INTT = 4, KID_SPECIAL_INTT = 5,
@@ -107,9 +127,12 @@ struct Stager {
     hipError_t (*h2d)(void* user, void* dst, const void* src, size_t bytes);
 };
 // items_host[r].src must index uniq_host (U distinct inputs); items_dev holds >= R items + U pointers
+// SEAL convention (T.ks_seal): with `sh` non-null and every rotated item carrying its `corr`, inputs shared by
+// several items are decomposed once (hoisted, one stream synchronisation to read the zero flag); otherwise
+// every item's automorphed input is decomposed on its own
 hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, const u64* const* uniq_host, int U,
                             int l, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
-                            const KTimer* tm);
+                            const KTimer* tm, SealHoist* sh = nullptr);
 size_t keyswitch_workspace_bytes(const DevTables& T, int R, int U, int l);
 
 // Hadamard + giant steps of the fused BSGS (fhs_kernels.hip launch_bsgs), enqueued on `st`.

@@ -622,7 +622,7 @@ __device__ __noinline__ int centered_exact(const u64* y, const u64* qs, int ns, 
 
 // (a2) v[u][j][n] = round(sum_{u in digit j} y_u / q_u): fixed-point fast path (error < 2 ns ulp
 // of 2^-64), exact fallback within 64 ulp of a half (oracle: ock_centered_count).
-__global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, int l, int U) {
+__global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, int l, int U, unsigned* zflag) {
     // grid (N / 256, U dn): the (input, digit) pair is per workgroup, so no 64-bit index division
     const int N = T.N, P_ = T.P, dn = (l + P_ - 1) / P_;
     const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -634,7 +634,9 @@ __global__ void k_centered(DevTables T, const u64* acoef, unsigned char* vout, i
         const u64* yb = acoef + ((size_t)u * l + s0) * N + n;
         int v;
         if (ns == 1) {   // SEAL: the limb's residue in [0, q) is lifted as is
-            v = T.ks_seal ? 0 : (yb[0] > (PK(T, s0).q >> 1) ? 1 : 0);
+            const u64 y0 = yb[0];
+            v = T.ks_seal ? 0 : (y0 > (PK(T, s0).q >> 1) ? 1 : 0);
+            if (zflag && y0 == 0) atomicOr(zflag, 1u);   // hoisted SEAL rotations: SealHoist
         } else {
             // fixed-point fast path in registers (a guarded unrolled loop: no private arrays, so no
             // scratch traffic); the exact path re-reads the digit into its own arrays
@@ -690,12 +692,13 @@ __global__ void k_centered_x(DevTables T, u64* acoef, int l, int U) {
     yb[2 * (size_t)N] = w[2];
 }
 
-static void launch_centered(const DevTables& T, u64* acoef, unsigned char* vout, int l, int U, hipStream_t st) {
+static void launch_centered(const DevTables& T, u64* acoef, unsigned char* vout, int l, int U, hipStream_t st,
+                            unsigned* zflag = nullptr) {
     const int dn = (l + T.P - 1) / T.P;
     if (modup_xform(T, l))
         hipLaunchKernelGGL(k_centered_x, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, l, U);
     else
-        hipLaunchKernelGGL(k_centered, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, vout, l, U);
+        hipLaunchKernelGGL(k_centered, dim3((T.N + 255) / 256, U * dn), dim3(256), 0, st, T, acoef, vout, l, U, zflag);
 }
 
 // (b1) ModUp + NTT: ext[u][j][t] = NTT_t(centred conv_{digit j -> t}(y_u)) for t outside digit
@@ -1067,8 +1070,13 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
         ks_digits<true>(o, seeds, cx, RD, qb, dn, c0, c1);
     else
         ks_digits<false>(o, seeds, cx, RD, qb, dn, c0, c1);
-    acc[(((size_t)r * 2 + 0) * E + t) * N + n] = reduce128(c0.lo, c0.hi, RD);
-    acc[(((size_t)r * 2 + 1) * E + t) * N + n] = reduce128(c1.lo, c1.hi, RD);
+    u64 v0 = reduce128(c0.lo, c0.hi, RD), v1 = reduce128(c1.lo, c1.hi, RD);
+    if (it.corr) {   // hoisted SEAL convention: the item's correction (SealHoist)
+        v0 = addmod(v0, it.corr[(size_t)t * N + n], RD.q);
+        v1 = addmod(v1, it.corr[((size_t)E + t) * N + n], RD.q);
+    }
+    acc[(((size_t)r * 2 + 0) * E + t) * N + n] = v0;
+    acc[(((size_t)r * 2 + 1) * E + t) * N + n] = v1;
 }
 
 // Giant steps, limbs t < l: the key inner products of all R rotations summed in place, already
@@ -1099,6 +1107,10 @@ __global__ void __launch_bounds__(256) k_ks_ip_sum(DevTables T, const KsItem* it
             ks_digits<false>(o, seeds, cx, RD, qb, dn, c0, c1);
         s0 = addmod(s0, reduce128(c0.lo, c0.hi, RD), q);
         s1 = addmod(s1, reduce128(c1.lo, c1.hi, RD), q);
+        if (it.corr) {   // hoisted SEAL convention (SealHoist)
+            s0 = addmod(s0, it.corr[(size_t)t * N + n], q);
+            s1 = addmod(s1, it.corr[((size_t)E + t) * N + n], q);
+        }
         sadd = addmod(sadd, bload64(brsrc(it.add0 + (size_t)t * N, (uint32_t)N * 8), o.sn8, 0), q);
     }
     const u64 pinv = T.md_pinv[2 * t], pinv_s = T.md_pinv[2 * t + 1];
@@ -1391,6 +1403,7 @@ static void seal_rewrite(const DevTables& T, KsItem* items, int R, const u64** u
             if (it.add0) it.add0 = pc;
             it.elt = 1;
         }
+        it.corr = nullptr;   // the automorphed input is decomposed itself: nothing to correct
         uniq[r] = it.a;
         it.src = (u64)r;
     }
@@ -1408,6 +1421,21 @@ static hipError_t seal_permute(const DevTables& T, const KsItem* orig, int R, in
     return hipSuccess;
 }
 
+// key-switch workspace carve: acoef | ext | acc | ycoef | centred counts (ks_core_bytes)
+struct KsBufs {
+    u64 *acoef, *ext, *acc, *ycoef;
+    unsigned char* vcnt;
+};
+static KsBufs ks_carve(const DevTables& T, u64* ws, int R, int U, int l) {
+    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
+    KsBufs b;
+    b.acoef = ws;
+    b.ext = b.acoef + (size_t)U * l * N;
+    b.acc = b.ext + (size_t)U * dn * E * N;
+    b.ycoef = b.acc + (size_t)R * 2 * E * N;
+    b.vcnt = reinterpret_cast<unsigned char*>(b.ycoef + (size_t)R * 2 * T.P * N);
+    return b;
+}
 // INTT + centred ModUp per distinct input, then key inner product and special-limb INTT per item;
 // leaves acc [R][2][E][N] and ycoef [R][2][P][N]
 template <int LOGN>
@@ -1441,6 +1469,35 @@ static void ks_front(const DevTables& T, const KsItem* it, const u64* const* uni
     *ycoef_out = ycoef;
 }
 
+// ModDown of the R accumulators (acc, ycoef from ks_front) into the items' outputs
+template <int LOGN>
+static hipError_t launch_moddown(const DevTables& T, const KsItem* it, u64* acc, u64* ycoef, int l, int R, hipStream_t st,
+                                 const KTimer* tm) {
+    FHS_TMARK(tm, KID_MODDOWN, 1, st);
+    if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
+        if (T.md_xform) {   // the special digit to its X form, then the two-product conversion
+            hipLaunchKernelGGL(k_special_x, dim3((T.N + 255) / 256, 2 * R), dim3(256), 0, st, T, ycoef, 2 * R);
+            if (T.conv_b59)
+                hipLaunchKernelGGL((k_moddown_h<LOGN, true, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
+                                   it, acc, ycoef, l, R);
+            else
+                hipLaunchKernelGGL((k_moddown_h<LOGN, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc,
+                                   ycoef, l, R);
+        } else {
+            if (T.all_b59)
+                hipLaunchKernelGGL((k_moddown_h<LOGN, false, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
+                                   it, acc, ycoef, l, R);
+            else
+                hipLaunchKernelGGL((k_moddown_h<LOGN, false>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it,
+                                   acc, ycoef, l, R);
+        }
+    } else {
+        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
+    }
+    FHS_TMARK(tm, KID_MODDOWN, 0, st);
+    return hipGetLastError();
+}
+
 static hipError_t upload_items(const KsItem* items, int R, const u64* const* uniq, int U, void* dev, const Stager& sg,
                                const KsItem** it_dev, const u64* const** uniq_dev) {
     // one staged copy: [R items][U pointers]
@@ -1454,14 +1511,109 @@ static hipError_t upload_items(const KsItem* items, int R, const u64* const* uni
     return e;
 }
 
+// ---- SEAL-convention hoisting (fhs_kernels.h SealHoist)
+// mask_sigma in coefficient form, replicated over the K primes: coefficient i of a moves to i elt mod 2N,
+// negated when that lands in [N, 2N) -- mask[k] = 1 exactly where sigma(a)[k] = -a_i
+__global__ void k_seal_mask(DevTables T, u64 elt, u64* out) {
+    const int N = T.N, i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const u64 j = ((u64)i * elt) & (2 * (u64)N - 1);
+    const u64 v = j >> T.logN;
+    const size_t k = j & (N - 1);
+    for (int t = 0; t < T.K; ++t) out[(size_t)t * N + k] = v;
+}
+// corr_c[t][n] = M_t[n] sum_{j < l, j != t} (q_j mod p_t) key_j[c][t][n], M_t = NTT_t(mask_sigma), t over the
+// level's data limbs then the special primes (one-limb digits: P = 1 in SEAL's convention); key_j[1] is
+// a_j, regenerated from the seeds as the key inner product does, or read from an imported key
+__global__ void __launch_bounds__(256) k_seal_corr(DevTables T, const u64* key, const u64* akey, const u64* M,
+                                                    int l, u64* out) {
+    const int N = T.N, K = T.K, E = l + T.P;
+    const int n = blockIdx.x * blockDim.x + threadIdx.x, t = blockIdx.y;
+    if (n >= N || t >= E) return;
+    const int pt = t < l ? t : T.L0 + (t - l);
+    const RedU RD = redu(PK(T, pt));
+    const u64 p = RD.q;
+    const unsigned qb = 64 - __clzll(p);
+    const u64* seeds = key + (size_t)T.dnum * K * N;
+    const u64 cx = seeded_ctr_mix(pt, n);
+    u128 s0 = {0, 0}, s1 = {0, 0};
+    for (int j = 0; j < l; ++j) {
+        if (j == t) continue;   // the digit's own limb is not lifted (k_ks_ip reads the input itself)
+        const u64 qj = reduce128(PK(T, j).q, 0, RD);
+        const size_t kx = ((size_t)j * K + pt) * N + n;
+        const u64 a = akey ? akey[kx] : seeded_uniform_x(seeds[j] + cx, p, qb);
+        mac128(s0, key[kx], qj);
+        mac128(s1, a, qj);
+        if ((j & 7) == 7) {   // < 2^120 per product: fold every 8
+            s0 = u128{reduce128(s0.lo, s0.hi, RD), 0};
+            s1 = u128{reduce128(s1.lo, s1.hi, RD), 0};
+        }
+    }
+    const u64 m = M[(size_t)pt * N + n];
+    const u64 r0 = reduce128(s0.lo, s0.hi, RD), r1 = reduce128(s1.lo, s1.hi, RD);
+    out[(size_t)t * N + n] = reduce128(r0 * m, __umul64hi(r0, m), RD);
+    out[((size_t)E + t) * N + n] = reduce128(r1 * m, __umul64hi(r1, m), RD);
+}
+hipError_t launch_seal_corr(const DevTables& T, const u64* key, const u64* akey, u64 elt, int l, u64* mask_scratch,
+                            u64* out, hipStream_t st) {
+    if (T.P != 1 || l < 1 || l > T.L0 || !key || !out || !mask_scratch) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_seal_mask, dim3((T.N + 255) / 256), dim3(256), 0, st, T, elt, mask_scratch);
+    hipError_t e = launch_ntt_fwd(T, mask_scratch, T.K, T.L0, 1, 0, st);   // limb t at prime t: l_split = L0
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seal_corr, dim3((T.N + 255) / 256, l + T.P), dim3(256), 0, st, T, key, akey, mask_scratch,
+                       l, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R, const u64* const* uniq_host, int U,
                             int l, u64* ws, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
-                            const KTimer* tm) {
+                            const KTimer* tm, SealHoist* sh) {
     if (keyswitch_workspace_bytes(T, R, U, l) > ws_bytes) return hipErrorInvalidValue;
     const KsItem* it;
     const u64* const* uq;
     std::vector<KsItem> sitems;
     std::vector<const u64*> suniq;
+    // SEAL convention: hoist only when some input is shared (U < R) and every rotated item has its correction
+    bool hoist = T.ks_seal && sh && U < R;
+    for (int r = 0; hoist && r < R; ++r) hoist = items_host[r].elt == 1 || items_host[r].corr;
+    if (hoist) {
+        hipError_t e = upload_items(items_host, R, uniq_host, U, items_dev, sg, &it, &uq);
+        if (e == hipSuccess) e = hipMemsetAsync(sh->zflag_dev, 0, sizeof(unsigned), st);
+        if (e != hipSuccess) return e;
+        const KsBufs b = ks_carve(T, ws, R, U, l);
+        FHS_DISPATCH_LOGN(T.logN, {
+            FHS_TMARK(tm, KID_KS_INTT, 1, st);
+            if (ks_intt_half<LOGN>(l * U))
+                hipLaunchKernelGGL((k_ks_intt_h<LOGN>), dim3(l * U), dim3((1 << LOGN) / 32), 0, st, T, uq, b.acoef, l, U);
+            else
+                hipLaunchKernelGGL((k_ks_intt<LOGN>), dim3(l * U), dim3((1 << LOGN) / 16), 0, st, T, uq, b.acoef, l, U);
+            launch_centered(T, b.acoef, b.vcnt, l, U, st, sh->zflag_dev);
+            FHS_TMARK(tm, KID_KS_INTT, 0, st);
+        });
+        e = hipMemcpyAsync(sh->zflag_host, sh->zflag_dev, sizeof(unsigned), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        if (*(volatile unsigned*)sh->zflag_host) {   // a zero digit coefficient: SEAL's own per-rotation path
+            ++sh->fallback;
+            return launch_keyswitch(T, items_host, R, uniq_host, U, l, ws, ws_bytes, items_dev, sg, st, tm, nullptr);
+        }
+        ++sh->hoisted;
+        FHS_DISPATCH_LOGN(T.logN, {
+            FHS_TMARK(tm, KID_MODUP, 1, st);
+            launch_modup<LOGN>(T, uq, b.acoef, b.vcnt, b.ext, l, U, st);
+            FHS_TMARK(tm, KID_MODUP, 0, st);
+            FHS_TMARK(tm, KID_KS_IP, 1, st);
+            hipLaunchKernelGGL(k_ks_ip, dim3(xcd_grid(l + T.P, R * (int)(T.N >> 8))), dim3(256), 0, st, T, it, uq, b.ext,
+                               b.acc, l, R, 0);
+            FHS_TMARK(tm, KID_KS_IP, 0, st);
+            FHS_TMARK(tm, KID_SPECIAL_INTT, 1, st);
+            FHS_NTT_LAUNCH(k_ks_special_intt, T.P * 2 * R, dim3(T.P, 2, R), st, T, b.acc, b.ycoef, l, R);
+            FHS_TMARK(tm, KID_SPECIAL_INTT, 0, st);
+            e = launch_moddown<LOGN>(T, it, b.acc, b.ycoef, l, R, st, tm);
+        });
+        if (e != hipSuccess) return e;
+        return hipGetLastError();
+    }
     if (T.ks_seal) {
         sitems.assign(items_host, items_host + R);
         suniq.resize(R);
@@ -1475,31 +1627,13 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
     }
     hipError_t e = upload_items(items_host, R, uniq_host, U, items_dev, sg, &it, &uq);
     if (e != hipSuccess) return e;
+    hipError_t me = hipSuccess;
     FHS_DISPATCH_LOGN(T.logN, {
         u64 *acc, *ycoef;
         ks_front<LOGN>(T, it, uq, R, U, l, ws, st, tm, &acc, &ycoef);
-        FHS_TMARK(tm, KID_MODDOWN, 1, st);
-        if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
-            if (T.md_xform) {   // the special digit to its X form, then the two-product conversion
-                hipLaunchKernelGGL(k_special_x, dim3((T.N + 255) / 256, 2 * R), dim3(256), 0, st, T, ycoef, 2 * R);
-                if (T.conv_b59)
-                    hipLaunchKernelGGL((k_moddown_h<LOGN, true, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
-                                       it, acc, ycoef, l, R);
-                else
-                hipLaunchKernelGGL((k_moddown_h<LOGN, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it, acc,
-                                   ycoef, l, R);
-            } else {
-                if (T.all_b59)
-                    hipLaunchKernelGGL((k_moddown_h<LOGN, false, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
-                                       it, acc, ycoef, l, R);
-                else
-                hipLaunchKernelGGL((k_moddown_h<LOGN, false>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T, it,
-                                   acc, ycoef, l, R);
-            }
-        } else
-        hipLaunchKernelGGL((k_moddown<LOGN>), dim3(l * 2 * R), dim3((1 << LOGN) / 16), 0, st, T, it, acc, ycoef, l, R);
-        FHS_TMARK(tm, KID_MODDOWN, 0, st);
+        me = launch_moddown<LOGN>(T, it, acc, ycoef, l, R, st, tm);
     });
+    if (me != hipSuccess) return me;
     return hipGetLastError();
 }
 
@@ -1707,20 +1841,6 @@ __global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_giant_final(DevTab
 }
 
 // ---- key-switch stages of the BSGS giant steps
-struct KsBufs {
-    u64 *acoef, *ext, *acc, *ycoef;
-    unsigned char* vcnt;
-};
-static KsBufs ks_carve(const DevTables& T, u64* ws, int R, int U, int l) {
-    const size_t N = T.N, E = l + T.P, dn = (l + T.P - 1) / T.P;
-    KsBufs b;
-    b.acoef = ws;
-    b.ext = b.acoef + (size_t)U * l * N;
-    b.acc = b.ext + (size_t)U * dn * E * N;
-    b.ycoef = b.acc + (size_t)R * 2 * E * N;
-    b.vcnt = reinterpret_cast<unsigned char*>(b.ycoef + (size_t)R * 2 * T.P * N);
-    return b;
-}
 template <int LOGN>
 static void ks_modup_stage(const DevTables& T, const u64* const* uniq, int U, int l, const KsBufs& b, hipStream_t st,
                            const KTimer* tm) {

@@ -107,6 +107,7 @@ _SIGS = {
     "fhs_secret_key_import": (C.c_int, [_vp, _u64p, C.POINTER(_vp)]),
     "fhs_context_set_key_switch_mode": (C.c_int, [_vp, C.c_int]),
     "fhs_context_key_switch_mode": (C.c_int, [_vp, _ip]),
+    "fhs_seal_hoist_stats": (C.c_int, [_vp, _u64p, _u64p]),
     "fhs_public_key_export": (C.c_int, [_vp, _vp, _u64p]),
     "fhs_galois_keys_bytes": (C.c_int, [_vp, _u64p]),
     "fhs_ciphertext_destroy": (C.c_int, [_vp]),
@@ -368,7 +369,8 @@ class context:
         """Key-switch convention (extension): 'exact' (default: exact centred ModUp,
         ModDown without rounding -- rotations of one input share a ModUp) or 'seal' (special_modulus_size
         1 only: SEAL's switch_key_inplace -- per-limb lift without centring, automorphism before the
-        decomposition, ModDown rounded -- no hoisting)."""
+        decomposition, ModDown rounded; batched rotations of one input still share one decomposition,
+        corrected to SEAL's limbs per Galois key -- see seal_hoist_stats)."""
         modes = {"exact": 0, "seal": 1}
         if mode not in modes:
             raise ValueError("key switch mode: 'exact' or 'seal'")
@@ -378,6 +380,13 @@ class context:
         v = C.c_int()
         _check(_lib.fhs_context_key_switch_mode(self._h, C.byref(v)), "key_switch_mode")
         return ("exact", "seal")[v.value]
+
+    def seal_hoist_stats(self):
+        """(hoisted, fallback): key-switch flushes in the SEAL convention that shared one decomposition per
+        input, and those that fell back to SEAL's per-rotation decomposition (a digit coefficient was 0)."""
+        h, f = C.c_uint64(), C.c_uint64()
+        _check(_lib.fhs_seal_hoist_stats(self._h, C.byref(h), C.byref(f)), "seal_hoist_stats")
+        return int(h.value), int(f.value)
 
     def galois_elts(self):
         """The Galois elements keys are made for (the params' set, or the SEAL/Phantom default

@@ -104,6 +104,10 @@ fhs_status fhs_secret_key_import(fhs_context* ctx, const uint64_t* host /* [L0+P
 #define FHS_KS_SEAL 1
 fhs_status fhs_context_set_key_switch_mode(fhs_context* ctx, int mode);
 fhs_status fhs_context_key_switch_mode(const fhs_context* ctx, int* mode);
+/* SEAL convention: batched rotations of one ciphertext share one decomposition (the same limbs as SEAL's
+ * per-rotation decomposition via a per-(Galois key, level) correction); a digit coefficient
+ * equal to 0 falls back to the per-rotation path.  Counts of flushes taken each way. */
+fhs_status fhs_seal_hoist_stats(fhs_context* ctx, uint64_t* hoisted, uint64_t* fallback);
 fhs_status fhs_public_key_export(fhs_context* ctx, const fhs_public_key* pk, uint64_t* host /* [2][L0][N] */);
 fhs_status fhs_galois_keys_bytes(const fhs_galois_keys* gk, uint64_t* bytes);
 

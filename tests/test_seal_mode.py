@@ -11,8 +11,9 @@ The context's key_switch_mode('seal') selects it (oracle: Oracle.set_key_switch_
 (galois_keys_from_numpy, relin_key_from_numpy, secret_key_from_numpy) express "identical keys".
 
 Pinned here: the oracle's SEAL mode against a direct Python transcription of the published algorithm
-(CPU); the GPU in SEAL mode bit-exact against the oracle for rotations (single and batched: each one
-decomposed on its own), relinearize and the fused BSGS; imported keys reproduce the exporting
+(CPU); the GPU in SEAL mode bit-exact against the oracle for rotations (single, and batched: one
+decomposition shared by the rotations of an input, corrected per Galois key to SEAL's per-rotation
+lift -- or SEAL's own per-rotation path when a digit coefficient is 0), relinearize and the fused BSGS; imported keys reproduce the exporting
 context's rotations.  Parity against SEAL itself stays unpinned: SEAL/TenSEAL are not importable here
 (SURVEY.md §8c), and SEAL's rotation group generator is 3 where the reference (bg:24) and Phantom use 5."""
 import numpy as np
@@ -123,9 +124,18 @@ def test_gpu_seal_mode_bit_exact_vs_oracle(ph, orc, N, L0):
     ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(rng.normal(0, 0.1, D), N // 2 // D), 2.0 ** 40))
     c_np = ct.to_numpy()
     okeys = {e: o.gen_galois_key(33, s, e) for e in elts}
+    h0 = ctx.seal_hoist_stats()
     baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
     for b in range(1, G):
         assert np.array_equal(baby[b].to_numpy(), o.rotate(c_np, okeys[ph.get_elt_from_step(b, N)], b)), f"rotation {b}"
+    h1 = ctx.seal_hoist_stats()
+    assert h1[0] == h0[0] + 1 and h1[1] == h0[1], "the batch of rotations of one input took the hoisted path"
+    # a lower level: the corrections are per (key, level)
+    low = ph.mod_switch_to_next(ctx, ct)
+    lows = [ph.rotate(ctx, low, b, gk) for b in (1, 2, 3)]
+    for b, r in zip((1, 2, 3), lows):
+        assert np.array_equal(r.to_numpy(), o.rotate(low.to_numpy(), okeys[ph.get_elt_from_step(b, N)], b))
+    assert ctx.seal_hoist_stats()[0] == h1[0] + 1
     sq = ph.multiply(ctx, ct, ct)
     got = ph.relinearize(ctx, sq, rk).to_numpy()
     assert np.array_equal(got, o.relinearize(sq.to_numpy(), o.gen_relin_key(33, s)))
@@ -134,6 +144,49 @@ def test_gpu_seal_mode_bit_exact_vs_oracle(ph, orc, N, L0):
     want = o.bsgs_loop([b_.to_numpy() for b_ in baby], [p.to_numpy() for p in pts],
                        [None] + [okeys[ph.get_elt_from_step(g * G, N)] for g in range(1, B)], G, B, D)
     assert np.array_equal(y.to_numpy(), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,L0", [(1024, 4), (8192, 24)])
+def test_gpu_seal_hoisting_with_a_zero_digit_coefficient(ph, orc, N, L0):
+    """SEAL lifts the automorphed digit without centring: at a coefficient sigma negates, -y lifts to
+    q_j - y, which the hoisted path's correction reproduces only for y != 0.  A ciphertext whose digit has
+    coefficient 0 at a position the first rotation negates (and, in a second digit, one it does not)
+    must take SEAL's per-rotation path and still match the oracle limb for limb; the same rotations of
+    an unmodified ciphertext take the hoisted path."""
+    bits = [59] * L0 + [60]
+    steps = [1, 2, 3, 7]
+    elts = sorted(set(ph.get_elts_from_steps(steps, N)))
+    ctx = _gpu_ctx(ph, N, bits, 1, elts)
+    ctx.set_key_switch_mode("seal")
+    primes = [int(q) for q in ctx.primes]
+    o = orc.Oracle(N, primes, 1)
+    o.set_key_switch_mode("seal")
+    sk = ph.secret_key(ctx, seed=71)
+    gk = sk.create_galois_keys(ctx)
+    s = o.gen_secret(71)
+    okeys = {e: o.gen_galois_key(71, s, e) for e in elts}
+    enc = ph.ckks_encoder(ctx)
+    x = np.random.default_rng(8).normal(0, 0.1, N // 2)
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, x, 2.0 ** 40))
+    c = ct.to_numpy().copy()
+    l = c.shape[1]
+    e1 = ph.get_elt_from_step(1, N)
+    neg = [i for i in range(N) if (i * e1) % (2 * N) >= N]
+    pos = [i for i in range(N) if (i * e1) % (2 * N) < N]
+    for limb, i in ((0, neg[5]), (l - 1, neg[-3]), (1, pos[7])):
+        coef = np.array(o.intt(c[1, limb], limb), dtype=np.uint64)
+        coef[i] = 0
+        c[1, limb] = o.ntt(coef, limb)
+    bad = ph.ciphertext_from_numpy(ctx, c, ct.chain_index(), ct.scale())
+    for src, path in ((bad, 1), (ct, 0)):
+        h0 = ctx.seal_hoist_stats()
+        rots = ph.hoisting(ctx, src, gk, steps)
+        s_np = src.to_numpy()
+        for st, r in zip(steps, rots):
+            assert np.array_equal(r.to_numpy(), o.rotate(s_np, okeys[ph.get_elt_from_step(st, N)], st)), st
+        h1 = ctx.seal_hoist_stats()
+        assert h1[path] == h0[path] + 1 and h1[1 - path] == h0[1 - path]
 
 
 @pytest.mark.gpu
@@ -171,6 +224,9 @@ def test_gpu_imported_keys_reproduce_rotations(ph, orc, mode):
         r = ph.rotate(ctx, ct, st, gk)
         assert np.array_equal(r.to_numpy(), o.rotate(c_np, okeys[ph.get_elt_from_step(st, N)], st))
         assert np.max(np.abs(np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, r))) - np.roll(x, -st))) < 1e-6
+    # the same rotations batched (one decomposition; in SEAL mode the corrections from the imported a_j)
+    for st, r in zip(steps, ph.hoisting(ctx, ct, gk, steps)):
+        assert np.array_equal(r.to_numpy(), o.rotate(c_np, okeys[ph.get_elt_from_step(st, N)], st))
     sq = ph.multiply(ctx, ct, ct)
     assert np.array_equal(ph.relinearize(ctx, sq, rk).to_numpy(), o.relinearize(sq.to_numpy(), o.gen_relin_key(1234, s)))
     assert np.array_equal(gk.export(elts[0]), okeys[elts[0]])
