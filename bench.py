@@ -63,6 +63,12 @@ CONFIGS = {
                                                                   "L0=6 P=3 (test size)"),
 }
 SK_SEED, INPUT_SEED, DIAG_SEED = 1000, 10000, 2   # tests/golden/make_bench_digest.py
+# BASELINE configs[4] (tf:233-298): the FFN chain at N=32768, L0=36, P=3, d=2048, F=4096; 12 blocks reach the
+# first bootstrap (before block 11) -- the 24-block run is 2 x this with 4 bootstraps (tests/test_full_size.py)
+CFG5 = dict(N=32768, L0=36, P=3, D=2048, F=4096,
+            workload="fully encrypted FFN chain (tf:26-118, 233-298) d=2048 F=4096 N=32768 L0=36 P=3, bootstrap when "
+                     "< 4 levels remain")
+CFG5_BLOCKS = 12
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md chip table)
 BFLY_PEAK_GOPS = 1466.6        # measured lazy NTT butterflies/s, registers only (tools/microbench/bfly.hip)
 
@@ -232,6 +238,9 @@ def main():
                          "mode, each projection's giant steps sharded over a rank group as with --split)")
     ap.add_argument("--split", action="store_true",
                     help="cfg3 over N GPUs: latency mode, giant steps of each projection sharded over a rank group")
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the cfg5 leg (FFN chain at N=32768 with a bootstrap)")
+    ap.add_argument("--cfg5-blocks", type=int, default=CFG5_BLOCKS,
+                    help="FFN blocks of the cfg5 leg (12 include one bootstrap)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -261,9 +270,19 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import pyPhantom as ph
+    import fhespear_dist
+
+    # every data-path exchange logged per kind (RCCL broadcast / gather / reduce / reduce-scatter / send-recv:
+    # calls, bytes, event-timed ms), and every rank's device gathered to rank 0
+    tdist = fhespear_dist.TimedDist(dist) if dist is not None else None
+    ident = fhespear_dist.device_identity(ph, local)
+    idents = fhespear_dist.gather_identities(dist, ident) if dist is not None else [ident]
+    ranks_rec = {"world_size": dist.get_world_size() if dist is not None else 1,
+                 "backend": dist.get_backend() if dist is not None else None, "devices": idents,
+                 "distinct_devices": len({d.get("pci_bus_id") for d in idents}) == len(idents)}
 
     if args.config == "cfg3":
-        return bench_block(args, ph, dist, rank, world, local)
+        return bench_block(args, ph, tdist, rank, world, local)
     cfg = CONFIGS[args.config]
     N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
@@ -294,7 +313,6 @@ def main():
         import torch
         out_words = 2 * (L0 - 1) * N
         gather_buf = torch.empty(out_words, dtype=torch.int64, device=f"cuda:{local}")
-        import fhespear_dist
 
     gathered = [None]
     SYNC_GATHER = os.environ.get("FHESPEAR_BENCH_SYNC_GATHER") == "1"
@@ -305,17 +323,17 @@ def main():
         if dist is not None:     # cfg4: output ciphertexts to rank 0 over RCCL (xGMI)
             if dist.get_backend() == "gloo":   # rehearsal: host-staged
                 ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
-                gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf.cpu(), world, rank)
+                gathered[0] = fhespear_dist.gather_to_root(tdist, gather_buf.cpu(), world, rank)
             elif SYNC_GATHER:   # round 1-3 ordering (A/B knob): host waits for the step, then for the gather
                 torch.cuda.current_stream().synchronize()
                 ph.ciphertext_copy_to_device(ctx, y, gather_buf.data_ptr())
-                gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
+                gathered[0] = fhespear_dist.gather_to_root(tdist, gather_buf, world, rank)
             else:
                 # device-side ordering only (fhespear_dist.to_buffer): the copy waits on the library stream
                 # for torch's pending work on the buffer (the previous step's gather), RCCL's gather waits for
                 # the copy -- the host never blocks, so it enqueues the next step while this one runs
                 fhespear_dist.to_buffer(ph, ctx, y, gather_buf)
-                gathered[0] = fhespear_dist.gather_to_root(dist, gather_buf, world, rank)
+                gathered[0] = fhespear_dist.gather_to_root(tdist, gather_buf, world, rank)
         return y
 
     for _ in range(args.warmup):
@@ -352,6 +370,8 @@ def main():
     ph.kernel_timer_arm(ctx, sorted({dom, "k_modup", "k_bsgs_inner"}))
     barrier()
     ctx.synchronize()
+    if tdist is not None:
+        tdist.start()
     t0 = time.perf_counter()
     evs = []
     for _ in range(args.steps):
@@ -361,6 +381,10 @@ def main():
     ctx.synchronize()
     barrier()
     t1 = time.perf_counter()
+    exchange = None
+    if tdist is not None:
+        tdist.stop()
+        exchange = tdist.summary(per=args.steps)
     # per-step device time on the library stream (HIP events; the host enqueues ahead, so these
     # bracket the GPU work of each step): the value is quoted on their median
     step_ms = sorted(a.elapsed_ms(b) for a, b in evs)
@@ -402,12 +426,14 @@ def main():
         dist.all_reduce(tm, op=dist.ReduceOp.MAX)
         median_ms = float(tm.item())
     seal = None
+    released = False   # the matvec leg's objects, freed before the next leg allocates
     if world == 1 and args.config == "cfg2" and not args.no_seal:
         # north_star's bit-exact claim is stated against SEAL's switch_key_inplace convention: the same
         # matvec in that mode (P = 1, dnum = L0, every rotation decomposed on its own, no hoisting)
         del pts, ct, y, gk, sk, pt_x
         ctx.synchronize()
         del ctx
+        released = True
         try:
             seal = seal_leg(args, ph, cfg)
         except Exception as e:   # reported, never hidden
@@ -416,15 +442,36 @@ def main():
     if not args.no_block and args.config == "cfg2":
         # the metric's second half, measured: one client-aided RWKV-7 block (cfg3 shapes) on the same
         # ranks, after this configuration's memory is released
-        if seal is None:
+        if not released:
             del pts, ct, y, gk, sk, pt_x
             ctx.synchronize()
             del ctx
+            released = True
         try:
-            block = run_block(args, ph, dist, rank, world, local, args.block_steps, 1,
+            block = run_block(args, ph, tdist, rank, world, local, args.block_steps, 1,
                               capture=world == 1 and not args.no_cpu_baseline)
         except Exception as e:   # reported, never hidden: the matvec line stands on its own
             block = {"error": f"{type(e).__name__}: {e}"[:400]}
+        if world > 1:
+            # north_star: "baby-step rotations are computed once and broadcast" -- the FFN key pair's shared
+            # baby steps in that mode too (the line above recomputes them on each owning rank)
+            try:
+                bb = run_block(args, ph, tdist, rank, world, local, args.block_steps, 1, baby_mode="broadcast")
+            except Exception as e:   # reported, never hidden
+                bb = {"error": f"{type(e).__name__}: {e}"[:400]}
+            if rank == 0 and isinstance(block, dict):
+                block["baby_broadcast"] = bb
+    cfg5 = None
+    if not args.no_cfg5 and args.config == "cfg2":
+        if not released:
+            del pts, ct, y, gk, sk, pt_x
+            ctx.synchronize()
+            del ctx
+            released = True
+        try:
+            cfg5 = run_cfg5(args, ph, tdist, rank, world, local)
+        except Exception as e:   # reported, never hidden
+            cfg5 = {"error": f"{type(e).__name__}: {e}"[:400]}
     if rank == 0:
         total = args.steps * world
         mean_value = total / elapsed
@@ -505,6 +552,9 @@ def main():
             # reference's stage dependencies (r,k,v -> o -> FFN key -> FFN value) and is the latency figure
             "sec_per_8proj_independent": round(8.0 / value, 6),
             "rwkv_block": block,
+            "cfg5_chain": cfg5,
+            "ranks": ranks_rec,
+            "exchange_per_step": exchange,
             # the same matvec in SEAL's key-switch convention (P = 1, non-hoisted): the convention of
             # north_star's bit-exact claim; `value` above is the default exact-centred hoisted P = 3 mode
             "seal_mode_value": seal.get("value") if seal else None,
@@ -628,7 +678,7 @@ def seal_leg(args, ph, cfg):
     return res
 
 
-def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, config="cfg3"):
+def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, config="cfg3", baby_mode="recompute"):
     """One client-aided RWKV-7 block (cfg3 shapes, tools/rwkv_block.py = bg:756-899) on these ranks:
     8 BSGS projections in 4 dependent stages, pre-encoded diagonals resident, stage projections
     dealt over the ranks.  Returns rank 0's {sec_per_block (median), ...} (None elsewhere).
@@ -647,7 +697,7 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, 
     # rank groups unless --block-dealt
     split = getattr(args, "split", False) or (world > 1 and not getattr(args, "block_dealt", False)
                                               and args.config == "cfg2")
-    run = rb.BlockRunner(srv, blk, True, dist, rank, world, split=split)
+    run = rb.BlockRunner(srv, blk, True, dist, rank, world, split=split, baby_mode=baby_mode)
     x = rng.standard_normal(D)
     st = (x, np.zeros(D), np.zeros(D), np.zeros((H, 64, 64)), rng.standard_normal(D))
 
@@ -660,6 +710,8 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, 
 
     for _ in range(warmup):
         out = rb.client_aided_block(run, *st)
+    if hasattr(dist, "start"):
+        dist.start()
     secs, stage = [], {}
     for _ in range(steps):
         barrier()
@@ -669,6 +721,10 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, 
         secs.append(time.perf_counter() - t0)
         for k, v in out[5].items():
             stage[k] = stage.get(k, 0.0) + v
+    exchange = None
+    if hasattr(dist, "start"):
+        dist.stop()
+        exchange = dist.summary(per=steps)
     sec = float(np.median(secs))
     if dist is not None:
         import torch
@@ -702,13 +758,62 @@ def run_block(args, ph, dist, rank, world, local, steps, warmup, capture=False, 
                "server_ms": round(1e3 * sum(v for k, v in stage.items() if k.startswith("server_")) / steps, 2),
                "client_ms": round(1e3 * sum(v for k, v in stage.items() if k.startswith("client_")) / steps, 2),
                "max_abs_err_vs_plaintext_block": err,
-               "workload": cfg["workload"], "n_gpus": world,
+               "workload": cfg["workload"], "n_gpus": world, "baby_mode": run.baby_mode,
+               "exchange_per_block_rank0": exchange,
                "parallelism": (f"giant-step-split projections x{world}" if split
                                else f"stage-dealt projections x{world}") + (" + RCCL broadcast/gather" if world > 1 else "")}
         if cap is not None:
             res["_capture"] = cap
     del run, srv
     return res
+
+
+def run_cfg5(args, ph, dist, rank, world, local):
+    """BASELINE configs[4] on these ranks (tf:233-298): the fully encrypted FFN chain at N=32768, L0=36, P=3,
+    d=2048, F=4096 -- `--cfg5-blocks` blocks (12: the first bootstrap comes before block 11), fresh random
+    weights per block re-encoded at the ciphertext's level as tf does (tf:48, 76).  Over N ranks
+    (tools/ffn_block.py FfnRanks): each block's F/D key chunks and value chunks dealt to rank groups, each
+    chunk's giant groups sharded inside its group, the bootstrap's CoeffToSlot / SlotToCoeff giant groups over
+    every rank.  Reports per-block and bootstrap seconds (device-synchronised, barrier-bracketed, max over
+    ranks), the exchange per block, and the final ciphertext's limb digest against the committed one-rank
+    digest (tests/golden/manifest.json gpu_chain_digests: FfnRanks is limb-identical to the one-rank chain)."""
+    sys.path.insert(0, str(REPO / "tools"))
+    import ffn_block
+    c = CFG5
+    if hasattr(dist, "start"):
+        dist.start()
+    r = ffn_block.chain_over_ranks(ph, c["N"], c["L0"], c["P"], c["D"], c["F"], args.cfg5_blocks, True, dist, rank,
+                                   world, f"cuda:{local}")
+    exchange = None
+    if hasattr(dist, "start"):
+        dist.stop()
+        exchange = dist.summary(per=max(1, len(r["block_seconds"])))
+    blk = np.asarray(r["block_seconds"])
+    boot = np.asarray(r["bootstrap_seconds"] or [0.0])
+    if dist is not None:
+        import torch
+        tt = torch.tensor(np.concatenate([blk, boot]), dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        v = tt.cpu().numpy()
+        blk, boot = v[:len(blk)], v[len(blk):]
+    if rank != 0:
+        return None
+    man = json.loads((REPO / "tests" / "golden" / "manifest.json").read_text()).get("gpu_chain_digests", {})
+    key = f"cfg5_{args.cfg5_blocks}blk"
+    want = man.get(key, {}).get("sha256")
+    return {"workload": c["workload"], "n_gpus": world, "blocks": len(blk),
+            "sec_per_block_median": round(float(np.median(blk)), 4), "sec_per_block_mean": round(float(np.mean(blk)), 4),
+            "block_seconds": [round(float(v), 4) for v in blk],
+            "bootstraps": len(r["bootstrap_seconds"]),
+            "bootstrap_seconds": [round(float(v), 4) for v in boot] if r["bootstrap_seconds"] else [],
+            "setup_s": round(r["setup_s"], 2), "chain_index": r["chain_index"],
+            "max_err_vs_plaintext": max(r["max_err"]), "exchange_per_block_rank0": exchange,
+            "parallelism": (f"FfnRanks x{world}: chunks dealt to rank groups, giant groups sharded, bootstrap linear "
+                            f"transforms sharded" if world > 1 else "one rank"),
+            "parity": {"ct_sha256": r["ct_sha256"], "one_rank_sha256": want,
+                       "matches_one_rank": (r["ct_sha256"] == want) if want else None,
+                       "source": f"tests/golden/manifest.json gpu_chain_digests.{key} (one-rank GPU run of the same "
+                                 "seeds; the FFN encodes with the float64 GPU encoder, so the digest is the GPU's own)"}}
 
 
 def bench_block(args, ph, dist, rank, world, local):

@@ -78,6 +78,12 @@ extern "C" int fhs_device_count(void) {
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
 }
+extern "C" fhs_status fhs_device_pci_bus_id(int device, char* buf, int len) {
+    if (!buf || len < 13) return fail(FHS_ERR_INVALID, "device_pci_bus_id: buffer of at least 13 bytes");
+    hipError_t e = hipDeviceGetPCIBusId(buf, len, device);
+    if (e != hipSuccess) return hip_fail(e, "device_pci_bus_id");
+    return FHS_OK;
+}
 
 // ============================================================================ host number theory
 static inline uint64_t h_mulmod(uint64_t a, uint64_t b, uint64_t q) { return (uint64_t)(((hu128)a * b) % q); }

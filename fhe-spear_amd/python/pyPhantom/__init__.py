@@ -82,6 +82,7 @@ _SIGS = {
     "fhs_last_error": (C.c_char_p, []),
     "fhs_version": (C.c_char_p, []),
     "fhs_device_count": (C.c_int, []),
+    "fhs_device_pci_bus_id": (C.c_int, [C.c_int, C.c_char_p, C.c_int]),
     "fhs_create_coeff_modulus": (C.c_int, [_u64, _ip, C.c_int, _u64p]),
     "fhs_galois_elt_from_step": (_u64, [C.c_int, _u64]),
     "fhs_context_create": (C.c_int, [_u64, _u64p, C.c_int, C.c_int, _u64p, C.c_int, C.c_int, C.POINTER(_vp)]),
@@ -1161,6 +1162,13 @@ ckks_bootstrapper._ph = sys.modules[__name__]
 
 def device_count():
     return int(_lib.fhs_device_count())
+
+
+def device_pci_bus_id(device):
+    """PCI bus id of HIP device `device` (extension: the multi-rank bench line's device check)."""
+    buf = C.create_string_buffer(64)
+    _check(_lib.fhs_device_pci_bus_id(int(device), buf, 64), "device_pci_bus_id")
+    return buf.value.decode()
 
 
 _lock = threading.Lock()

@@ -50,6 +50,9 @@ typedef struct fhs_galois_keys fhs_galois_keys;
 const char* fhs_last_error(void);
 const char* fhs_version(void);
 int fhs_device_count(void);
+/* PCI bus id of HIP device `device` (e.g. "0000:05:00.0"), for the multi-rank line's device check.  Replaces
+ * no pb symbol (extension). */
+fhs_status fhs_device_pci_bus_id(int device, char* buf, int len);
 
 /* ---- parameters (pb:78-98) ---- */
 /* pb:81 create_coeff_modulus: SEAL CoeffModulus::Create (largest primes = 1 mod 2N per size) */

@@ -194,16 +194,24 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        td = fd.TimedDist(dist)          # the bench's exchange log (every call below goes through it)
+        td.start()
         mine = fd.my_projections(8, world, rank)
         t = torch.full((4,), rank * 10 + len(mine), dtype=torch.int64)
-        got = fd.gather_to_root(dist, t, world, rank)
+        got = fd.gather_to_root(td, t, world, rank)
         b = torch.arange(4, dtype=torch.int64) if rank == 1 else torch.zeros(4, dtype=torch.int64)
-        fd.broadcast_from(dist, b, src=1)
+        fd.broadcast_from(td, b, src=1)
+        big = torch.full((2048,), rank, dtype=torch.int64)
+        fd.broadcast_from(td, big, src=0)
         primes = [(1 << 59) - 55, (1 << 59) - 99]
         r = torch.tensor([[primes[0] - 1 - rank, 5], [primes[1] - 2, 7 + rank]], dtype=torch.int64)
-        fd.modular_reduce_sum(dist, r.view(-1), primes)
+        fd.modular_reduce_sum(td, r.view(-1), primes)
+        td.stop()
+        fd.broadcast_from(td, b, src=1)   # not logged
+        ids = fd.gather_identities(td, {"local_rank": rank, "pci_bus_id": f"0000:0{rank}:00.0"})
         q.put((rank, mine, None if got is None else [x.tolist() for x in got], b.tolist(),
-               r.tolist() if rank == 0 else None, fd.stage_assignment(world, rank)))
+               r.tolist() if rank == 0 else None, fd.stage_assignment(world, rank), td.summary(per=1), ids,
+               int(big[0])))
     finally:
         dist.destroy_process_group()
 
@@ -231,6 +239,16 @@ def test_two_rank_exchange_gloo():
     assert res[0][4] == [[(2 * p0 - 3) % p0, 10], [(2 * p1 - 4) % p1, 15]]
     assert res[0][5] == [["r", "v"], ["o"], ["ffn_key_0"], ["ffn_val_0"]]
     assert res[1][5] == [["k"], [], ["ffn_key_1"], ["ffn_val_1"]]
+    # exchange log schema (bench.py exchange_per_step / exchange_per_block_rank0): per kind calls, MB, ms;
+    # transfers under 4 KiB are the _small kinds
+    for rk in (0, 1):
+        ex = res[rk][6]
+        assert set(ex) == {"gather_small", "broadcast_small", "broadcast", "reduce_small"}, ex
+        assert ex["broadcast"]["calls"] == 1 and ex["broadcast"]["MB"] == round(2048 * 8 / 1e6, 3)
+        assert all(set(v) == {"calls", "MB", "ms"} and v["ms"] >= 0 for v in ex.values())
+    assert res[1][8] == 0
+    assert res[0][7] == res[1][7] == [{"local_rank": 0, "pci_bus_id": "0000:00:00.0"},
+                                      {"local_rank": 1, "pci_bus_id": "0000:01:00.0"}]
 
 
 # ------------------------------------------------------------------ exact centred ModUp / hoisting

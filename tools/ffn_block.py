@@ -338,21 +338,33 @@ def ct_digest(ct):
     return hashlib.sha256(np.ascontiguousarray(ct.to_numpy()).tobytes()).hexdigest()
 
 
-def run_ranks(ph, a, dist, rank, world, device):
-    """--blocks FFN blocks (random weights, same seeds on every rank) through FfnRanks on rank 0's chain
-    (world 1 without --dist: the one-rank ffn_block); rank 0 prints the final ciphertext's limb digest,
-    the per-block times and the decrypted error against the plaintext chain."""
-    rng = np.random.default_rng(42)
-    ck = Ckks(ph, a.N, a.L0, a.P, a.D, bootstrap=a.bootstrap)
-    x = rng.normal(0, 0.1, a.D)
+def chain_over_ranks(ph, N, L0, P, D, F, blocks, bootstrap, dist, rank, world, device, shard="giant", rb=None,
+                     baby_mode="recompute", seed=42, log=None):
+    """`blocks` FFN blocks (random weights from `seed`, the same on every rank) on rank 0's chain:
+    FfnRanks over the ranks when `dist` is given (any world), else the one-rank ffn_block -- limb-identical.
+    tf:239-266: a bootstrap (+ one rescale) before a block whenever fewer than 4 levels remain, its linear
+    transforms' giant groups over every rank.  Returns {block_seconds, bootstrap_seconds, chain_index,
+    max_err, ct_sha256 (rank 0), setup_s}; every block and bootstrap is bracketed by a device
+    synchronisation and (over ranks) a barrier."""
+    rng = np.random.default_rng(seed)
+    t_setup = time.perf_counter()
+    ck = Ckks(ph, N, L0, P, D, bootstrap=bootstrap)
+    x = rng.normal(0, 0.1, D)
     ct = ck.encrypt_replicated(x) if rank == 0 else None
     ref = x.copy()
-    fr = FfnRanks(ck, a.D, a.F, dist, rank, world, a.shard, a.rb, a.baby_mode, device) if dist is not None else None
-    times, boots = [], 0
-    for b in range(a.blocks):
-        Wk = rng.normal(0, 0.02, (a.D, a.F))
-        Wv = rng.normal(0, 0.02, (a.F, a.D))
-        if a.bootstrap:   # tf:239-266: fewer than 4 levels left -> bootstrap (+ one rescale)
+    fr = FfnRanks(ck, D, F, dist, rank, world, shard, rb, baby_mode, device) if dist is not None else None
+    ck.ctx.synchronize()
+    t_setup = time.perf_counter() - t_setup
+    times, boots, cis, errs = [], [], [], []
+
+    def sync():
+        ck.ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+    for b in range(blocks):
+        Wk = rng.normal(0, 0.02, (D, F))
+        Wv = rng.normal(0, 0.02, (F, D))
+        if bootstrap:   # tf:239-266: fewer than 4 levels left -> bootstrap (+ one rescale)
             need = int(rank == 0 and (ck.L0 - 1) - ct.chain_index() < 4)
             if dist is not None:
                 import torch
@@ -360,7 +372,8 @@ def run_ranks(ph, a, dist, rank, world, device):
                 dist.broadcast(flag, src=0)
                 need = int(flag.item())
             if need:
-                boots += 1
+                sync()
+                t0 = time.perf_counter()
                 if dist is None:
                     ct = ck.ph.rescale_to_next(ck.ctx, ck.bootstrap(ct))
                 else:                          # its linear transforms' giant groups over every rank
@@ -369,22 +382,35 @@ def run_ranks(ph, a, dist, rank, world, device):
                             ct = ck.ph.mod_switch_to_next(ck.ctx, ct)
                     out = ck.bt.bootstrap_ranks(ck.ctx, ct if rank == 0 else None, dist, device)
                     ct = ck.ph.rescale_to_next(ck.ctx, out) if rank == 0 else None
-        if dist is not None:
-            dist.barrier()
-        ck.ctx.synchronize()
+                sync()
+                boots.append(time.perf_counter() - t0)
+        sync()
         t0 = time.perf_counter()
-        ct = fr.block(ct, Wk, Wv) if fr is not None else ffn_block(ck, ct, Wk, Wv, a.D, a.F)
-        ck.ctx.synchronize()
-        if dist is not None:
-            dist.barrier()
+        ct = fr.block(ct, Wk, Wv) if fr is not None else ffn_block(ck, ct, Wk, Wv, D, F)
+        sync()
         times.append(time.perf_counter() - t0)
         ref = plain_ffn(ref, Wk, Wv)
         if rank == 0:
-            err = float(np.max(np.abs(ck.decrypt(ct, a.D) - ref)))
-            print(f"block {b}: {1e3 * times[-1]:.1f} ms chain_index={ct.chain_index()} max_err={err:.3e}", flush=True)
+            errs.append(float(np.max(np.abs(ck.decrypt(ct, D) - ref))))
+            cis.append(ct.chain_index())
+            if log:
+                log(f"block {b}: {1e3 * times[-1]:.1f} ms chain_index={cis[-1]} max_err={errs[-1]:.3e}")
+    res = {"block_seconds": times, "bootstrap_seconds": boots, "setup_s": t_setup}
+    if rank == 0:
+        res.update(chain_index=cis, max_err=errs, ct_sha256=ct_digest(ct))
+    del fr, ct, ck
+    return res
+
+
+def run_ranks(ph, a, dist, rank, world, device):
+    """--blocks FFN blocks through chain_over_ranks; rank 0 prints the per-block times, the decrypted error
+    against the plaintext chain and the final ciphertext's limb digest."""
+    r = chain_over_ranks(ph, a.N, a.L0, a.P, a.D, a.F, a.blocks, a.bootstrap, dist, rank, world, device, a.shard,
+                         a.rb, a.baby_mode, log=lambda m: print(m, flush=True))
     if rank == 0:
         print(f"ffn world {world} shard {a.shard if dist is not None else 'none'} babies {a.baby_mode}: "
-              f"mean block {1e3 * np.mean(times):.1f} ms, bootstraps {boots}, ct_sha256 {ct_digest(ct)}", flush=True)
+              f"mean block {1e3 * np.mean(r['block_seconds']):.1f} ms, bootstraps {len(r['bootstrap_seconds'])}, "
+              f"ct_sha256 {r['ct_sha256']}", flush=True)
 
 
 def main():

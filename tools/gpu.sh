@@ -11,6 +11,7 @@
 #                           steady state of the timed steps)
 #   pmc[=config]            FETCH_SIZE, WRITE_SIZE and VALU counter passes (one rocprofv3 run each)
 #                           -> OUT/pmc_traffic_<config>.json, OUT/pmc_valu_<config>.json
+#   stall[=config]          wave-cycle attribution passes (SQ_WAIT_*, LDS, instruction mix) -> OUT/pmc_stall_<config>.json
 #   rehearse=N[:bench args] N ranks sharing this one GPU (gloo, host-staged exchange; timings
 #                           meaningless): bench.py --gpus N self-launches them -> OUT/rehearse_nN.json
 #   dist1[=NAME[:ENV=v,..]] matvec bench at world 1 under torchrun with the RCCL gather step -> OUT/NAME.json
@@ -21,7 +22,7 @@ OUT=gpurun_out/$1
 shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-MV="--no-cpu-baseline --no-block --no-seal"
+MV="--no-cpu-baseline --no-block --no-seal --no-cfg5"
 fail() { echo "step $1 failed"; tail -20 "$2"; exit 1; }
 for step in "$@"; do
     name=${step%%=*}
@@ -66,6 +67,22 @@ for step in "$@"; do
         python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" \
             "$OUT/pmc_write/run_counter_collection.csv" 7 "$OUT/pmc_traffic_$cfg.json" || exit 1
         python3 tools/pmc_valu.py "$OUT/pmc_valu/run_counter_collection.csv" 7 "$OUT/pmc_valu_$cfg.json" || exit 1 ;;
+    stall)
+        # where k_modup_h's / k_bsgs_inner's wave cycles go (tools/pmc_stall.py): the counter list, then two SQ
+        # passes of 8 counters (+ GRBM) each, one rocprofv3 run per pass
+        cfg=${arg:-cfg2}
+        timeout -k 10 60 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || fail "counter list" "$OUT/counters_list.txt"
+        K="k_modup|k_bsgs_inner|k_ks_ip"
+        i=0
+        for c in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" \
+                 "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"; do
+            i=$((i + 1))
+            timeout -s KILL 240 rocprofv3 --kernel-include-regex "$K" --pmc $c -d "$OUT/stall_$i" -o run \
+                --output-format csv -- python3 bench.py --config "$cfg" --steps 3 --warmup 1 $MV > "$OUT/stall_$i.log" 2>&1 \
+                || fail "stall pass $i" "$OUT/stall_$i.log"
+        done
+        python3 tools/pmc_stall.py "$OUT/pmc_stall_$cfg.json" 7 "$OUT/stall_1/run_counter_collection.csv" \
+            "$OUT/stall_2/run_counter_collection.csv" || exit 1 ;;
     dist1)
         # the multi-rank step (RCCL gather, device-side stream ordering) at world 1 on this one GPU
         v=${arg%%:*}
