@@ -376,11 +376,20 @@ struct fhs_ciphertext {
     int ncomp, ci, l;
     double scale;
 };
+// One device block shared by the plaintexts of a batch (new_pts): a block per plaintext cost a hipMalloc per
+// diagonal and, once a chain walking down the levels pushed the cache over its cap, thousands of hipFree's
+// (round-5 cfg5 leg: 0.5-4.7 s per FFN block instead of ~0.2).  Freed when its last plaintext is destroyed.
+struct PtSlab {
+    uint64_t* base;
+    size_t bytes;
+    int refs;
+};
 struct fhs_plaintext {
     fhs_context* ctx;
     uint64_t* d;
     int ci, l;
     double scale;
+    PtSlab* slab = nullptr;   // non-null: d points into a batch's shared block
 };
 struct fhs_secret_key {
     fhs_context* ctx;
@@ -572,6 +581,39 @@ static fhs_status new_pt(fhs_context* c, int ci, double scale, fhs_plaintext** o
     }
     ctx_retain(c);
     *out = pt;
+    return FHS_OK;
+}
+// A block of at least *bytes: a cached block up to 1.5x the request is taken whole (*bytes becomes its size),
+// so the batches of a chain walking down the levels reuse the larger blocks the levels above left in the
+// cache instead of allocating (and, over the cap, freeing) one per level.
+static hipError_t dalloc_fit(fhs_context* c, uint64_t** p, size_t* bytes) {
+    size_t best = 0;
+    for (auto& kv : c->free_blocks)
+        if (!kv.second.empty() && kv.first >= *bytes && kv.first <= *bytes + *bytes / 2 && (!best || kv.first < best))
+            best = kv.first;
+    if (best) *bytes = best;
+    return dalloc(c, p, *bytes);
+}
+// `count` new plaintexts at chain index ci in one device block (PtSlab, dalloc_fit).  On failure nothing is
+// left allocated and outs[0..count) are null.
+static fhs_status new_pts(fhs_context* c, size_t count, int ci, double scale, fhs_plaintext** outs) {
+    const int l = c->L0 + 1 - ci;
+    if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
+    for (size_t k = 0; k < count; ++k) outs[k] = nullptr;
+    if (count == 0) return FHS_OK;
+    if (count == 1) return new_pt(c, ci, scale, outs);
+    const size_t per = (size_t)l * c->N;
+    auto* slab = new PtSlab{nullptr, 8 * count * per, 0};
+    hipError_t e = dalloc_fit(c, &slab->base, &slab->bytes);
+    if (e != hipSuccess) {
+        delete slab;
+        return hip_fail(e, "plaintext allocation");
+    }
+    for (size_t k = 0; k < count; ++k) {
+        outs[k] = new fhs_plaintext{c, slab->base + k * per, ci, l, scale, slab};
+        ++slab->refs;
+        ctx_retain(c);
+    }
     return FHS_OK;
 }
 static size_t ct_bytes(const fhs_ciphertext* ct) { return 8ull * ct->ncomp * ct->l * ct->ctx->N; }
@@ -1611,7 +1653,17 @@ extern "C" fhs_status fhs_ciphertext_destroy(fhs_ciphertext* ct) {
 extern "C" fhs_status fhs_plaintext_destroy(fhs_plaintext* pt) {
     if (!pt) return FHS_OK;
     fhs_context* c = pt->ctx;
-    { Guard g(c); dfree(c, pt->d, pt_bytes(pt)); }
+    {
+        Guard g(c);
+        if (pt->slab) {
+            if (--pt->slab->refs == 0) {
+                dfree(c, pt->slab->base, pt->slab->bytes);
+                delete pt->slab;
+            }
+        } else {
+            dfree(c, pt->d, pt_bytes(pt));
+        }
+    }
     delete pt;
     ctx_release(c);
     return FHS_OK;
@@ -1750,13 +1802,9 @@ static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cn
                                   bool is_real, double scale, int ci, fhs_plaintext** outs) {
     const int l = c->L0 + 1 - ci;
     std::vector<uint64_t*> ptrs(cnt);
-    for (size_t v = 0; v < cnt; ++v) {
-        fhs_plaintext* pt = nullptr;
-        fhs_status s = new_pt(c, ci, scale, &pt);
-        if (s != FHS_OK) return s;
-        outs[v] = pt;
-        ptrs[v] = pt->d;
-    }
+    fhs_status s0 = new_pts(c, cnt, ci, scale, outs);
+    if (s0 != FHS_OK) return s0;
+    for (size_t v = 0; v < cnt; ++v) ptrs[v] = outs[v]->d;
     uint64_t* dptrs = nullptr;
     hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * cnt, &dptrs);
     if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * cnt);
@@ -1952,12 +2000,10 @@ extern "C" fhs_status fhs_encode_precise(fhs_context* c, const double* re_im, si
     if (e == hipSuccess) e = hipMemcpyAsync(dbuf + count * N, lo.data(), 8 * count * N, hipMemcpyHostToDevice, c->st);
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);
     std::vector<uint64_t*> ptrs(count);
-    for (size_t v = 0; v < count && e == hipSuccess; ++v) {
-        fhs_plaintext* pt = nullptr;
-        fhs_status s = new_pt(c, ci, scale, &pt);
+    if (e == hipSuccess) {
+        fhs_status s = new_pts(c, count, ci, scale, outs);
         if (s != FHS_OK) { dfree(c, dbuf, 16 * count * N); return s; }
-        outs[v] = pt;
-        ptrs[v] = pt->d;
+        for (size_t v = 0; v < count; ++v) ptrs[v] = outs[v]->d;
     }
     uint64_t* dptrs = nullptr;
     if (e == hipSuccess) e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * count, &dptrs);
@@ -3363,11 +3409,10 @@ extern "C" fhs_status fhs_upload_plaintexts(fhs_context* c, const uint64_t* host
     ENTER(c);
     if (!host || !outs || count < 1) return fail(FHS_ERR_INVALID, "upload: bad args");
     BatchOut bo(outs, (size_t)count);
+    fhs_status s0 = new_pts(c, (size_t)count, ci, scale, outs);
+    if (s0 != FHS_OK) return s0;
     for (int k = 0; k < count; ++k) {
-        fhs_plaintext* pt;
-        fhs_status s = new_pt(c, ci, scale, &pt);
-        if (s != FHS_OK) return s;
-        outs[k] = pt;
+        fhs_plaintext* pt = outs[k];
         HIPCHK(hipMemcpyAsync(pt->d, host + (size_t)k * pt->l * c->N, pt_bytes(pt), hipMemcpyHostToDevice, c->st), "upload");
     }
     HIPCHK(hipStreamSynchronize(c->st), "upload");
@@ -3397,11 +3442,10 @@ extern "C" fhs_status fhs_random_plaintexts(fhs_context* c, uint64_t seed, int c
     ENTER(c);
     if (!outs || count < 1) return fail(FHS_ERR_INVALID, "random_plaintexts: bad args");
     BatchOut bo(outs, (size_t)count);
+    fhs_status s0 = new_pts(c, (size_t)count, ci, scale, outs);
+    if (s0 != FHS_OK) return s0;
     for (int k = 0; k < count; ++k) {
-        fhs_plaintext* pt;
-        fhs_status s = new_pt(c, ci, scale, &pt);
-        if (s != FHS_OK) return s;
-        outs[k] = pt;
+        fhs_plaintext* pt = outs[k];
         HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_TESTDATA, PrfKey{}, sm64(seed ^ sm64((7ull << 56) | (uint64_t)k)), pt->d, pt->l, c->st), "random_plaintexts");
     }
     return bo.keep(FHS_OK);

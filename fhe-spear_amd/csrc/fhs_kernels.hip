@@ -928,14 +928,34 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
         __syncthreads();
         // the radix-4 conversion (modup_convert3x, FHS_MODUP_R4) did each half's local stage 0 already
         constexpr int S0 = DP == 3 ? 1 : 0;
-        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0>(lds, tid, tw, m, lazy_of<LOGN, B59>(R), 1 + h);
+        // wave-local tail: no barriers between the passes with TL <= 64, none before the stores
+        constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, FHS_MODUPH_RL, S0>();
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0, WLX>(lds, tid, tw, m, lazy_of<LOGN, B59>(R), 1 + h);
         // buffer stores: per-lane offset tid, the half / row offset in soffset.  The extended limbs feed only
         // the key inner products, whose split-30 sums take any value < 2^60: lazy outputs are folded once
         // (pm_fold_lt60), without fwd_canon's final subtraction.  The wave-uniform lazy choice is made once
         // per sweep, outside the unrolled loop, so its 16 LDS reads issue together (a choice per element
         // split the loop into blocks, each waiting for its own read)
         const __amdgpu_buffer_rsrc_t ro = brsrc(o, N * 8);
-        if (lazy_of<LOGN, B59>(R)) {
+        if constexpr (WLX) {   // this wave's own outputs (wl_base + wl_off): rows of 64 consecutive elements
+            constexpr int GS = 1 << FHS_MODUPH_RL;
+            const int wb = wl_base<LOGN - 1, 16, GS>(tid), wp = lds_pad(wb);
+            if (lazy_of<LOGN, B59>(R)) {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) {
+                    const int off = wl_off<LOGN - 1, 16, GS>(c);
+                    bstore64_aux<FHS_MODUP_STORE_AUX>(pm_fold_lt60(lds[wp + off + off / 16], R), ro, wb * 8,
+                                                      (h * NH + off) * 8);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) {
+                    const int off = wl_off<LOGN - 1, 16, GS>(c);
+                    bstore64_aux<FHS_MODUP_STORE_AUX>(fwd_canon(lds[wp + off + off / 16], R), ro, wb * 8,
+                                                      (h * NH + off) * 8);
+                }
+            }
+        } else if (lazy_of<LOGN, B59>(R)) {
 #pragma unroll
             for (int c = 0; c < 16; ++c)
                 bstore64_aux<FHS_MODUP_STORE_AUX>(pm_fold_lt60(lds[row_pad<TH>(tid, c)], R), ro, tid * 8,

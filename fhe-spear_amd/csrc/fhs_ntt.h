@@ -128,13 +128,40 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
     }
 }
 
-template <int LOGN, int RL, int S, int EPT, bool LAZY>
+// Wave-local passes (round 5).  A pass whose butterfly groups have TL <= 64 hands wave w exactly the
+// blocks [GS (64 w + c T), + 64 GS) for c < EPT / GS (lanes take consecutive gids, TL divides 64, a group
+// spans GS TL elements): the same elements in every such pass of the same radix.  Between two of them no
+// workgroup barrier is needed -- the LDS operations of one wave execute in issue order, and
+// wave_barrier() keeps the compiler from moving LDS accesses across the pass boundary -- and after the last
+// one the caller may read its own wave's blocks (wl_elem) without a barrier either.  PMC (profiles/r05,
+// k_modup_h): 35 % of wave cycles parked on s_waitcnt / barriers, 25 % of SIMD cycles without VALU issue.
+#ifndef FHS_NTT_WAVELOCAL
+#define FHS_NTT_WAVELOCAL 1
+#endif
+template <int LOGN, int S, int R>
+constexpr int pass_tl() { return ((1 << LOGN) >> (S + 1)) >> (R - 1); }
+template <int LOGN, int RL, int S>
+constexpr int pass_r() { return (LOGN - S) < RL ? (LOGN - S) : RL; }
+// element index of output q (q < EPT, compile-time) of thread tid after a wave-local transform (WL) whose
+// passes have radix 2^R: block c = q / GS of the wave, row r = q % GS, lane-consecutive
+template <int LOGN, int EPT, int GS>
+__device__ __forceinline__ int wl_base(int tid) { return GS * 64 * (tid >> 6) + (tid & 63); }
+template <int LOGN, int EPT, int GS>
+constexpr int wl_off(int q) { return GS * ((1 << LOGN) / EPT) * (q / GS) + 64 * (q % GS); }
+
+template <int LOGN, int RL, int S, int EPT, bool LAZY, bool WL = false>
 __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
     if constexpr (S < LOGN) {
-        constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
+        constexpr int R = pass_r<LOGN, RL, S>();
         ntt_pass<LOGN, S, R, true, EPT, LAZY>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
-        __syncthreads();
-        fwd_from<LOGN, RL, S + R, EPT, LAZY>(lds, tid, tw, q, hoff);
+        constexpr int S2 = S + R;
+        constexpr bool here = WL && pass_tl<LOGN, S, R>() <= 64;
+        constexpr bool next = S2 >= LOGN || (pass_r<LOGN, RL, S2>() == R && pass_tl<LOGN, S2, pass_r<LOGN, RL, S2>()>() <= 64);
+        if constexpr (here && next)
+            __builtin_amdgcn_wave_barrier();
+        else
+            __syncthreads();
+        fwd_from<LOGN, RL, S2, EPT, LAZY, WL>(lds, tid, tw, q, hoff);
     }
 }
 // inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first
@@ -153,15 +180,23 @@ __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restric
 // Exit: bit-reversed-order output, after a barrier: < 4q (Harvey) or < (4 + 2 LOGN) q when
 // `lazy` (wave-uniform; RedU::lazy); fwd_canon() maps either to [0, q).
 // S0 > 0: stages [0, S0) were done by the caller (in registers), the passes start at stage S0.
-template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0>
+// WL: wave-local tail (above): the exit barrier is dropped when the last pass is wave-local, so the caller
+// must read only its wave's outputs (wl_base + wl_off) until its next barrier.
+template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0, bool WL = false>
 __device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, bool lazy,
                                             int hoff = 0) {
     static_assert(LOGN >= 7 && LOGN <= 14, "LDS-resident NTT supports 128 <= N <= 16384");
     static_assert(EPT >= 16 && (EPT & (EPT - 1)) == 0, "EPT must be a power of two >= 16");
     if (lazy)
-        fwd_from<LOGN, RL, S0, EPT, true>(lds, tid, tw, q, hoff);
+        fwd_from<LOGN, RL, S0, EPT, true, WL>(lds, tid, tw, q, hoff);
     else
-        fwd_from<LOGN, RL, S0, EPT, false>(lds, tid, tw, q, hoff);
+        fwd_from<LOGN, RL, S0, EPT, false, WL>(lds, tid, tw, q, hoff);
+}
+// true when ntt_fwd_lds<LOGN, RL, EPT, S0, true> leaves its outputs wave-local (every pass radix 2^RL, the
+// last wave-local): the caller reads wl_base + wl_off with GS = 2^RL
+template <int LOGN, int RL, int S0>
+constexpr bool fwd_exit_wave_local() {
+    return (LOGN - S0) % RL == 0 && pass_tl<LOGN, LOGN - RL, RL>() <= 64;
 }
 // Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.

@@ -16,6 +16,7 @@
 #                           meaningless): bench.py --gpus N self-launches them -> OUT/rehearse_nN.json
 #   dist1[=NAME[:ENV=v,..]] matvec bench at world 1 under torchrun with the RCCL gather step -> OUT/NAME.json
 #   py=SCRIPT[:args]        python SCRIPT args                                  -> OUT/py_<name>.log
+#   exe=BINARY              a prebuilt microbenchmark                          -> OUT/exe_<name>.log
 #   ptrace=SCRIPT[:args]    the same under rocprofv3 --kernel-trace --stats      -> OUT/ptrace_<name>/
 set -o pipefail
 OUT=gpurun_out/$1
@@ -109,6 +110,11 @@ for step in "$@"; do
         b=$(basename "$s" .py)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/ptrace_$b" -o run --output-format csv \
             -- python3 -u "$s" $a > "$OUT/ptrace_$b.log" 2>&1 || fail "ptrace $s" "$OUT/ptrace_$b.log" ;;
+    exe)
+        # a prebuilt microbenchmark binary (tools/microbench/*, built here with hipcc)
+        b=$(basename "$arg")
+        timeout -k 10 180 "$arg" > "$OUT/exe_$b.log" 2>&1 || fail "exe $arg" "$OUT/exe_$b.log"
+        tail -4 "$OUT/exe_$b.log" ;;
     py)
         s=${arg%%:*}
         a=""
