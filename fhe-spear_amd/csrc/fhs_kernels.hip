@@ -252,9 +252,19 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
                 for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
             }
             __syncthreads();
-            ntt_fwd_lds<LOGN - 1, 3, 16, 1>(lds, tid, tw, R.q, R.lazy, 1 + h);
+            constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, 3, 1>();
+            ntt_fwd_lds<LOGN - 1, 3, 16, 1, WLX>(lds, tid, tw, R.q, R.lazy, 1 + h);
+            if constexpr (WLX) {   // this wave's own outputs (wave-local tail, fhs_ntt.h)
+                const int wb = wl_base<LOGN - 1, 16, 8>(tid), wp = lds_pad(wb);
 #pragma unroll
-            for (int c = 0; c < 16; ++c) store(h * NH + tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
+                for (int c = 0; c < 16; ++c) {
+                    const int off = wl_off<LOGN - 1, 16, 8>(c);
+                    store(h * NH + wb + off, fwd_canon(lds[wp + off + off / 16], R));
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) store(h * NH + tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
+            }
         }
     }
 }
@@ -278,10 +288,20 @@ __device__ __forceinline__ void inv_limb(u64* lds, int tid, const u64* __restric
 #pragma unroll 1
         for (int h = 0; h < 2; ++h) {
             if (h) __syncthreads();
+            constexpr bool WLI = FHS_NTT_WAVELOCAL && (LOGN - 2) % 3 == 0;
+            if constexpr (WLI) {   // wave-local head: each wave loads the blocks its deep passes transform
+                const int wb = wl_base<LOGN - 1, 16, 8>(tid), wp = lds_pad(wb);
 #pragma unroll
-            for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(h * NH + tid + c * TH);
-            __syncthreads();
-            ntt_inv_half_lds<LOGN - 1, 3, 16, 1>(lds, tid, tw, q, 1 + h);   // local stage 0: inv_quad_last2
+                for (int c = 0; c < 16; ++c) {
+                    const int off = wl_off<LOGN - 1, 16, 8>(c);
+                    lds[wp + off + off / 16] = load(h * NH + wb + off);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = load(h * NH + tid + c * TH);
+                __syncthreads();
+            }
+            ntt_inv_half_lds<LOGN - 1, 3, 16, 1, WLI>(lds, tid, tw, q, 1 + h);   // local stage 0: inv_quad_last2
             if (h == 0) {
 #pragma unroll
                 for (int c = 0; c < 16; ++c) lo[c] = lds[row_pad<TH>(tid, c)];
@@ -530,17 +550,24 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_ks_intt_h(DevTables T, 
     const __amdgpu_buffer_rsrc_t rs = brsrc(uniq[u] + (size_t)i * N, N * 8);
     const u64* tw = T.tw_inv + (size_t)i * N * 2;
     u64 lo[16];
+    // wave-local head (fhs_ntt.h inv_from): each wave loads the blocks its deep passes transform, so no barrier
+    // before them and none between them
+    constexpr bool WLI = FHS_NTT_WAVELOCAL && (LOGN - 2) % FHS_NTT_RL == 0;
+    constexpr int GS = 1 << FHS_NTT_RL;
+    const int tb = WLI ? wl_base<LOGN - 1, 16, GS>(tid) : tid;
+    auto eoff = [&](int c) { return WLI ? wl_off<LOGN - 1, 16, GS>(c) : c * TH; };
+    auto lidx = [&](int c) { return WLI ? lds_pad(tb) + eoff(c) + eoff(c) / 16 : row_pad<TH>(tid, c); };
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
         if (h) __syncthreads();
         u64 v[16];
 #pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = bload64(rs, tid * 8, (h * NH + c * TH) * 8);
+        for (int c = 0; c < 16; ++c) v[c] = bload64(rs, tb * 8, (h * NH + eoff(c)) * 8);
 #pragma unroll
-        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = v[c];
-        __syncthreads();
+        for (int c = 0; c < 16; ++c) lds[lidx(c)] = v[c];
+        if constexpr (!WLI) __syncthreads();
         // every stage of the half but its local stage 0 (rows c, c + 8: done below in registers)
-        ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL, 16, 1>(lds, tid, tw, q, 1 + h);
+        ntt_inv_half_lds<LOGN - 1, FHS_NTT_RL, 16, 1, WLI>(lds, tid, tw, q, 1 + h);
         if (h == 0) {
 #pragma unroll
             for (int c = 0; c < 16; ++c) lo[c] = lds[row_pad<TH>(tid, c)];
@@ -1348,7 +1375,14 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
         }
         __syncthreads();
-        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, 1>(lds, tid, tw, q, lazy_of<LOGN, B59>(RU), 1 + h);
+        // wave-local tail (fhs_ntt.h): the outputs are read by the wave that made them, no exit barrier; element
+        // of output c: tb + eoff(c) (tb = wl_base or tid), LDS word lb + loff(c)
+        constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, FHS_MODUPH_RL, 1>();
+        constexpr int GS = 1 << FHS_MODUPH_RL;
+        ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, 1, WLX>(lds, tid, tw, q, lazy_of<LOGN, B59>(RU), 1 + h);
+        const int tb = WLX ? wl_base<LOGN - 1, 16, GS>(tid) : tid, lb = lds_pad(tb);
+        auto eoff = [&](int c) { return WLX ? wl_off<LOGN - 1, 16, GS>(c) : c * TH; };
+        auto lidx = [&](int c) { return WLX ? lb + eoff(c) + eoff(c) / 16 : row_pad<TH>(tid, c); };
         // outputs in batches of 4 whose accumulator (and rotated c0) loads are issued together, with
         // the add / no-add choice outside the loop (one latency per batch, not one per coefficient);
         // buffer loads / stores with the row offsets in soffset
@@ -1357,15 +1391,15 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             const __amdgpu_buffer_rsrc_t rad = brsrc(add + (size_t)i * N, N * 8);
             // galois_src(e) for e = tid + c TH + h NH: rev(e) = rev(tid) + rev(c TH + h NH) (disjoint bits),
             // so the exponent (2 rev(e) + 1) elt mod 2N is a per-thread base plus a wave-uniform term
-            const unsigned rt = __brev((unsigned)tid) >> (32 - LOGN);
+            const unsigned rt = __brev((unsigned)tb) >> (32 - LOGN);
             const u64 ebase = ((2 * (u64)rt + 1) * aelt) & (2 * (u64)N - 1);
 #pragma unroll
             for (int c0 = 0; c0 < 16; c0 += 4) {
                 u64 av[4], dv[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int eo = h * NH + (c0 + k) * TH;
-                    av[k] = bload64(rac, tid * 8, eo * 8);
+                    const int eo = h * NH + eoff(c0 + k);
+                    av[k] = bload64(rac, tb * 8, eo * 8);
                     const u64 ec = (2 * (u64)(__brev((unsigned)eo) >> (32 - LOGN)) * aelt) & (2 * (u64)N - 1);
                     const u64 e2 = (ebase + ec) & (2 * (u64)N - 1);
                     const int src = (int)(__brev((unsigned)((e2 - 1) >> 1)) >> (32 - LOGN));
@@ -1375,9 +1409,9 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
                 for (int k = 0; k < 4; ++k) {
                     // B59: the NTT output folded once (< 2q) and a + 2q - v handed to the Shoup product
                     // (any 64-bit input) -- no run-time lazy choice per element, no canonicalisation
-                    const u64 x = lds[row_pad<TH>(tid, c0 + k)];
+                    const u64 x = lds[lidx(c0 + k)];
                     const u64 dif = B59 ? av[k] + q2 - fold59(x, RU.d) : submod(av[k], fwd_canon(x, RU), q);
-                    bstore64(addmod(shoup(dif, pinv, pinv_s, q), dv[k], q), ro, tid * 8, (h * NH + (c0 + k) * TH) * 8);
+                    bstore64(addmod(shoup(dif, pinv, pinv_s, q), dv[k], q), ro, tb * 8, (h * NH + eoff(c0 + k)) * 8);
                 }
             }
         } else {
@@ -1385,12 +1419,12 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
             for (int c0 = 0; c0 < 16; c0 += 4) {
                 u64 av[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) av[k] = bload64(rac, tid * 8, (h * NH + (c0 + k) * TH) * 8);
+                for (int k = 0; k < 4; ++k) av[k] = bload64(rac, tb * 8, (h * NH + eoff(c0 + k)) * 8);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const u64 x = lds[row_pad<TH>(tid, c0 + k)];
+                    const u64 x = lds[lidx(c0 + k)];
                     const u64 dif = B59 ? av[k] + q2 - fold59(x, RU.d) : submod(av[k], fwd_canon(x, RU), q);
-                    bstore64(shoup(dif, pinv, pinv_s, q), ro, tid * 8, (h * NH + (c0 + k) * TH) * 8);
+                    bstore64(shoup(dif, pinv, pinv_s, q), ro, tb * 8, (h * NH + eoff(c0 + k)) * 8);
                 }
             }
         }

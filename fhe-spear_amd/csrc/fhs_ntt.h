@@ -128,9 +128,10 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
     }
 }
 
-// Wave-local passes (round 5).  A pass whose butterfly groups have TL <= 64 hands wave w exactly the
-// blocks [GS (64 w + c T), + 64 GS) for c < EPT / GS (lanes take consecutive gids, TL divides 64, a group
-// spans GS TL elements): the same elements in every such pass of the same radix.  Between two of them no
+// Wave-local passes (round 5).  A pass whose butterfly groups have TL <= W (W = 64 lanes, or all T threads
+// when there are fewer) hands wave w exactly the blocks [GS (W w + c T), + W GS) for c < EPT / GS (lanes take
+// consecutive gids, TL divides W, a group spans GS TL elements): the same elements in every such pass of the
+// same radix.  Between two of them no
 // workgroup barrier is needed -- the LDS operations of one wave execute in issue order, and
 // wave_barrier() keeps the compiler from moving LDS accesses across the pass boundary -- and after the last
 // one the caller may read its own wave's blocks (wl_elem) without a barrier either.  PMC (profiles/r05,
@@ -140,14 +141,20 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
 #endif
 template <int LOGN, int S, int R>
 constexpr int pass_tl() { return ((1 << LOGN) >> (S + 1)) >> (R - 1); }
+// lanes of a wave that take part: 64, or all T = N / EPT threads when the transform has fewer (one wave)
+template <int LOGN, int EPT>
+constexpr int wl_width() { return (1 << LOGN) / EPT < 64 ? (1 << LOGN) / EPT : 64; }
 template <int LOGN, int RL, int S>
 constexpr int pass_r() { return (LOGN - S) < RL ? (LOGN - S) : RL; }
 // element index of output q (q < EPT, compile-time) of thread tid after a wave-local transform (WL) whose
 // passes have radix 2^R: block c = q / GS of the wave, row r = q % GS, lane-consecutive
 template <int LOGN, int EPT, int GS>
-__device__ __forceinline__ int wl_base(int tid) { return GS * 64 * (tid >> 6) + (tid & 63); }
+__device__ __forceinline__ int wl_base(int tid) {
+    constexpr int W = wl_width<LOGN, EPT>();
+    return GS * W * (tid / W) + (tid % W);
+}
 template <int LOGN, int EPT, int GS>
-constexpr int wl_off(int q) { return GS * ((1 << LOGN) / EPT) * (q / GS) + 64 * (q % GS); }
+constexpr int wl_off(int q) { return GS * ((1 << LOGN) / EPT) * (q / GS) + wl_width<LOGN, EPT>() * (q % GS); }
 
 template <int LOGN, int RL, int S, int EPT, bool LAZY, bool WL = false>
 __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
@@ -155,8 +162,9 @@ __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restric
         constexpr int R = pass_r<LOGN, RL, S>();
         ntt_pass<LOGN, S, R, true, EPT, LAZY>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
         constexpr int S2 = S + R;
-        constexpr bool here = WL && pass_tl<LOGN, S, R>() <= 64;
-        constexpr bool next = S2 >= LOGN || (pass_r<LOGN, RL, S2>() == R && pass_tl<LOGN, S2, pass_r<LOGN, RL, S2>()>() <= 64);
+        constexpr int W = wl_width<LOGN, EPT>();
+        constexpr bool here = WL && pass_tl<LOGN, S, R>() <= W;
+        constexpr bool next = S2 >= LOGN || (pass_r<LOGN, RL, S2>() == R && pass_tl<LOGN, S2, pass_r<LOGN, RL, S2>()>() <= W);
         if constexpr (here && next)
             __builtin_amdgcn_wave_barrier();
         else
@@ -164,15 +172,22 @@ __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restric
         fwd_from<LOGN, RL, S2, EPT, LAZY, WL>(lds, tid, tw, q, hoff);
     }
 }
-// inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first
-template <int LOGN, int RL, int S, int EPT, bool NOFOLD = false>
+// inverse: chunks [0,RL), [RL,2RL), ... processed last-to-first.  WL (every pass radix RL from S0): the
+// barrier after pass S is skipped when the pass executed next (S - RL) is wave-local too (TL <= 64 for both;
+// see fwd_from) -- the deep passes, which run first; a caller that wrote its input wave-locally (wl_base +
+// wl_off) needs no barrier before the transform either.
+template <int LOGN, int RL, int S, int EPT, bool NOFOLD = false, bool WL = false, int S0 = 0>
 __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
                                          u64 s1, u64 s1s, int hoff = 0) {
     if constexpr (S < LOGN) {
-        constexpr int R = (LOGN - S) < RL ? (LOGN - S) : RL;
-        inv_from<LOGN, RL, S + R, EPT, NOFOLD>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
+        constexpr int R = pass_r<LOGN, RL, S>();
+        inv_from<LOGN, RL, S + R, EPT, NOFOLD, WL, S0>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
         ntt_pass<LOGN, S, R, false, EPT, false, NOFOLD>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
-        __syncthreads();
+        if constexpr (WL && S - RL >= S0 && pass_tl<LOGN, S, R>() <= wl_width<LOGN, EPT>() &&
+                      pass_tl<LOGN, S - RL, RL>() <= wl_width<LOGN, EPT>())
+            __builtin_amdgcn_wave_barrier();
+        else
+            __syncthreads();
     }
 }
 
@@ -194,18 +209,19 @@ __device__ __forceinline__ void ntt_fwd_lds(u64* lds, int tid, const u64* __rest
 }
 // true when ntt_fwd_lds<LOGN, RL, EPT, S0, true> leaves its outputs wave-local (every pass radix 2^RL, the
 // last wave-local): the caller reads wl_base + wl_off with GS = 2^RL
-template <int LOGN, int RL, int S0>
+template <int LOGN, int RL, int S0, int EPT = 16>
 constexpr bool fwd_exit_wave_local() {
-    return (LOGN - S0) % RL == 0 && pass_tl<LOGN, LOGN - RL, RL>() <= 64;
+    return (LOGN - S0) % RL == 0 && pass_tl<LOGN, LOGN - RL, RL>() <= wl_width<LOGN, EPT>();
 }
 // Inverse transform in LDS; the final stage multiplies by (s0, s1) = (N^-1 c, psi^-1 N^-1 c) for a
 // per-limb constant c.  Exit: natural-order output in [0, 2q), after a barrier.
 // Inverse on one half (h = hoff - 1) of a 2^(LOGN+1)-point inverse: all of its stages except the
 // global last one, which the caller applies to the (e, e + 2^LOGN) pairs.  Output in [0, 2q).
 // S0 > 0: stages [0, S0) are left to the caller (done in registers afterwards).
-template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0>
+template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0, bool WL = false>
 __device__ __forceinline__ void ntt_inv_half_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
-    inv_from<LOGN, RL, S0, EPT, true>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
+    static_assert(!WL || (LOGN - S0) % RL == 0, "wave-local inverse passes need one radix throughout");
+    inv_from<LOGN, RL, S0, EPT, true, WL, S0>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
 }
 template <int LOGN, int RL = 3, int EPT = 16>
 __device__ __forceinline__ void ntt_inv_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, u64 s0, u64 s0s,
