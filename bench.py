@@ -598,8 +598,10 @@ def main():
 
 def seal_leg(args, ph, cfg):
     """cfg2's matvec with context.set_key_switch_mode('seal'): primes [59] x (L0 + 1), one special
-    prime, SEAL's switch_key_inplace per rotation (DESIGN.md §3 SEAL convention).  Same seeds as the
-    main leg; output limbs checked against the oracle's digest of this mode (bench_digests cfg2_seal).
+    prime, SEAL's switch_key_inplace limbs (DESIGN.md §3 SEAL convention; round 5: the 45 baby rotations
+    share one decomposition, corrected per Galois key to SEAL's per-rotation lift -- `hoisting` counts the
+    flushes taken each way).  Same seeds as the main leg; output limbs checked against the oracle's digest of
+    this mode (bench_digests cfg2_seal: the oracle rotates one rotation at a time).
     One instrumented step gives the per-kernel breakdown; the roofline kernel is chosen as for the main
     leg (hash-matched rocprof_summary_cfg2seal record, else the instrumented step) and timed live with
     HIP events in the timed steps; `matvec_roofline` prices the whole matvec at SURVEY §8(d)'s bytes for
