@@ -120,3 +120,26 @@ def test_gpu_scripts_parse():
     for f in sorted((REPO / "tools").glob("*.sh")) + sorted((REPO / "tools" / "debug").glob("*.sh")):
         r = subprocess.run(["bash", "-n", str(f)], capture_output=True, text=True)
         assert r.returncode == 0, (f.name, r.stderr)
+
+
+def test_pmc_stall_shares(tmp_path):
+    """tools/pmc_stall.py: per-kernel sums over two PMC passes, per step, shares of
+    SQ_WAVE_CYCLES, VALU busy against the SIMD cycles (GRBM_GUI_ACTIVE averaged over the passes carrying it)."""
+    hdr = "Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n"
+    k = '"void fhs::k_modup_h<14, 3, true>(fhs::DevTables, ...)"'   # quoted, as rocprofv3 writes it
+    p1 = tmp_path / "p1.csv"
+    p1.write_text(hdr + "".join(f"{d},{k},{n},{v}\n" for d in (1, 2) for n, v in (
+        ("SQ_WAVE_CYCLES", 1000), ("SQ_WAIT_ANY", 350), ("SQ_WAIT_INST_ANY", 350), ("SQ_ACTIVE_INST_ANY", 300),
+        ("SQ_ACTIVE_INST_VALU", 2048 * 8), ("GRBM_GUI_ACTIVE", 8 * 64))))
+    p2 = tmp_path / "p2.csv"
+    p2.write_text(hdr + "".join(f"{d},{k},{n},{v}\n" for d in (5, 6) for n, v in (
+        ("SQ_INSTS_VALU", 100), ("SQ_INSTS_LDS", 10), ("SQ_LDS_BANK_CONFLICT", 17), ("GRBM_GUI_ACTIVE", 8 * 64))))
+    out = tmp_path / "stall.json"
+    subprocess.run([sys.executable, str(REPO / "tools" / "pmc_stall.py"), str(out), "2", str(p1), str(p2)], check=True,
+                   capture_output=True)
+    rec = json.loads(out.read_text())["kernels"]["k_modup_h"]
+    assert rec["launches_per_step"] == 1.0
+    assert rec["share_wait_any"] == 0.35 and rec["share_active_inst_any"] == 0.3
+    # per step: 2048 x 8 VALU quad-cycles x 4 over 1024 SIMDs x (512 per pass, 2 passes -> 512) / 8 cycles
+    assert rec["valu_busy"] == round(2048 * 8 * 4 / (1024 * 512 / 8), 3)
+    assert rec["bank_conflict_cycles_per_lds_inst"] == 1.7 and rec["lds_per_valu"] == 0.1
