@@ -1710,9 +1710,6 @@ __device__ __forceinline__ void ld_diag(const u64* limb, int voff, int soff, u64
         out[0] = __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kBufNT));
     }
 }
-#ifndef FHS_INNER_TAIL_ROLL
-#define FHS_INNER_TAIL_ROLL 1   // k_bsgs_inner (FOLD 16): partial last batch rolled, next group prefetched
-#endif
 // FOLD: products per Acc3 before its fold into the 128-bit sums -- 8 for any prime < 2^60, 16 when every
 // prime is < 2^59 (T.max_qbits <= 59): then the split-30 high halves are < 2^29, so L and M gain < 2^60
 // and H < 2^58 per product and 16 products stay below 2^64
@@ -1734,95 +1731,6 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     // stream too.
     u64 p[8][VEC];
     const int gcur = g0 + wave;
-    if constexpr (FOLD == 16 && FHS_INNER_TAIL_ROLL) {
-        // Round 5: the partial last batch of a group (bmax % 8 diagonals: 6 of cfg2's 46) rolls like the
-        // full ones -- its missing slots load zeros through a zero-size buffer descriptor (no branch around
-        // a load, so no drain) and multiply the zeros in -- and the last batch's refill requests the wave's
-        // NEXT group's first batch, so the loads stay in flight across the group's folds and stores
-        // (round 4 loaded the tail one diagonal at a time and restarted the stream after the stores).
-        auto ndiag = [&](int g) { return g < g1 ? max(0, min(G, D - g * G)) : 0; };
-        // slot load: diagonal k of `base` when valid, else zeros (num_records 0 drops the load)
-        auto ld_slot = [&](const u64* const* base, int k, bool valid, u64* dst) {
-            const u64* pk = base[valid ? k : 0];
-            const __amdgpu_buffer_rsrc_t r = brsrc(pk + (size_t)i * N, valid ? 0x7ffffff0u : 0u);
-            if constexpr (VEC == 2) {
-                const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, lane * VEC * 8, n0 * 8, kBufNT);
-                dst[0] = ((u64)t[1] << 32) | t[0];
-                dst[1] = ((u64)t[3] << 32) | t[2];
-            } else {
-                dst[0] = __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, lane * VEC * 8, n0 * 8, kBufNT));
-            }
-        };
-        int g = gcur;
-        while (g < g1 && ndiag(g) == 0) g += WAVES;
-        if (g < g1) {
-            const int n = ndiag(g);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) ld_slot(pts + (size_t)g * G, u, u < n, p[u]);
-        }
-        for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
-            const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
-            sb[idx] = pack30(baby[b][comp * S + (size_t)i * N + n0 + c]);
-        }
-        __syncthreads();
-        const RedU R = redu(PK(T, i));
-        while (g < g1) {
-            const int bmax = ndiag(g);
-            int gn = g + WAVES;
-            while (gn < g1 && ndiag(gn) == 0) gn += WAVES;
-            const int nbn = ndiag(gn);
-            u128 c0[VEC], c1[VEC];
-            Acc3 a0[VEC], a1[VEC];
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) {
-                c0[v] = c1[v] = u128{0, 0};
-                a0[v] = a1[v] = Acc3{0, 0, 0};
-            }
-            const u64* const* pg = pts + (size_t)g * G;
-            const int nb = (bmax + 7) / 8;
-            int b = 0;
-            for (int bi = 0; bi < nb; ++bi, b += 8) {
-                // refill source: this group's next batch, or after the last batch the next group's first
-                const bool last = bi + 1 == nb;
-                const u64* const* nsrc = last ? pts + (size_t)(gn < g1 ? gn : g) * G : pg + b + 8;
-                const int nlim = last ? nbn : bmax - (b + 8);
-#pragma unroll
-                for (int h = 0; h < 8; h += 4) {   // half a batch: products, fold, that half's refill
-#pragma unroll
-                    for (int u = h; u < h + 4; ++u) {
-                        const int bb = b + u < bmax ? b + u : 0;   // a missing slot holds zeros: any baby step
-#pragma unroll
-                        for (int v = 0; v < VEC; ++v) {
-                            const Split30 y = split30(p[u][v]);
-                            acc3_mac(a0[v], unpack30(sb[(bb * 2 + 0) * W + lane * VEC + v]), y);
-                            acc3_mac(a1[v], unpack30(sb[(bb * 2 + 1) * W + lane * VEC + v]), y);
-                        }
-                    }
-                    if (h == 4 && (b & 15) == 8) {   // 16 products per Acc3 (every prime < 2^59)
-#pragma unroll
-                        for (int v = 0; v < VEC; ++v) {
-                            acc3_fold(c0[v], a0[v]);
-                            acc3_fold(c1[v], a1[v]);
-                        }
-                    }
-#pragma unroll
-                    for (int u = h; u < h + 4; ++u) ld_slot(nsrc, u, u < nlim, p[u]);
-                }
-            }
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) {
-                acc3_fold(c0[v], a0[v]);
-                acc3_fold(c1[v], a1[v]);
-            }
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) {
-                inner[(size_t)g * 2 * S + off + v] = reduce128(c0[v].lo, c0[v].hi, R);
-                inner[(size_t)g * 2 * S + S + off + v] = reduce128(c1[v].lo, c1[v].hi, R);
-            }
-            g = gn;
-        }
-        return;
-    }
     auto full_batches = [&](int g) { return g < g1 ? max(0, min(G, D - g * G)) / 8 : 0; };
     int gf = gcur;   // the wave's first group with a full batch
     while (gf < g1 && full_batches(gf) == 0) gf += WAVES;
