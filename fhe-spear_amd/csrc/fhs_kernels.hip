@@ -855,6 +855,31 @@ __device__ __forceinline__ void modup_convert1(const u64* yb, const unsigned cha
     }
 }
 
+// The same with global stages 0 and 1 as a register radix-4 (fwd_quad_first2), so the half transforms start at
+// their local stage 1 (four radix-8 passes, no radix-2 pass, wave-local tail): B59 chains only, where every
+// prime is within 2^27 of 2^59, so y < q_u < 2 m and y + v negQ < 3 m; one conditional subtraction of 2 m
+// gives fwd_quad_first2's input bound (< 2 m) for the lazy and the Harvey form alike.  SEAL's convention (P = 1).
+template <int LOGN>
+__device__ __forceinline__ void modup_convert1_r4(const u64* yb, const unsigned char* vb, u64 negQ, u64 m,
+                                                  bool lazy, const u64* tw, int tid, u64* lds, u64 hi[16]) {
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
+    const __amdgpu_buffer_rsrc_t ry = brsrc(yb, N * 8), rv = brsrc(vb, N);
+    const Tw4 w4 = ld_tw4(tw);
+#pragma unroll
+    for (int ch = 0; ch < 8; ++ch) {
+        u64 x[4];   // rows ch (k = 0, 2) and ch + 8 (k = 1, 3) of the lower (k < 2) / upper half
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int e = (ch + 8 * (k & 1)) * TH + (k >= 2 ? NH : 0);
+            const u64 y = bload64(ry, tid * 8, e * 8);
+            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b8(rv, tid, e, 0);
+            const u64 t = y + (v ? negQ : 0);
+            x[k] = t >= 2 * m ? t - 2 * m : t;
+        }
+        fwd_quad_first2<TH>(x, w4, m, lazy, lds, tid, ch, hi);
+    }
+}
+
 // (b1') ModUp + NTT with half the limb in LDS (68 KiB at N = 16384): two workgroups share a CU,
 // so one's loads and base conversion overlap the other's NTT.  Stage 0 of the forward NTT pairs
 // coefficient e with e + N/2; each thread converts both, applies that butterfly in registers, keeps
@@ -893,6 +918,8 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
         // the usual digit (P = 3 limbs, pseudo-Mersenne target): compile-time digit size, buffer loads
         // whose limb / chunk offsets are scalar (no per-load address arithmetic on the VALU)
         modup_convert3x<LOGN, B59>(yb, T.modup_xt + (size_t)pt * 4, R, tw, tid, lds, hi);
+    } else if (DP == 1 && B59) {   // one-limb digits on a 59-bit chain: radix-4 first stages
+        modup_convert1_r4<LOGN>(yb, vb, negQ, m, lazy_of<LOGN, B59>(R), tw, tid, lds, hi);
     } else if (DP == 1 && ns == 1 && PK(T, s0).q <= 3 * m) {   // y + v negQ < q_u + m <= 4 m: the NTT's input bound
         modup_convert1<LOGN>(yb, vb, negQ, m, w0, w0p, tid, lds, hi);
     } else {
@@ -954,7 +981,7 @@ __device__ __forceinline__ void modup_h_body(const DevTables& T, const u64* acoe
         }
         __syncthreads();
         // the radix-4 conversion (modup_convert3x, FHS_MODUP_R4) did each half's local stage 0 already
-        constexpr int S0 = DP == 3 ? 1 : 0;
+        constexpr int S0 = (DP == 3 || (DP == 1 && B59)) ? 1 : 0;
         // wave-local tail: no barriers between the passes with TL <= 64, none before the stores
         constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, FHS_MODUPH_RL, S0>();
         ntt_fwd_lds<LOGN - 1, FHS_MODUPH_RL, 16, S0, WLX>(lds, tid, tw, m, lazy_of<LOGN, B59>(R), 1 + h);

@@ -5,7 +5,7 @@
 #   tests[=pytest args]     GPU suite (default: all of tests/ -m gpu; args may quote, e.g. -k 'a or b')
 #   smoke                   __graft_entry__.smoke()                              -> OUT/smoke.log
 #   bench[=bench args]      one bench line (default: the driver's default line)  -> OUT/bench.json
-#   ab=NAME[:ENV=v,ENV=v]   cfg2 matvec-only bench under extra environment       -> OUT/ab_NAME.json
+#   ab=NAME[:ENV=v,ENV=v]   cfg2 matvec-only bench under extra environment (AB_ARGS: more bench args) -> OUT/ab_NAME.json
 #   trace[=bench args]      rocprofv3 --kernel-trace --stats of a matvec-only bench -> OUT/trace_<config>/,
 #                           OUT/rocprof_summary_<config>.json (tools/rocprof_summary.py: per-dispatch
 #                           steady state of the timed steps)
@@ -46,7 +46,7 @@ for step in "$@"; do
         v=${arg%%:*}
         envs=""
         [ "$v" != "$arg" ] && envs=$(echo "${arg#*:}" | tr ',' ' ')
-        env $envs timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 $MV > "$OUT/ab_$v.log" 2>&1 || fail "ab $v" "$OUT/ab_$v.log"
+        env $envs timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 $MV $AB_ARGS > "$OUT/ab_$v.log" 2>&1 || fail "ab $v" "$OUT/ab_$v.log"
         grep '^{' "$OUT/ab_$v.log" | tail -1 > "$OUT/ab_$v.json"
         python3 tools/show_bench.py "$OUT/ab_$v.json" "$v" ;;
     trace)
