@@ -220,6 +220,49 @@ def ntt_butterflies_per_matvec(cfg, l):
     return B * (dn * E - l) * (N // 2) * logn
 
 
+PHASE = ["start"]
+
+
+def heartbeat(rank, every=45.0):
+    """A progress line on stderr every `every` s from rank 0 (the GPU pool kills a command that writes nothing
+    for 3 minutes; an 8-rank rehearsal sharing one GPU can spend that long in one leg)."""
+    import threading
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(every)
+            mem = ""
+            try:   # device memory in use by every process on this GPU (ranks sharing one GPU in a rehearsal)
+                import torch
+                free, total = torch.cuda.mem_get_info()
+                mem = f", device memory used {(total - free) / 2**30:.1f} of {total / 2**30:.0f} GiB"
+            except Exception:
+                pass
+            print(f"bench: rank {rank} in {PHASE[0]} at {time.time() - t0:.0f} s{mem}", file=sys.stderr, flush=True)
+
+    if rank == 0:
+        threading.Thread(target=beat, daemon=True).start()
+
+
+def leg_failed(rank, e):
+    print(f"bench: rank {rank} leg {PHASE[0]!r} failed: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+
+
+def phase(name):
+    # each leg starts from the memory it needs: the previous leg's contexts (and their allocation caches) are
+    # destroyed when collected, torch's cached blocks go back to the device (ranks sharing one GPU in a rehearsal)
+    import gc
+    gc.collect()
+    if "torch" in sys.modules:
+        import torch
+        if torch.cuda.is_initialized():
+            torch.cuda.empty_cache()
+    PHASE[0] = name
+    print(f"bench: {name}", file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,6 +296,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    heartbeat(rank)
     os.environ.setdefault("FHESPEAR_DEVICE", str(local))
     dist = None
     # FHESPEAR_BENCH_DIST=1 under torchrun at world 1: the multi-rank step (RCCL gather to rank 0) on one
@@ -262,7 +306,10 @@ def main():
         import torch.distributed as dist
         if os.environ.get("FHESPEAR_DIST_BACKEND", "nccl") == "gloo":
             # rehearsal only (several ranks sharing one GPU, host-staged exchange); timings meaningless
-            dist.init_process_group("gloo")
+            import datetime
+            # a rank whose leg failed alone leaves the others in a collective: bounded wait, not gloo's 30 min
+            dist.init_process_group("gloo", timeout=datetime.timedelta(
+                seconds=int(os.environ.get("FHESPEAR_GLOO_TIMEOUT", "600"))))
             local = int(os.environ.get("FHESPEAR_DEVICE", "0"))
             torch.cuda.set_device(local)
         else:
@@ -287,6 +334,7 @@ def main():
     N, L0, P, D = cfg["N"], cfg["L0"], cfg["P"], cfg["D"]
     G, B = bsgs_params(D)
     steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    phase(f"{args.config} setup")
     primes = ph.create_coeff_modulus(N, [59] * (L0 + P))
     parms = ph.params(ph.scheme_type.ckks)
     parms.set_poly_modulus_degree(N)
@@ -336,9 +384,11 @@ def main():
                 gathered[0] = fhespear_dist.gather_to_root(tdist, gather_buf, world, rank)
         return y
 
+    phase(f"{args.config} warmup")
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
+    phase(f"{args.config} timed steps")
 
     def barrier():
         if dist is not None:
@@ -435,9 +485,11 @@ def main():
         del ctx
         released = True
         try:
+            phase("seal leg")
             seal = seal_leg(args, ph, cfg)
         except Exception as e:   # reported, never hidden
             seal = {"error": f"{type(e).__name__}: {e}"[:400]}
+            leg_failed(rank, e)
     block = None
     if not args.no_block and args.config == "cfg2":
         # the metric's second half, measured: one client-aided RWKV-7 block (cfg3 shapes) on the same
@@ -448,17 +500,21 @@ def main():
             del ctx
             released = True
         try:
+            phase("block leg")
             block = run_block(args, ph, tdist, rank, world, local, args.block_steps, 1,
                               capture=world == 1 and not args.no_cpu_baseline)
         except Exception as e:   # reported, never hidden: the matvec line stands on its own
             block = {"error": f"{type(e).__name__}: {e}"[:400]}
+            leg_failed(rank, e)
         if world > 1:
             # north_star: "baby-step rotations are computed once and broadcast" -- the FFN key pair's shared
             # baby steps in that mode too (the line above recomputes them on each owning rank)
             try:
+                phase("block leg, broadcast baby steps")
                 bb = run_block(args, ph, tdist, rank, world, local, args.block_steps, 1, baby_mode="broadcast")
             except Exception as e:   # reported, never hidden
                 bb = {"error": f"{type(e).__name__}: {e}"[:400]}
+                leg_failed(rank, e)
             if rank == 0 and isinstance(block, dict):
                 block["baby_broadcast"] = bb
     cfg5 = None
@@ -469,9 +525,11 @@ def main():
             del ctx
             released = True
         try:
+            phase("cfg5 leg")
             cfg5 = run_cfg5(args, ph, tdist, rank, world, local)
         except Exception as e:   # reported, never hidden
             cfg5 = {"error": f"{type(e).__name__}: {e}"[:400]}
+            leg_failed(rank, e)
     if rank == 0:
         total = args.steps * world
         mean_value = total / elapsed
@@ -572,6 +630,7 @@ def main():
             "parity": parity,
         }
         if world == 1 and not args.no_cpu_baseline:
+            phase("cpu baseline")
             res["cpu_baseline"] = cpu_baseline(cfg, [int(q) for q in primes], args, cfg.get("mode", "exact"))
             if seal is not None and "error" not in seal:
                 # the SEAL-convention leg's own CPU baseline: the same matvec in the same convention

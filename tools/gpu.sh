@@ -12,7 +12,7 @@
 #   pmc[=config]            FETCH_SIZE, WRITE_SIZE and VALU counter passes (one rocprofv3 run each)
 #                           -> OUT/pmc_traffic_<config>.json, OUT/pmc_valu_<config>.json
 #   stall[=config]          wave-cycle attribution passes (SQ_WAIT_*, LDS, instruction mix) -> OUT/pmc_stall_<config>.json
-#   rehearse=N[:bench args] N ranks sharing this one GPU (gloo, host-staged exchange; timings
+#   rehearse=N[:bench args] N ranks sharing this one GPU (gloo, host-staged exchange, 2 GiB allocation cache per rank; timings
 #                           meaningless): bench.py --gpus N self-launches them -> OUT/rehearse_nN.json
 #   dist1[=NAME[:ENV=v,..]] matvec bench at world 1 under torchrun with the RCCL gather step -> OUT/NAME.json
 #   py=SCRIPT[:args]        python SCRIPT args                                  -> OUT/py_<name>.log
@@ -99,7 +99,7 @@ for step in "$@"; do
         n=${arg%%:*}
         a=""
         [ "$n" != "$arg" ] && a=${arg#*:}
-        FHESPEAR_DIST_BACKEND=gloo FHESPEAR_DEVICE=0 timeout -k 10 900 python bench.py --gpus "$n" $a \
+        FHESPEAR_DIST_BACKEND=gloo FHESPEAR_DEVICE=0 FHESPEAR_CACHE_BYTES=${FHESPEAR_CACHE_BYTES:-2147483648} timeout -k 10 1100 python bench.py --gpus "$n" $a \
             > "$OUT/rehearse_n$n.log" 2>&1 || fail "rehearse $n" "$OUT/rehearse_n$n.log"
         grep '^{' "$OUT/rehearse_n$n.log" | tail -1 > "$OUT/rehearse_n$n.json"
         python3 tools/show_bench.py "$OUT/rehearse_n$n.json" ;;
