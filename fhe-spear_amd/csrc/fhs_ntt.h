@@ -140,7 +140,7 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
 #define FHS_NTT_WAVELOCAL 1
 #endif
 template <int LOGN, int S, int R>
-constexpr int pass_tl() { return ((1 << LOGN) >> (S + 1)) >> (R - 1); }
+constexpr int pass_tl() { return R > 0 ? ((1 << LOGN) >> (S + 1)) >> (R - 1) : 0; }
 // lanes of a wave that take part: 64, or all T = N / EPT threads when the transform has fewer (one wave)
 template <int LOGN, int EPT>
 constexpr int wl_width() { return (1 << LOGN) / EPT < 64 ? (1 << LOGN) / EPT : 64; }
@@ -183,7 +183,7 @@ __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restric
         constexpr int R = pass_r<LOGN, RL, S>();
         inv_from<LOGN, RL, S + R, EPT, NOFOLD, WL, S0>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
         ntt_pass<LOGN, S, R, false, EPT, false, NOFOLD>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
-        if constexpr (WL && S - RL >= S0 && pass_tl<LOGN, S, R>() <= wl_width<LOGN, EPT>() &&
+        if constexpr (WL && R == RL && S - RL >= S0 && pass_tl<LOGN, S, R>() <= wl_width<LOGN, EPT>() &&
                       pass_tl<LOGN, S - RL, RL>() <= wl_width<LOGN, EPT>())
             __builtin_amdgcn_wave_barrier();
         else

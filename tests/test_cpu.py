@@ -424,6 +424,19 @@ def test_device_ntt_passes_emulated_match_direct_evaluation(tmp_path):
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
 
 
+def test_wave_local_passes_touch_only_their_waves_elements(tmp_path):
+    """The barriers fhs_ntt.h's wave-local passes drop (fwd_from / inv_from with WL, the wave-local exits
+    and heads the ModUp / INTT kernels rely on) are safe: with fhs_ntt.h's own ntt_pass run thread by thread
+    and the LDS array diffed, every element a thread touches after a dropped barrier was written by its own
+    wave (64 lanes, or every thread of a one-wave transform) -- tools/debug/wl_check.cpp."""
+    import subprocess
+    exe = tmp_path / "wl_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-DFHS_ASM_SHOUP=0", f"-I{REPO / 'tools/debug/shim'}",
+                    f"-I{REPO / 'fhe-spear_amd/csrc'}", str(REPO / "tools/debug/wl_check.cpp"), "-o", str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout
+
+
 def _sm64(x):
     M = (1 << 64) - 1
     x = (x + 0x9E3779B97F4A7C15) & M

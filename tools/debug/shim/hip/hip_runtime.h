@@ -14,4 +14,5 @@ static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((
 static inline unsigned __umulhi(unsigned a, unsigned b) { return (unsigned)(((uint64_t)a * b) >> 32); }
 #define __builtin_amdgcn_readfirstlane(x) (x)
 static inline void __syncthreads() {}
+static inline void __builtin_amdgcn_wave_barrier() {}
 static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
