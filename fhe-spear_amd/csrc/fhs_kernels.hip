@@ -46,6 +46,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_MODUP_CH 4         // k_modup (full-limb form): coefficients per conversion chunk
 #define FHS_MODUP_RL 4         // k_modup (full-limb form): radix (log2) of the NTT register passes
 #define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
+#ifndef FHS_KSIP_HALVES
+#define FHS_KSIP_HALVES 1      // k_ks_ip (hoisted): coefficient halves outermost (L2 reuse of the extension)
+#endif
 
 namespace fhs {
 
@@ -1130,7 +1133,22 @@ __global__ void __launch_bounds__(256) k_ks_ip(DevTables T, const KsItem* items,
     // limbs would leave 5 of them idle)
     if (!(t0 > 0 ? plain_tm(E - t0, R * NB, t, m) : xcd_touter(E - t0, R * NB, t, m))) return;
     t += t0;
-    const int r = m / NB, n = ((m % NB) << 8) + threadIdx.x;
+    int r, nb;
+    if (FHS_KSIP_HALVES && t0 == 0 && NB >= 2 && (size_t)dn * N * 8 > ((size_t)3 << 20)) {
+        // half-major: every rotation's lower coefficient half, then every rotation's upper half.  A rotation
+        // X -> X^(5^g) maps NTT slot exponents 2 rev(n) + 1 = 1 mod 4 (n < N/2) to 1 mod 4 again, so each half
+        // reads only its own half of the shared extension: the limb's working set on its XCD halves (SEAL's
+        // convention: 36 one-limb digits x 128 KiB = 4.6 MiB per limb, over the 4 MiB L2; 2.3 MiB per half).
+        // Only where the limb's extension would not fit the L2 anyway: the default convention's 12 digits
+        // (1.5 MiB) measured 2 % slower half-major (profiles/r05/ab_seal_perm_halves)
+        const int hb = NB >> 1, h = m / (R * hb), k = m % (R * hb);
+        r = k / hb;
+        nb = h * hb + k % hb;
+    } else {
+        r = m / NB;
+        nb = m % NB;
+    }
+    const int n = (nb << 8) + threadIdx.x;
     const int pt = t < l ? t : T.L0 + (t - l);
     const RedU RD = redu(PK(T, pt));
     const KsItem it = items[r];
@@ -1489,17 +1507,53 @@ static void seal_rewrite(const DevTables& T, KsItem* items, int R, const u64** u
         it.src = (u64)r;
     }
 }
+// up to kPermBatch permutations per launch, passed by value (one launch per 32 polynomials instead of one each:
+// the giant steps' 2 (B - 1) permutations were 88 launches of ~5 us at cfg2)
+constexpr int kPermBatch = 32;
+struct PermBatch {
+    const u64* in[kPermBatch];
+    u64* out[kPermBatch];
+    u64 elt[kPermBatch];
+};
+__global__ void __launch_bounds__(256) k_galois_perm_batch(DevTables T, PermBatch pb, int limbs) {
+    const int y = blockIdx.y;
+    const u64* in = pb.in[y];
+    u64* out = pb.out[y];
+    const u64 elt = pb.elt[y];
+    const size_t S = (size_t)limbs * T.N;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < S; idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t base = idx - idx % T.N;
+        out[idx] = in[base + galois_src((int)(idx % T.N), elt, T.logN)];
+    }
+}
 static hipError_t seal_permute(const DevTables& T, const KsItem* orig, int R, int l, u64* perm, hipStream_t st) {
     const size_t S = (size_t)l * T.N;
+    PermBatch pb;
+    int n = 0;
+    const int gx = std::max(1, eltwise_grid(S) / 8);
+    auto flush = [&]() -> hipError_t {
+        if (!n) return hipSuccess;
+        hipLaunchKernelGGL(k_galois_perm_batch, dim3(gx, n), dim3(256), 0, st, T, pb, l);
+        n = 0;
+        return hipGetLastError();
+    };
     for (int r = 0; r < R; ++r) {
         const KsItem& it = orig[r];
         if (it.elt == 1) continue;
         u64* pc = perm + (size_t)r * 2 * S;
-        hipError_t e = launch_galois_perm(T, it.a, pc + S, l, it.elt, st);
-        if (e == hipSuccess && it.add0) e = launch_galois_perm(T, it.add0, pc, l, it.elt, st);
-        if (e != hipSuccess) return e;
+        for (int c = 1; c >= 0; --c) {
+            const u64* src = c ? it.a : it.add0;
+            if (!src) continue;
+            pb.in[n] = src;
+            pb.out[n] = pc + (c ? S : 0);
+            pb.elt[n] = it.elt;
+            if (++n == kPermBatch) {
+                hipError_t e = flush();
+                if (e != hipSuccess) return e;
+            }
+        }
     }
-    return hipSuccess;
+    return flush();
 }
 
 // key-switch workspace carve: acoef | ext | acc | ycoef | centred counts (ks_core_bytes)
