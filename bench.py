@@ -649,10 +649,55 @@ def main():
             block.pop("_capture", None)
         if isinstance(seal, dict):
             seal.pop("_primes", None)
+        res["schema_errors"] = line_schema_errors(res)
         print(json.dumps(res))
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def line_schema_errors(res):
+    """What the driver's N > 1 runs must carry, checked on the line itself and, by
+    tests/test_cpu.py, on the committed rehearsal records: world size and one device record (with its PCI bus
+    id) per rank; per-kind exchange records {calls, MB, ms}; the block leg with its baby-step mode (both modes
+    at N > 1); the cfg5 leg with per-block seconds, bootstrap seconds and a digest compared with the one-rank
+    digest.  A leg that failed carries {"error"} instead and is reported as such.  [] when complete."""
+    err = []
+    n = res.get("n_gpus")
+    rk = res.get("ranks") or {}
+    if rk.get("world_size") != n:
+        err.append(f"ranks.world_size {rk.get('world_size')} != n_gpus {n}")
+    devs = rk.get("devices") or []
+    if len(devs) != n or any("pci_bus_id" not in d for d in devs):
+        err.append("ranks.devices: one record with pci_bus_id per rank")
+
+    def exchange_ok(ex, where):
+        if not isinstance(ex, dict) or not all(isinstance(v, dict) and set(v) == {"calls", "MB", "ms"}
+                                               for v in ex.values()):
+            err.append(f"{where}: per-kind {{calls, MB, ms}}")
+
+    if n and n > 1:
+        exchange_ok(res.get("exchange_per_step"), "exchange_per_step")
+    blk = res.get("rwkv_block")
+    if isinstance(blk, dict) and "error" not in blk:
+        if blk.get("baby_mode") not in ("recompute", "broadcast"):
+            err.append("rwkv_block.baby_mode")
+        if n and n > 1:
+            exchange_ok(blk.get("exchange_per_block_rank0"), "rwkv_block.exchange_per_block_rank0")
+            bb = blk.get("baby_broadcast")
+            if not isinstance(bb, dict) or ("error" not in bb and bb.get("baby_mode") != "broadcast"):
+                err.append("rwkv_block.baby_broadcast (north_star's broadcast baby steps, timed at N > 1)")
+    c5 = res.get("cfg5_chain")
+    if isinstance(c5, dict) and "error" not in c5:
+        for k in ("sec_per_block_median", "block_seconds", "bootstrap_seconds", "blocks", "n_gpus"):
+            if k not in c5:
+                err.append(f"cfg5_chain.{k}")
+        par = c5.get("parity") or {}
+        if "ct_sha256" not in par or "matches_one_rank" not in par:
+            err.append("cfg5_chain.parity {ct_sha256, matches_one_rank}")
+        if n and n > 1:
+            exchange_ok(c5.get("exchange_per_block_rank0"), "cfg5_chain.exchange_per_block_rank0")
+    return err
 
 
 def seal_leg(args, ph, cfg):

@@ -143,3 +143,30 @@ def test_pmc_stall_shares(tmp_path):
     # per step: 2048 x 8 VALU quad-cycles x 4 over 1024 SIMDs x (512 per pass, 2 passes -> 512) / 8 cycles
     assert rec["valu_busy"] == round(2048 * 8 * 4 / (1024 * 512 / 8), 3)
     assert rec["bank_conflict_cycles_per_lds_inst"] == 1.7 and rec["lds_per_valu"] == 0.1
+
+
+@pytest.mark.parametrize("record", ["rehearse_n8_gloo_one_gpu_matvec_cfg5.json",
+                                    "rehearse_n8_gloo_one_gpu_matvec_block.json",
+                                    "rehearse_n2_gloo_one_gpu.json"])
+def test_multi_rank_line_schema_on_the_rehearsal_records(record):
+    """the fields the driver's first 8-GPU run must carry -- world size, a device record
+    with its PCI bus id per rank, per-kind exchange {calls, MB, ms} for the matvec, block and cfg5 legs, the
+    block in both baby-step modes, the cfg5 digest against the one-rank digest -- pinned by bench.py's own
+    checker (which also stamps `schema_errors` into every line) on the committed world-2 / world-8
+    rehearsals (8 gloo ranks sharing one GPU: the matvec + cfg5 legs and the matvec + block legs ran as two
+    records, the ranks' memory together exceeding one GPU's 288 GB with all legs at once)."""
+    res = json.loads((REPO / "profiles" / "r05" / record).read_text())
+    assert bench.line_schema_errors(res) == []
+    if "cfg5" in record:
+        assert res["cfg5_chain"]["parity"]["matches_one_rank"] is True
+    if res.get("rwkv_block"):
+        assert res["rwkv_block"]["baby_broadcast"]["baby_mode"] == "broadcast"
+
+
+def test_multi_rank_line_schema_reports_what_is_missing():
+    res = json.loads((REPO / "profiles" / "r05" / "rehearse_n8_gloo_one_gpu_matvec_block.json").read_text())
+    res["ranks"]["devices"] = res["ranks"]["devices"][:7]
+    del res["rwkv_block"]["baby_broadcast"]
+    res["exchange_per_step"]["gather"].pop("ms")
+    err = bench.line_schema_errors(res)
+    assert len(err) == 3 and any("pci_bus_id" in e for e in err) and any("baby_broadcast" in e for e in err)
