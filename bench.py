@@ -223,7 +223,7 @@ def ntt_butterflies_per_matvec(cfg, l):
 PHASE = ["start"]
 
 
-def heartbeat(rank, every=45.0):
+def heartbeat(rank, local, every=45.0):
     """A progress line on stderr every `every` s from rank 0 (the GPU pool kills a command that writes nothing
     for 3 minutes; an 8-rank rehearsal sharing one GPU can spend that long in one leg)."""
     import threading
@@ -234,9 +234,13 @@ def heartbeat(rank, every=45.0):
         while True:
             time.sleep(every)
             mem = ""
-            try:   # device memory in use by every process on this GPU (ranks sharing one GPU in a rehearsal)
+            try:   # device memory in use by every process on this GPU (ranks sharing one GPU in a rehearsal);
+                # only once torch has initialised the device itself, and named explicitly (this thread's
+                # current device is not the main thread's)
                 import torch
-                free, total = torch.cuda.mem_get_info()
+                if not torch.cuda.is_initialized():
+                    raise RuntimeError
+                free, total = torch.cuda.mem_get_info(local)
                 mem = f", device memory used {(total - free) / 2**30:.1f} of {total / 2**30:.0f} GiB"
             except Exception:
                 pass
@@ -296,7 +300,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    heartbeat(rank)
+    heartbeat(rank, local)
     os.environ.setdefault("FHESPEAR_DEVICE", str(local))
     dist = None
     # FHESPEAR_BENCH_DIST=1 under torchrun at world 1: the multi-rank step (RCCL gather to rank 0) on one
