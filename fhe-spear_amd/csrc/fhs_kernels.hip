@@ -46,6 +46,9 @@ typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
 #define FHS_MODUP_CH 4         // k_modup (full-limb form): coefficients per conversion chunk
 #define FHS_MODUP_RL 4         // k_modup (full-limb form): radix (log2) of the NTT register passes
 #define FHS_NTT_RL 3           // radix (log2) for the other NTT kernels
+#ifndef FHS_FWD_FIRST3
+#define FHS_FWD_FIRST3 1       // half-limb forward transforms at N = 32768: global stages 0-2 in registers
+#endif
 #ifndef FHS_KSIP_HALVES
 #define FHS_KSIP_HALVES 1      // k_ks_ip (hoisted): coefficient halves outermost (L2 reuse of the extension)
 #endif
@@ -202,6 +205,43 @@ __device__ __forceinline__ void fwd_quad_first2(u64 x[4], const Tw4& w, u64 q, b
     hi[c] = x[2] + tb;
     hi[c + 8] = x[2] + (q2 - tb);
 }
+// Radix-8 first stages (N = 32768): the half transforms have 14 stages, which start-at-1 splits 3+3+3+3+1 (a
+// radix-2 pass, and no wave-local exit); with global stages 0-2 in registers they start at local stage 2: four
+// radix-8 passes, the last three wave-local.  x[k] = element e + k N/8 (e = tid + c TH, c < 4: rows c + 4k of
+// the lower half for k < 4, of the upper half for k >= 4), each < 2q; stage s twiddle psi^rev(2^s + block).
+// Lower-half results to LDS rows c, c + 4, c + 8, c + 12, upper-half results to hi[] at the same rows.
+template <int TH>
+__device__ __forceinline__ void fwd_oct_first3(u64 x[8], const u64* __restrict__ tw, u64 q, bool lazy, u64* lds,
+                                               int tid, int c, u64 hi[16]) {
+    const u64 q2 = 2 * q;
+    auto bfly = [&](int a, int b, int wi) {
+        u64 w, wp;
+        ld_tw(tw, wi, w, wp);
+        u64 X = x[a];
+        if (!lazy) X = X >= q2 ? X - q2 : X;
+        const u64 t = shoup_lazy(x[b], w, wp, q);
+        x[a] = X + t;
+        x[b] = X + (q2 - t);
+    };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bfly(k, k + 4, 1);   // global stage 0: (e, e + N/2)
+#pragma unroll
+    for (int k = 0; k < 8; k += 4) {                  // stage 1: (e, e + N/4) in each half
+        bfly(k, k + 2, 2 + k / 4);
+        bfly(k + 1, k + 3, 2 + k / 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) bfly(k, k + 1, 4 + k / 2);   // stage 2: (e, e + N/8) in each quarter
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        lds[row_pad<TH>(tid, c + 4 * k)] = x[k];
+        hi[c + 4 * k] = x[4 + k];
+    }
+}
+// radix-8 first stages where they leave the half transforms whole radix-8 passes and radix-4 would not
+template <int LOGN>
+constexpr bool fwd_first3() { return (LOGN - 2) % 3 != 0 && (LOGN - 3) % 3 == 0; }
+
 // The inverse counterpart: the last two stages of a half-limb inverse in registers.  x = {half 0 row c,
 // half 0 row c + 8, half 1 row c, half 1 row c + 8} (each < 2q, after the halves' LDS passes from local
 // stage 1 on): the halves' local stage 0 (twiddle psi^-rev(2) / psi^-rev(3)), then the global stage 0
@@ -239,13 +279,25 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
         for (int c = 0; c < 16; ++c) store(tid + c * TH, fwd_canon(lds[row_pad<TH>(tid, c)], R));
     } else {
         constexpr int NH = N / 2, TH = N / 32;
-        const Tw4 w4 = ld_tw4(tw);
+        constexpr bool F3 = FHS_FWD_FIRST3 && fwd_first3<LOGN>();
+        constexpr int S0 = F3 ? 2 : 1;
         u64 hi[16];
+        if constexpr (F3) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {   // rows c, c + 8 of both halves: global stages 0-1 in registers
-            const int e = tid + c * TH;
-            u64 x[4] = {load(e), load(e + 8 * TH), load(e + NH), load(e + NH + 8 * TH)};
-            fwd_quad_first2<TH>(x, w4, R.q, R.lazy, lds, tid, c, hi);
+            for (int c = 0; c < 4; ++c) {   // rows c + 4k of both halves: global stages 0-2 in registers
+                u64 x[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[k] = load(tid + (c + 4 * k) * TH);
+                fwd_oct_first3<TH>(x, tw, R.q, R.lazy, lds, tid, c, hi);
+            }
+        } else {
+            const Tw4 w4 = ld_tw4(tw);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {   // rows c, c + 8 of both halves: global stages 0-1 in registers
+                const int e = tid + c * TH;
+                u64 x[4] = {load(e), load(e + 8 * TH), load(e + NH), load(e + NH + 8 * TH)};
+                fwd_quad_first2<TH>(x, w4, R.q, R.lazy, lds, tid, c, hi);
+            }
         }
 #pragma unroll 1
         for (int h = 0; h < 2; ++h) {
@@ -255,8 +307,8 @@ __device__ __forceinline__ void fwd_limb(u64* lds, int tid, const u64* __restric
                 for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
             }
             __syncthreads();
-            constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, 3, 1>();
-            ntt_fwd_lds<LOGN - 1, 3, 16, 1, WLX>(lds, tid, tw, R.q, R.lazy, 1 + h);
+            constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, 3, S0>();
+            ntt_fwd_lds<LOGN - 1, 3, 16, S0, WLX>(lds, tid, tw, R.q, R.lazy, 1 + h);
             if constexpr (WLX) {   // this wave's own outputs (wave-local tail, fhs_ntt.h)
                 const int wb = wl_base<LOGN - 1, 16, 8>(tid), wp = lds_pad(wb);
 #pragma unroll

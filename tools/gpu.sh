@@ -6,6 +6,7 @@
 #   smoke                   __graft_entry__.smoke()                              -> OUT/smoke.log
 #   bench[=bench args]      one bench line (default: the driver's default line)  -> OUT/bench.json
 #   ab=NAME[:ENV=v,ENV=v]   cfg2 matvec-only bench under extra environment (AB_ARGS: more bench args) -> OUT/ab_NAME.json
+#   abx=NAME[:ENV=v,ENV=v]  bench with AB_ARGS only (no matvec-only flags)           -> OUT/ab_NAME.json
 #   trace[=bench args]      rocprofv3 --kernel-trace --stats of a matvec-only bench -> OUT/trace_<config>/,
 #                           OUT/rocprof_summary_<config>.json (tools/rocprof_summary.py: per-dispatch
 #                           steady state of the timed steps)
@@ -47,6 +48,14 @@ for step in "$@"; do
         envs=""
         [ "$v" != "$arg" ] && envs=$(echo "${arg#*:}" | tr ',' ' ')
         env $envs timeout -k 10 300 python3 bench.py --steps 20 --warmup 3 $MV $AB_ARGS > "$OUT/ab_$v.log" 2>&1 || fail "ab $v" "$OUT/ab_$v.log"
+        grep '^{' "$OUT/ab_$v.log" | tail -1 > "$OUT/ab_$v.json"
+        python3 tools/show_bench.py "$OUT/ab_$v.json" "$v" ;;
+    abx)
+        # as ab, but the bench arguments are AB_ARGS alone (no matvec-only flags): e.g. the cfg5 leg
+        v=${arg%%:*}
+        envs=""
+        [ "$v" != "$arg" ] && envs=$(echo "${arg#*:}" | tr ',' ' ')
+        env $envs timeout -k 10 600 python3 bench.py $AB_ARGS > "$OUT/ab_$v.log" 2>&1 || fail "abx $v" "$OUT/ab_$v.log"
         grep '^{' "$OUT/ab_$v.log" | tail -1 > "$OUT/ab_$v.json"
         python3 tools/show_bench.py "$OUT/ab_$v.json" "$v" ;;
     trace)
