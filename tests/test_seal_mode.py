@@ -100,10 +100,12 @@ def _gpu_ctx(ph, N, bits, P, elts=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,L0", [(1024, 4), (8192, 24)])
+@pytest.mark.parametrize("N,L0", [(1024, 4), (8192, 24), (16384, 26)])
 def test_gpu_seal_mode_bit_exact_vs_oracle(ph, orc, N, L0):
     """Rotations (a batch of 5 of one input: each decomposed after its automorphism), relinearize and
-    the fused BSGS (its giant steps too) in SEAL mode, limb for limb against the oracle."""
+    the fused BSGS (its giant steps too) in SEAL mode, limb for limb against the oracle.  (16384, 26): a limb's
+    extension (26 one-limb digits x 128 KiB) exceeds 3 MiB, so the hoisted key inner product runs half-major
+    (FHS_KSIP_HALVES), at both levels."""
     bits = [59] * L0 + [60]
     D = 32
     G, B = 6, 6
