@@ -145,7 +145,7 @@ def test_pmc_stall_shares(tmp_path):
     assert rec["bank_conflict_cycles_per_lds_inst"] == 1.7 and rec["lds_per_valu"] == 0.1
 
 
-@pytest.mark.parametrize("record", ["rehearse_n8_gloo_one_gpu_matvec_cfg5.json",
+@pytest.mark.parametrize("record", ["rehearse_n4_gloo_one_gpu.json", "rehearse_n8_gloo_one_gpu_matvec_cfg5.json",
                                     "rehearse_n8_gloo_one_gpu_matvec_block.json",
                                     "rehearse_n2_gloo_one_gpu.json"])
 def test_multi_rank_line_schema_on_the_rehearsal_records(record):
