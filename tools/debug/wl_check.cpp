@@ -157,6 +157,7 @@ int main() {
     // whole limbs with S0 = 0, one-wave transforms (N = 1024: 64 threads -> wl_width 64; N = 512: 32)
     bad += check_fwd<13, 3, 16, 1>();
     bad += check_fwd<14, 3, 16, 1>();
+    bad += check_fwd<14, 3, 16, 2>();   // N = 32768 half limbs after the radix-8 first stages (fwd_oct_first3)
     bad += check_fwd<13, 3, 16, 0>();
     bad += check_fwd<12, 3, 16, 0>();
     bad += check_fwd<10, 3, 16, 1>();
