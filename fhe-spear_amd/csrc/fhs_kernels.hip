@@ -2283,7 +2283,41 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_small(DevTables
                                [&](int e) { const int v = sm[e]; return v >= 0 ? (u64)v : q - (u64)(-v); },
                                [&](int e, u64 v) { p[e] = v; });
 }
-__device__ __forceinline__ u64 dbl_mod(const DevTables& T, double d, int i);   // below, with the encoder
+// The limb's reduction of a 64-bit integer: on the pseudo-Mersenne fold one fold and one subtraction when
+// 2^b + (2^(64-b) - 1) d < 2q (every 59-bit chain: d < 2^27), else reduce64's three folds or Barrett -- the
+// same canonical residue either way.  The encoder's NTT loads reduce one rounded coefficient per element per
+// limb with it (k_ntt_fwd_from_dbl: ~12 % of the N = 32768 encode's VALU instructions were this reduction).
+struct DblMod {
+    const PrimeK* P;
+    const u64* pow2;   // 2^k mod q of this limb (DevTables::pow2 row)
+    u64 q, mask;
+    unsigned b, d;
+    bool fold1;
+};
+__device__ __forceinline__ DblMod dbl_mod_of(const DevTables& T, int i) {
+    const PrimeK& P = PK(T, i);
+    const u64 pm = P.pm, q = P.q;   // i may vary per lane (k_encode_reduce): no readfirstlane
+    const unsigned b = (unsigned)(pm & 127), d = (unsigned)((pm >> 8) & 0xFFFFFFFFu);
+    const bool fold1 = b != 0 && ((u64)d << (64 - b)) + (1ull << b) < 2 * q;
+    return DblMod{&P, T.pow2 + (size_t)i * 1088, q, b ? (1ull << b) - 1 : 0, b, d, fold1};
+}
+__device__ __forceinline__ u64 dbl_mod(const DblMod& M, double v) {
+    const bool neg = v < 0;
+    const double a = neg ? -v : v;
+    u64 r;
+    if (a < 9.2e18) {
+        const u64 x = (u64)a;
+        r = M.fold1 ? csub((x & M.mask) + mul32w((uint32_t)(x >> M.b), M.d), M.q) : reduce64(x, *M.P);
+    } else {
+        const PrimeK& P = *M.P;
+        const u64 bits = (u64)__double_as_longlong(a);
+        const int ex = (int)((bits >> 52) & 0x7FF) - 1075;
+        const u64 mant = (bits & ((1ULL << 52) - 1)) | (1ULL << 52);
+        r = mulmod(reduce64(mant, P), M.pow2[ex], P);
+    }
+    return (neg && r) ? M.q - r : r;
+}
+__device__ __forceinline__ u64 dbl_mod(const DevTables& T, double d, int i) { return dbl_mod(dbl_mod_of(T, i), d); }
 // encode + encrypt fused: NTT(m + e) of the rounded message coefficients (coef, doubles; k_encode's
 // coef_out, reduced per limb by dbl_mod as k_ntt_fwd_from_dbl does) plus the small error -- the NTT is
 // linear and its outputs canonical, so the limbs equal NTT(m) + NTT(e) mod q, i.e. encode then encrypt
@@ -2298,10 +2332,11 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_msg_err(DevTabl
     const signed char* sm = small + (size_t)blockIdx.y * N;
     u64* p = out + ((size_t)blockIdx.y * limbs + b) * N;
     const u64 q = R.q;
+    const DblMod M = dbl_mod_of(T, b);
     fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
                                [&](int e) {   // < 2q: inside the forward NTT's input bound
                                    const int v = sm[e];
-                                   return dbl_mod(T, cf[e], b) + (v >= 0 ? (u64)v : q - (u64)(-v));
+                                   return dbl_mod(M, cf[e]) + (v >= 0 ? (u64)v : q - (u64)(-v));
                                },
                                [&](int e, u64 v) { p[e] = v; });
 }
@@ -2401,21 +2436,6 @@ hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u6
 
 // exact residue of integral doubles: coef [count][N] -> out [count][l][N] (coefficient form)
 // exact residue of an integral double (any magnitude) mod prime i
-__device__ __forceinline__ u64 dbl_mod(const DevTables& T, double d, int i) {
-    const PrimeK& P = PK(T, i);
-    const bool neg = d < 0;
-    const double a = neg ? -d : d;
-    u64 r;
-    if (a < 9.2e18) {
-        r = reduce64((u64)a, P);
-    } else {
-        const u64 bits = (u64)__double_as_longlong(a);
-        const int ex = (int)((bits >> 52) & 0x7FF) - 1075;
-        const u64 mant = (bits & ((1ULL << 52) - 1)) | (1ULL << 52);
-        r = mulmod(reduce64(mant, P), T.pow2[(size_t)i * 1088 + ex], P);
-    }
-    return (neg && r) ? P.q - r : r;
-}
 
 __global__ void k_encode_reduce(DevTables T, const double* coef, int count, u64* out, int l) {
     const int N = T.N;
@@ -2669,8 +2689,9 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_from_dbl(DevTab
     const RedU R = redu(PK(T, b));
     const double* cf = coef + (size_t)blockIdx.y * N;
     u64* p = ptrs[blockIdx.y] + (size_t)b * N;
+    const DblMod M = dbl_mod_of(T, b);
     fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
-                               [&](int e) { return dbl_mod(T, cf[e], b); }, [&](int e, u64 v) { p[e] = v; });
+                               [&](int e) { return dbl_mod(M, cf[e]); }, [&](int e, u64 v) { p[e] = v; });
 }
 
 hipError_t launch_encode_coef(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,

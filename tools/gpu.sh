@@ -18,6 +18,7 @@
 #   dist1[=NAME[:ENV=v,..]] matvec bench at world 1 under torchrun with the RCCL gather step -> OUT/NAME.json
 #   py=SCRIPT[:args]        python SCRIPT args                                  -> OUT/py_<name>.log
 #   exe=BINARY              a prebuilt microbenchmark                          -> OUT/exe_<name>.log
+#   pstall=SCRIPT[:args]    the stall passes over a script's kernels (KREGEX)       -> OUT/pmc_stall_<name>.json
 #   ptrace=SCRIPT[:args]    the same under rocprofv3 --kernel-trace --stats      -> OUT/ptrace_<name>/
 set -o pipefail
 OUT=gpurun_out/$1
@@ -93,6 +94,22 @@ for step in "$@"; do
         done
         python3 tools/pmc_stall.py "$OUT/pmc_stall_$cfg.json" 7 "$OUT/stall_1/run_counter_collection.csv" \
             "$OUT/stall_2/run_counter_collection.csv" || exit 1 ;;
+    pstall)
+        # the same two SQ passes over a script's kernels (KREGEX: which kernels) -> OUT/pmc_stall_<script>.json
+        s=${arg%%:*}
+        a=""
+        [ "$s" != "$arg" ] && a=${arg#*:}
+        b=$(basename "$s" .py)
+        K=${KREGEX:-k_ntt_fwd_from_dbl|k_modup_h}
+        i=0
+        for c in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE" \
+                 "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"; do
+            i=$((i + 1))
+            timeout -s KILL 400 rocprofv3 --kernel-include-regex "$K" --pmc $c -d "$OUT/pstall_$i" -o run \
+                --output-format csv -- python3 -u "$s" $a > "$OUT/pstall_$i.log" 2>&1 || fail "pstall pass $i" "$OUT/pstall_$i.log"
+        done
+        python3 tools/pmc_stall.py "$OUT/pmc_stall_$b.json" 1 "$OUT/pstall_1/run_counter_collection.csv" \
+            "$OUT/pstall_2/run_counter_collection.csv" || exit 1 ;;
     dist1)
         # the multi-rank step (RCCL gather, device-side stream ordering) at world 1 on this one GPU
         v=${arg%%:*}
