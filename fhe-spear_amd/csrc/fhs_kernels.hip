@@ -2318,6 +2318,14 @@ __device__ __forceinline__ u64 dbl_mod(const DblMod& M, double v) {
     return (neg && r) ? M.q - r : r;
 }
 __device__ __forceinline__ u64 dbl_mod(const DevTables& T, double d, int i) { return dbl_mod(dbl_mod_of(T, i), d); }
+// The encoder's forward NTTs start from inputs below 2q (a reduced coefficient, plus a small error when fused
+// with encryption), not the 4q the context's lazy bit assumes: every stage adds < 2q, so 15 lazy stages stay
+// below 2q + 30 q = 32 q <= 2^64 for q < 2^59 -- lazy at N = 32768 too, where the 4q bound (34 q) is not, with
+// the one-fold canonicalisation (pm_fold64 via fwd_canon) valid under DblMod::fold1.  Same canonical values.
+__device__ __forceinline__ RedU enc_lazy(RedU R, const DblMod& M) {
+    if (M.fold1 && R.q < (1ull << 59)) R.lazy = true;
+    return R;
+}
 // encode + encrypt fused: NTT(m + e) of the rounded message coefficients (coef, doubles; k_encode's
 // coef_out, reduced per limb by dbl_mod as k_ntt_fwd_from_dbl does) plus the small error -- the NTT is
 // linear and its outputs canonical, so the limbs equal NTT(m) + NTT(e) mod q, i.e. encode then encrypt
@@ -2333,7 +2341,7 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_msg_err(DevTabl
     u64* p = out + ((size_t)blockIdx.y * limbs + b) * N;
     const u64 q = R.q;
     const DblMod M = dbl_mod_of(T, b);
-    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, enc_lazy(R, M),
                                [&](int e) {   // < 2q: inside the forward NTT's input bound
                                    const int v = sm[e];
                                    return dbl_mod(M, cf[e]) + (v >= 0 ? (u64)v : q - (u64)(-v));
@@ -2690,7 +2698,7 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_from_dbl(DevTab
     const double* cf = coef + (size_t)blockIdx.y * N;
     u64* p = ptrs[blockIdx.y] + (size_t)b * N;
     const DblMod M = dbl_mod_of(T, b);
-    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, R,
+    fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, enc_lazy(R, M),
                                [&](int e) { return dbl_mod(M, cf[e]); }, [&](int e, u64 v) { p[e] = v; });
 }
 
