@@ -313,6 +313,7 @@ struct fhs_context {
     int pending_l = -1;
     std::set<const void*> pending_refs;   // inputs and outputs of queued rotations (destroy must flush)
     std::set<const void*> pending_outs;   // outputs of queued rotations (a consumer must flush)
+    int debug_fail_flushes = 0;           // fhs_debug_fail_next_flushes (testing hook)
     std::vector<std::complex<double>> fft_w;   // exp(2 pi i k / N), k < N
     std::vector<std::complex<double>> dec_twist;   // (cos, sin)(pi k / N), k < N
     std::vector<uint64_t> slot_index;          // (5^j mod 2N - 1)/2, j < N/2
@@ -375,6 +376,9 @@ struct fhs_ciphertext {
     uint64_t* d;
     int ncomp, ci, l;
     double scale;
+    // the queued rotation that was to produce it could not run (flush failed, e.g. out of memory): its limbs are
+    // undefined and every later use fails (drop_pending)
+    bool lost = false;
 };
 // One device block shared by the plaintexts of a batch (new_pts): a block per plaintext cost a hipMalloc per
 // diagonal and, once a chain walking down the levels pushed the cache over its cap, thousands of hipFree's
@@ -807,6 +811,20 @@ static hipError_t seal_prepare(fhs_context* c, std::vector<KsItem>& items, int l
 }
 
 // ---------------------------------------------------------------- deferred rotations
+// Every flush empties the queue.  One that cannot launch marks its outputs lost (every later use of them fails
+// loudly, live_ct) and no later flush may launch a key switch on inputs or outputs the caller has destroyed
+// meanwhile -- the round-5 world-8 rehearsal's rank-0 abort: a flush failed out of memory, the queue kept its
+// pointers, the objects were freed (and their blocks returned to the device when the cache was trimmed), and the
+// next flush's key switch read and wrote freed memory.
+static fhs_status drop_pending(fhs_context* c, fhs_status st) {
+    if (st != FHS_OK)
+        for (PendingRot& p : c->pending) p.out->lost = true;
+    c->pending.clear();
+    c->pending_refs.clear();
+    c->pending_outs.clear();
+    c->pending_l = -1;
+    return st;
+}
 static fhs_status flush(fhs_context* c) {
     if (c->pending.empty()) return FHS_OK;
     const int R = (int)c->pending.size(), l = c->pending_l;
@@ -824,9 +842,10 @@ static fhs_status flush(fhs_context* c) {
     const size_t wsb = fhs::keyswitch_workspace_bytes(c->T, R, U, l);
     uint64_t* ws = nullptr;
     HostTrace ht;
-    hipError_t e = scratch(c, fhs_context::SCR_KS, wsb, &ws);
+    hipError_t e = c->debug_fail_flushes > 0 ? (--c->debug_fail_flushes, hipErrorOutOfMemory)
+                                             : scratch(c, fhs_context::SCR_KS, wsb, &ws);
     ht.mark("flush: workspace");
-    if (e != hipSuccess) return hip_fail(e, "key-switch workspace");
+    if (e != hipSuccess) return drop_pending(c, hip_fail(e, "key-switch workspace"));
     fhs::SealHoist* sh = nullptr;
     if (c->T.ks_seal && U < R && seal_hoist_enabled()) {   // SEAL convention: one ModUp per shared input
         e = seal_prepare(c, items, l);
@@ -836,17 +855,13 @@ static fhs_status flush(fhs_context* c) {
             e = hipSuccess;
         }
         ht.mark("flush: seal corrections");
-        if (e != hipSuccess) return hip_fail(e, "seal corrections");
+        if (e != hipSuccess) return drop_pending(c, hip_fail(e, "seal corrections"));
     }
     e = fhs::launch_keyswitch(c->T, items.data(), R, reinterpret_cast<const fhs::u64* const*>(uniq.data()), U, l, ws,
                               wsb, c->items_dev, c->stager, c->st, c->timer_mask ? &c->ktimer : nullptr, sh);
     ht.mark("flush: launch keyswitch");
-    c->pending.clear();
-    c->pending_refs.clear();
-    c->pending_outs.clear();
-    c->pending_l = -1;
-    if (e != hipSuccess) return hip_fail(e, "key-switch launch");
-    return FHS_OK;
+    if (e != hipSuccess) return drop_pending(c, hip_fail(e, "key-switch launch"));
+    return drop_pending(c, FHS_OK);
 }
 
 struct Guard {
@@ -854,6 +869,17 @@ struct Guard {
     std::lock_guard<std::recursive_mutex> lk;
     explicit Guard(fhs_context* c_) : c(c_), lk(c_->mu) {}
 };
+// a ciphertext whose producing rotation was dropped (drop_pending) is not an operand
+static fhs_status live_ct(const fhs_ciphertext* a) {
+    if (a && a->lost) return fail(FHS_ERR_INVALID, "ciphertext lost: the queued rotation producing it could not run "
+                                                   "(an earlier call reported why)");
+    return FHS_OK;
+}
+#define LIVE(ct)                                   \
+    do {                                           \
+        fhs_status _ls = live_ct(ct);              \
+        if (_ls != FHS_OK) return _ls;             \
+    } while (0)
 #define ENTER(ctx)                                                           \
     if (!(ctx)) return fail(FHS_ERR_INVALID, "null context");               \
     Guard _g(ctx);                                                           \
@@ -1722,6 +1748,7 @@ extern "C" fhs_status fhs_plaintext_info(const fhs_plaintext* pt, int* ci, int* 
 extern "C" fhs_status fhs_ciphertext_export(fhs_context* c, const fhs_ciphertext* ct, uint64_t* host) {
     ENTER(c);
     if (!ct || !host) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(ct);
     return export_dev(c, ct->d, ct_bytes(ct), host);
 }
 extern "C" fhs_status fhs_plaintext_export(fhs_context* c, const fhs_plaintext* pt, uint64_t* host) {
@@ -1753,12 +1780,19 @@ extern "C" fhs_status fhs_plaintext_import(fhs_context* c, const uint64_t* host,
     *out = pt;
     return FHS_OK;
 }
+extern "C" fhs_status fhs_debug_fail_next_flushes(fhs_context* c, int count) {
+    if (!c || count < 0) return fail(FHS_ERR_INVALID, "debug_fail_next_flushes: bad args");
+    Guard g(c);
+    c->debug_fail_flushes = count;
+    return FHS_OK;
+}
 extern "C" fhs_status fhs_ciphertext_device_ptr(const fhs_ciphertext* ct, void** dptr, uint64_t* bytes) {
     if (!ct || !dptr) return fail(FHS_ERR_INVALID, "null argument");
     fhs_context* c = ct->ctx;
     Guard g(c);
     fhs_status s = flush(c);
     if (s != FHS_OK) return s;
+    LIVE(ct);
     *dptr = ct->d;
     if (bytes) *bytes = ct_bytes(ct);
     return FHS_OK;
@@ -2336,6 +2370,8 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
     const size_t N = c->N, n = N / 2;
     if ((!pts && !cts) || (cts && !sk) || !re_im || count < 0 || nslots < 1 || (size_t)nslots > n)
         return fail(FHS_ERR_INVALID, "decode: bad arguments");
+    if (cts)
+        for (int i = 0; i < count; ++i) LIVE(cts[i]);
     auto lv = [&](int i) { return cts ? cts[i]->l : pts[i]->l; };
     auto scl = [&](int i) { return cts ? cts[i]->scale : pts[i]->scale; };
     if (count == 0) return FHS_OK;
@@ -2664,6 +2700,7 @@ extern "C" fhs_status fhs_encrypt_asymmetric(fhs_context* c, fhs_public_key* pk,
 extern "C" fhs_status fhs_decrypt(fhs_context* c, fhs_secret_key* sk, const fhs_ciphertext* ct, fhs_plaintext** out) {
     ENTER(c);
     if (!sk || !ct || !out) return fail(FHS_ERR_INVALID, "decrypt: null argument");
+    LIVE(ct);
     fhs_plaintext* pt;
     fhs_status s = new_pt(c, ct->ci, ct->scale, &pt);
     if (s != FHS_OK) return s;
@@ -2681,6 +2718,8 @@ static bool scales_close(double a, double b) { return std::fabs(a - b) <= 1e-9 *
 
 static fhs_status binop(fhs_context* c, int op, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out) {
     if (!a || !b || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
+    LIVE(b);
     fhs_status s = same_level(a, b);
     if (s != FHS_OK) return s;
     if (a->ncomp != b->ncomp) return fail(FHS_ERR_INVALID, "ciphertext sizes differ");
@@ -2705,6 +2744,7 @@ extern "C" fhs_status fhs_sub(fhs_context* c, const fhs_ciphertext* a, const fhs
 extern "C" fhs_status fhs_negate(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, a->ncomp, a->ci, a->scale, &r);
     if (s != FHS_OK) return s;
@@ -2715,6 +2755,7 @@ extern "C" fhs_status fhs_negate(fhs_context* c, const fhs_ciphertext* a, fhs_ci
 }
 static fhs_status plainop(fhs_context* c, int op, const fhs_ciphertext* a, const fhs_plaintext* p, fhs_ciphertext** out) {
     if (!a || !p || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     if (a->ci != p->ci) return fail(FHS_ERR_LEVEL, "ciphertext and plaintext are at different chain indices");
     const double sc = op == fhs::OP_MULP ? a->scale * p->scale : a->scale;
     if (op != fhs::OP_MULP && !scales_close(a->scale, p->scale)) return fail(FHS_ERR_SCALE, "scale mismatch");
@@ -2742,6 +2783,8 @@ extern "C" fhs_status fhs_multiply_plain(fhs_context* c, const fhs_ciphertext* a
 extern "C" fhs_status fhs_multiply(fhs_context* c, const fhs_ciphertext* a, const fhs_ciphertext* b, fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !b || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
+    LIVE(b);
     fhs_status s = same_level(a, b);
     if (s != FHS_OK) return s;
     if (a->ncomp != 2 || b->ncomp != 2) return fail(FHS_ERR_INVALID, "multiply expects 2-component ciphertexts");
@@ -2773,6 +2816,7 @@ extern "C" fhs_status fhs_relinearize(fhs_context* c, const fhs_ciphertext* a, c
                                       fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !rk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     if (a->ncomp != 3) return fail(FHS_ERR_INVALID, "relinearize expects a 3-component ciphertext");
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, 2, a->ci, a->scale, &r);
@@ -2788,6 +2832,7 @@ extern "C" fhs_status fhs_relinearize(fhs_context* c, const fhs_ciphertext* a, c
 extern "C" fhs_status fhs_rescale_to_next(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     if (a->l < 2) return fail(FHS_ERR_LEVEL, "rescale_to_next: no level left (end of modulus switching chain)");
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, a->ncomp, a->ci + 1, a->scale / (double)c->q[a->l - 1], &r);
@@ -2800,6 +2845,7 @@ extern "C" fhs_status fhs_rescale_to_next(fhs_context* c, const fhs_ciphertext* 
 }
 
 static fhs_status drop_ct(fhs_context* c, const fhs_ciphertext* a, int ci, fhs_ciphertext** out) {
+    LIVE(a);
     if (ci < a->ci) return fail(FHS_ERR_LEVEL, "mod_switch_to: cannot switch to a higher level");
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, a->ncomp, ci, a->scale, &r);
@@ -2845,6 +2891,7 @@ extern "C" fhs_status fhs_plain_mod_switch_to(fhs_context* c, const fhs_plaintex
 static fhs_status queue_rotation(fhs_context* c, const fhs_ciphertext* a, uint64_t elt, const fhs_galois_keys* gk,
                                  fhs_ciphertext** out) {
     if (!a || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     if (a->ncomp != 2) return fail(FHS_ERR_INVALID, "rotate expects a 2-component ciphertext");
     auto it = gk->keys.find(elt);
     if (it == gk->keys.end()) return fail(FHS_ERR_KEY, "galois key for this rotation step is not present");
@@ -2907,6 +2954,7 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     for (int b = 0; b < G; ++b) {
         if (!baby[b] || baby[b]->l != l || baby[b]->ncomp != 2 || baby[b]->ci != ci)
             return fail(FHS_ERR_LEVEL, "bsgs: baby steps and diagonals must share one chain index");
+        LIVE(baby[b]);
     }
     if (rescale && l < 2) return fail(FHS_ERR_LEVEL, "bsgs: no level left for the final rescale");
     if (giant_elts && giant_elts[0] != 1) return fail(FHS_ERR_INVALID, "linear_transform: giant group 0 must be the identity");
@@ -2980,13 +3028,14 @@ extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_cip
 // inner products of the B groups into dst ([g][2][l][N] words, device memory), stream-ordered
 static fhs_status inner_products_core(fhs_context* c, const fhs_ciphertext* const* baby, int G,
                                       const fhs_plaintext* const* pts, int B, uint64_t* dst) {
-    if (G < 1 || G > 64 || B < 1) return fail(FHS_ERR_INVALID, "bsgs_inner_products: 1 <= G <= 64, B >= 1");
+    if (G < 1 || G > 2048 || B < 1) return fail(FHS_ERR_INVALID, "bsgs_inner_products: 1 <= G <= 2048, B >= 1");
     const int D = B * G, ci = baby[0]->ci, l = baby[0]->l;
     if ((size_t)D + G > (size_t)fhs_context::kMaxPtrs) return fail(FHS_ERR_INVALID, "bsgs_inner_products: too many plaintexts");
     std::vector<const uint64_t*> ptrs(G + D);
     for (int b = 0; b < G; ++b) {
         if (!baby[b] || baby[b]->l != l || baby[b]->ncomp != 2 || baby[b]->ci != ci)
             return fail(FHS_ERR_LEVEL, "bsgs_inner_products: baby steps must share one chain index");
+        LIVE(baby[b]);
         ptrs[b] = baby[b]->d;
     }
     for (int k = 0; k < D; ++k) {
@@ -3087,6 +3136,7 @@ extern "C" fhs_status fhs_bsgs_giant_steps(fhs_context* c, const fhs_ciphertext*
     for (int j = 0; j < k; ++j) {
         if (!inners[j] || inners[j]->ncomp != 2 || inners[j]->l != l || inners[j]->ci != ci)
             return fail(FHS_ERR_LEVEL, "bsgs_giant_steps: inner products must be 2-component at one chain index");
+        LIVE(inners[j]);
         if (!scales_close(inners[j]->scale, inners[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_giant_steps: scales differ");
     }
     return giant_steps_core(c, [&](int j) { return inners[j]->d; }, k, ci, inners[0]->scale, elts, gk, out);
@@ -3151,6 +3201,7 @@ extern "C" fhs_status fhs_multiply_const(fhs_context* c, const fhs_ciphertext* a
                                          fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     if (!(const_scale > 0) || !std::isfinite(const_scale)) return fail(FHS_ERR_INVALID, "multiply_const: bad scale");
     fhs::ScalarConsts K;
     fhs_status s = scalar_consts(c, value * const_scale, a->l, K);
@@ -3165,6 +3216,7 @@ extern "C" fhs_status fhs_multiply_const(fhs_context* c, const fhs_ciphertext* a
 extern "C" fhs_status fhs_add_const(fhs_context* c, const fhs_ciphertext* a, double value, fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     fhs::ScalarConsts K;
     fhs_status s = scalar_consts(c, value * a->scale, a->l, K);
     if (s != FHS_OK) return s;
@@ -3178,6 +3230,7 @@ extern "C" fhs_status fhs_add_const(fhs_context* c, const fhs_ciphertext* a, dou
 extern "C" fhs_status fhs_mod_raise(fhs_context* c, const fhs_ciphertext* a, fhs_ciphertext** out) {
     ENTER(c);
     if (!a || !out) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(a);
     if (a->ncomp != 2) return fail(FHS_ERR_INVALID, "mod_raise expects a 2-component ciphertext");
     fhs_ciphertext* r;
     fhs_status s = new_ct(c, 2, 1, a->scale, &r);
@@ -3362,6 +3415,7 @@ extern "C" fhs_status fhs_bootstrap_evalmod(fhs_context* c, const fhs_ciphertext
                                             fhs_ciphertext** out) {
     ENTER(c);
     if (!y || !rk || !cc || !cs || !out || ncoef < 1 || r < 1) return fail(FHS_ERR_INVALID, "evalmod: bad argument");
+    LIVE(y);
     try {
         EvalMod e{c, rk, {}, {}};
         e.T[1] = y;
@@ -3424,6 +3478,7 @@ extern "C" fhs_status fhs_bsgs_from_cpu(fhs_context* c, const fhs_ciphertext* co
     ENTER(c);
     if (!baby || !host || !gk || !out) return fail(FHS_ERR_INVALID, "null argument");
     if (ci != baby[0]->ci) return fail(FHS_ERR_LEVEL, "bsgs_from_cpu: diagonals at a different chain index");
+    for (int b = 0; b < G; ++b) LIVE(baby[b]);
     const int l = c->L0 + 1 - ci;
     const size_t bytes = 8ull * D * l * c->N;
     uint64_t* dev = nullptr;
@@ -3531,6 +3586,7 @@ extern "C" fhs_status fhs_staging_stats(fhs_context* c, uint64_t* reentries, uin
 // device-to-device copy of a ciphertext's limbs into caller memory (RCCL interop); synchronises
 static fhs_status copy_to_device(fhs_context* c, const fhs_ciphertext* ct, void* dst, bool sync) {
     if (!ct || !dst) return fail(FHS_ERR_INVALID, "null argument");
+    LIVE(ct);
     HIPCHK(hipMemcpyAsync(dst, ct->d, ct_bytes(ct), hipMemcpyDeviceToDevice, c->st), "copy_to_device");
     if (sync) HIPCHK(hipStreamSynchronize(c->st), "copy_to_device");
     return FHS_OK;

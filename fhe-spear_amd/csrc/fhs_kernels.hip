@@ -1846,11 +1846,14 @@ __device__ __forceinline__ void ld_diag(const u64* limb, int voff, int soff, u64
 // FOLD: products per Acc3 before its fold into the 128-bit sums -- 8 for any prime < 2^60, 16 when every
 // prime is < 2^59 (T.max_qbits <= 59): then the split-30 high halves are < 2^29, so L and M gain < 2^60
 // and H < 2^58 per product and 16 products stay below 2^64
-template <int VEC, int WAVES, int FOLD>
+// Baby-step window (G > 64: the slice of every baby step no longer fits LDS): this launch covers baby steps
+// [b0, b0 + Gw) -- `baby` and `pts` arrive offset by b0 (pts keeps its row stride G), D is the caller's D - b0 --
+// and ACC adds its sums to the previous windows' reduced inner products (one extra read of `inner` per window).
+template <int VEC, int WAVES, int FOLD, bool ACC>
 __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
-                                                    const u64* const* __restrict__ pts, int G, int g0, int g1, int D,
-                                                    int l, u64* __restrict__ inner) {
-    extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [G][2][W], split-30 packed
+                                                    const u64* const* __restrict__ pts, int G, int Gw, int g0, int g1,
+                                                    int D, int l, u64* __restrict__ inner) {
+    extern __shared__ __attribute__((aligned(16))) u64 sb[];   // [Gw][2][W], split-30 packed
     constexpr int W = 64 * VEC;
     const int N = T.N;
     const int i = blockIdx.y, n0 = blockIdx.x * W, tid = threadIdx.x, lane = tid & 63;
@@ -1864,7 +1867,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     // stream too.
     u64 p[8][VEC];
     const int gcur = g0 + wave;
-    auto full_batches = [&](int g) { return g < g1 ? max(0, min(G, D - g * G)) / 8 : 0; };
+    auto full_batches = [&](int g) { return g < g1 ? max(0, min(Gw, D - g * G)) / 8 : 0; };
     int gf = gcur;   // the wave's first group with a full batch
     while (gf < g1 && full_batches(gf) == 0) gf += WAVES;
     if (gf < g1) {
@@ -1872,14 +1875,14 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
 #pragma unroll
         for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
     }
-    for (int idx = tid; idx < G * 2 * W; idx += 64 * WAVES) {
+    for (int idx = tid; idx < Gw * 2 * W; idx += 64 * WAVES) {
         const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
         sb[idx] = pack30(baby[b][comp * S + (size_t)i * N + n0 + c]);
     }
     __syncthreads();
     const RedU R = redu(PK(T, i));
     for (int g = gcur; g < g1; g += WAVES) {
-        const int bmax = min(G, D - g * G);
+        const int bmax = min(Gw, D - g * G);
         if (bmax <= 0) continue;
         u128 c0[VEC], c1[VEC];
         Acc3 a0[VEC], a1[VEC];
@@ -1945,8 +1948,14 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
         }
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
-            inner[(size_t)g * 2 * S + off + v] = reduce128(c0[v].lo, c0[v].hi, R);
-            inner[(size_t)g * 2 * S + S + off + v] = reduce128(c1[v].lo, c1[v].hi, R);
+            u64* o0 = inner + (size_t)g * 2 * S + off + v;
+            u64 r0 = reduce128(c0[v].lo, c0[v].hi, R), r1 = reduce128(c1[v].lo, c1[v].hi, R);
+            if constexpr (ACC) {
+                r0 = addmod(r0, o0[0], R.q);
+                r1 = addmod(r1, o0[S], R.q);
+            }
+            o0[0] = r0;
+            o0[S] = r1;
         }
         if (gn < g1) {
             const u64* const* pgn = pts + (size_t)gn * G;
@@ -2060,31 +2069,52 @@ size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) {
     return keyswitch_workspace_bytes(T, R, R, l) + 8 * (size_t)T.N * 4 * l;
 }
 
+constexpr int kInnerWindow = 64;   // baby steps per k_bsgs_inner launch: [64][2][128] words = 128 KiB of LDS
 template <int VEC, int WAVES>
 static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, const u64* const* pts, int G, int g0,
                                  int g1, int D, int l, u64* inner, hipStream_t st) {
     constexpr int W = 64 * VEC;
     static bool attr = false;
     if (!attr) {   // dynamic LDS above 64 KiB must be opted into
-        for (const void* k : {reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8>),
-                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16>)}) {
-            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(64 * 2 * W * 8));
+        for (const void* k : {reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8, false>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8, true>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true>)}) {
+            hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(kInnerWindow * 2 * W * 8));
             if (e != hipSuccess) return e;
         }
         attr = true;
     }
-    if (T.max_qbits <= 59)
-        hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16>), dim3(T.N / W, l), dim3(64 * WAVES), (size_t)G * 2 * W * 8, st,
-                           T, baby, pts, G, g0, g1, D, l, inner);
-    else
-        hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 8>), dim3(T.N / W, l), dim3(64 * WAVES), (size_t)G * 2 * W * 8, st,
-                           T, baby, pts, G, g0, g1, D, l, inner);
-    return hipGetLastError();
+    // G <= 64: one launch over every baby step; else windows of 64, each adding to the previous ones' sums
+    for (int b0 = 0; b0 < G; b0 += kInnerWindow) {
+        const int Gw = std::min(kInnerWindow, G - b0), Dw = D - b0;
+        const size_t lds = (size_t)Gw * 2 * W * 8;
+        const dim3 grid(T.N / W, l), block(64 * WAVES);
+        if (T.max_qbits <= 59) {
+            if (b0)
+                hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, true>), grid, block, lds, st, T, baby + b0, pts + b0, G, Gw,
+                                   g0, g1, Dw, l, inner);
+            else
+                hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, false>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
+                                   Dw, l, inner);
+        } else {
+            if (b0)
+                hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 8, true>), grid, block, lds, st, T, baby + b0, pts + b0, G, Gw,
+                                   g0, g1, Dw, l, inner);
+            else
+                hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 8, false>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
+                                   Dw, l, inner);
+        }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int g0,
                              int g1, int D, int l, u64* inner, hipStream_t st) {
-    if (T.N % 128 || G > 64 || G < 1) return hipErrorInvalidValue;
+    if (T.N % 128 || G < 1) return hipErrorInvalidValue;
     return launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, g0, g1, D, l, inner, st);
 }
 
@@ -2099,7 +2129,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
                        const KTimer* tm) {
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
-    if (T.N % 128 || G > 64 || R > 512) return hipErrorInvalidValue;
+    if (T.N % 128 || G < 1 || R > 512) return hipErrorInvalidValue;
     if (R > 0 && bsgs_workspace_bytes(T, R, l) > ws_bytes) return hipErrorInvalidValue;
     KsItem items[512];
     const u64* uniq[512];

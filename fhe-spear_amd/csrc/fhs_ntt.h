@@ -139,6 +139,15 @@ __device__ __forceinline__ void ntt_pass(u64* lds, int tid, const u64* __restric
 #ifndef FHS_NTT_WAVELOCAL
 #define FHS_NTT_WAVELOCAL 1
 #endif
+// The hand-off between two wave-local passes (and at a wave-local head or tail): wave_barrier alone is IntrNoMem
+// in LLVM, so it does not stop the compiler from moving one lane's LDS read above another lane's LDS write; the
+// wavefront-scope release / acquire fences around it make that ordering a compiler constraint.  At wavefront
+// scope they emit no instruction (the wave's LDS operations already execute in issue order).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 template <int LOGN, int S, int R>
 constexpr int pass_tl() { return R > 0 ? ((1 << LOGN) >> (S + 1)) >> (R - 1) : 0; }
 // lanes of a wave that take part: 64, or all T = N / EPT threads when the transform has fewer (one wave)
@@ -166,7 +175,7 @@ __device__ __forceinline__ void fwd_from(u64* lds, int tid, const u64* __restric
         constexpr bool here = WL && pass_tl<LOGN, S, R>() <= W;
         constexpr bool next = S2 >= LOGN || (pass_r<LOGN, RL, S2>() == R && pass_tl<LOGN, S2, pass_r<LOGN, RL, S2>()>() <= W);
         if constexpr (here && next)
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
         else
             __syncthreads();
         fwd_from<LOGN, RL, S2, EPT, LAZY, WL>(lds, tid, tw, q, hoff);
@@ -185,7 +194,7 @@ __device__ __forceinline__ void inv_from(u64* lds, int tid, const u64* __restric
         ntt_pass<LOGN, S, R, false, EPT, false, NOFOLD>(lds, tid, tw, q, s0, s0s, s1, s1s, hoff);
         if constexpr (WL && R == RL && S - RL >= S0 && pass_tl<LOGN, S, R>() <= wl_width<LOGN, EPT>() &&
                       pass_tl<LOGN, S - RL, RL>() <= wl_width<LOGN, EPT>())
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
         else
             __syncthreads();
     }
@@ -221,6 +230,7 @@ constexpr bool fwd_exit_wave_local() {
 template <int LOGN, int RL = 3, int EPT = 16, int S0 = 0, bool WL = false>
 __device__ __forceinline__ void ntt_inv_half_lds(u64* lds, int tid, const u64* __restrict__ tw, u64 q, int hoff) {
     static_assert(!WL || (LOGN - S0) % RL == 0, "wave-local inverse passes need one radix throughout");
+    if constexpr (WL) wave_lds_sync();   // the caller's wave-local head writes (no workgroup barrier before)
     inv_from<LOGN, RL, S0, EPT, true, WL, S0>(lds, tid, tw, q, 0, 0, 0, 0, hoff);
 }
 template <int LOGN, int RL = 3, int EPT = 16>

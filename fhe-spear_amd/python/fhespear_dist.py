@@ -36,12 +36,17 @@ class TimedDist:
     delegated.  Per call: kind, bytes moved by this rank's tensor, and its duration -- for device tensors a
     pair of HIP events on the current stream around the collective (torch makes that stream wait for the
     RCCL stream, so the pair brackets the transfer and the wait for the peers, without synchronising the
-    host); for host tensors (gloo) wall time.  Calls moving < 4 KiB (headers) are logged as `<kind>_small`."""
+    host); for host tensors (gloo) wall time.  Calls moving < 4 KiB (headers) are logged as `<kind>_small`;
+    object and barrier collectives as `all_gather_object` / `barrier` (bytes 0).
+    With a FailureFence attached (`fence`), every collective first checks that no peer has failed in the
+    running leg, and `point(stage)` marks a stage boundary of a leg (fence check + failure injection)."""
 
-    KINDS = ("broadcast", "gather", "reduce", "reduce_scatter_tensor", "all_reduce", "send", "recv", "all_gather")
+    KINDS = ("broadcast", "gather", "reduce", "reduce_scatter", "all_reduce", "send", "recv", "all_gather",
+             "all_gather_object", "barrier")
 
-    def __init__(self, dist):
+    def __init__(self, dist, fence=None):
         self._d = dist
+        self.fence = fence
         self.on = False
         self.log = []
 
@@ -54,13 +59,19 @@ class TimedDist:
     def stop(self):
         self.on = False
 
+    def point(self, stage):
+        if self.fence is not None:
+            self.fence.point(stage)
+
     def _timed(self, kind, tensor, fn, *a, **k):
+        if self.fence is not None:
+            self.fence.check()
         if not self.on:
             return fn(*a, **k)
         import time
         import torch
         nbytes = tensor.numel() * tensor.element_size() if tensor is not None else 0
-        if nbytes < 4096:
+        if nbytes < 4096 and tensor is not None:
             kind += "_small"
         if tensor is not None and tensor.is_cuda:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -89,6 +100,15 @@ class TimedDist:
     def reduce_scatter_tensor(self, out, inp, *a, **k):
         return self._timed("reduce_scatter", inp, self._d.reduce_scatter_tensor, out, inp, *a, **k)
 
+    def all_gather(self, outs, tensor, *a, **k):
+        return self._timed("all_gather", tensor, self._d.all_gather, outs, tensor, *a, **k)
+
+    def all_gather_object(self, outs, obj, *a, **k):
+        return self._timed("all_gather_object", None, self._d.all_gather_object, outs, obj, *a, **k)
+
+    def barrier(self, *a, **k):
+        return self._timed("barrier", None, self._d.barrier, *a, **k)
+
     def send(self, tensor, *a, **k):
         return self._timed("send", tensor, self._d.send, tensor, *a, **k)
 
@@ -110,6 +130,257 @@ class TimedDist:
             s["ms"] += ms
         return {k: {"calls": round(v["calls"] / per, 2), "MB": round(v["MB"] / per, 3), "ms": round(v["ms"] / per, 3)}
                 for k, v in sorted(out.items())}
+
+
+# ------------------------------------------------------------------ failure agreement (bench legs over N ranks)
+class PeerFailed(RuntimeError):
+    """Raised on a rank whose leg is abandoned because another rank failed in it."""
+
+
+class InjectedFailure(RuntimeError):
+    """The failure FHESPEAR_BENCH_INJECT asked for (tests of the fence)."""
+
+
+def parse_inject(spec):
+    """FHESPEAR_BENCH_INJECT = "leg[/stage]@rank[,...]": raise InjectedFailure on that rank when leg `leg` starts
+    (no stage) or reaches FailureFence.point(stage).  Returns {(leg, stage or None, rank)}."""
+    out = set()
+    for item in (spec or "").split(","):
+        item = item.strip()
+        if not item:
+            continue
+        where, rank = item.rsplit("@", 1)
+        leg, _, stage = where.partition("/")
+        out.add((leg, stage or None, int(rank)))
+    return out
+
+
+class FailureFence:
+    """One rank's failure ends the leg on every rank, within seconds.
+
+    A bench run at N ranks is a sequence of legs (matvec, SEAL, RWKV block, cfg5 chain...).  Each runs through
+    `run(name, fn)`.  The agreement goes through the c10d store, never through the process group the legs'
+    collectives use, so it works while a peer sits in a collective:
+      * a rank whose leg raises publishes the error under the leg's `fail` key and aborts its process group
+        (gloo closes its pairs, so peers blocked on this rank wake at once; RCCL aborts its communicators);
+      * every rank runs a watcher thread that polls that key while a leg runs; on a peer's failure it aborts its
+        own process group, which wakes a collective this rank is blocked in, and `check()` / `point()` raise
+        PeerFailed at the next collective or stage boundary (TimedDist calls check() before every collective);
+      * at the leg's end every rank publishes {ok, error} and waits (polling, bounded) for all ranks' statuses:
+        all ranks then return the same verdict -- None, or {"error", "failed_ranks", "abandoned_ranks",
+        "unresponsive_ranks"};
+      * a leg that failed may leave collectives half-issued, so the process group is aborted on every rank;
+        with `reinit` (a function of a c10d store that makes a new default process group) every rank then joins
+        a fresh one under a new store prefix and the next leg runs; without it, or when a rank did not report,
+        the later legs are skipped (`run` returns {"skipped": ...}); `finish()` lets rank 0 print its line
+        before the others exit, and destroys the process group when it is still intact.
+    A leg still running after `leg_timeout_s` counts as failed on that rank (a hung collective).
+    World 1 without a process group: LocalFence (the same interface, legs independent)."""
+
+    PREFIX = "fhespear_fence/"
+
+    def __init__(self, dist, rank, world, store=None, poll_s=0.1, agree_timeout_s=120.0, leg_timeout_s=None,
+                 inject=None, log=None, reinit=None, max_reinits=3):
+        import os
+        import threading
+        self.d, self.rank, self.world = dist, rank, world
+        self.store = store if store is not None else dist.distributed_c10d._get_default_store()
+        self.poll_s, self.agree_timeout_s = poll_s, agree_timeout_s
+        self.leg_timeout_s = leg_timeout_s if leg_timeout_s is not None else float(
+            os.environ.get("FHESPEAR_LEG_TIMEOUT", "1200"))
+        self.inject = parse_inject(os.environ.get("FHESPEAR_BENCH_INJECT")) if inject is None else set(inject)
+        self.log = log or (lambda m: None)
+        self.seq = 0
+        self.active = None        # (seq, name, start time) of the running leg
+        self.tripped = None       # a peer's failure message for the running leg
+        self.aborted = False      # process group aborted: no collective may follow
+        self.failed_leg = None
+        self.reinit, self.reinits_left, self.reinits = reinit, max_reinits, 0
+        self._lock = threading.Lock()
+        self._stop = False
+        self._thread = threading.Thread(target=self._watch, name="fhespear-fence", daemon=True)
+        self._thread.start()
+
+    def _k(self, *parts):
+        return self.PREFIX + "/".join(str(p) for p in parts)
+
+    def _get(self, key):
+        return self.store.get(key).decode() if self.store.check([key]) else None
+
+    def _abort(self):
+        with self._lock:
+            if self.aborted:
+                return
+            self.aborted = True
+        try:
+            self.d.distributed_c10d._abort_process_group()
+        except Exception as e:   # reported, never hidden
+            self.log(f"fence: rank {self.rank} process-group abort raised {type(e).__name__}: {e}")
+
+    def _watch(self):
+        import time
+        while not self._stop:
+            time.sleep(self.poll_s)
+            act = self.active
+            if act is None or self.tripped is not None:
+                continue
+            seq, name, t0 = act
+            try:
+                msg = self._get(self._k("fail", seq))
+            except Exception:
+                continue
+            if msg is None and time.time() - t0 > self.leg_timeout_s:
+                msg = f"rank {self.rank}: leg {name!r} still running after {self.leg_timeout_s:.0f} s"
+                try:
+                    self.store.set(self._k("fail", seq), msg)
+                except Exception:
+                    pass
+            if msg is not None and self.active is act:
+                self.tripped = msg
+                self.log(f"fence: rank {self.rank} leaves leg {name!r}: {msg}")
+                self._abort()
+
+    def check(self):
+        """PeerFailed when another rank has failed in the running leg."""
+        if self.tripped is not None:
+            raise PeerFailed(self.tripped)
+
+    def point(self, stage):
+        """A stage boundary of the running leg: check(), then the injected failure if one is due here."""
+        self.check()
+        act = self.active
+        if act is not None and (act[1], stage, self.rank) in self.inject:
+            raise InjectedFailure(f"injected failure in leg {act[1]!r} at {stage!r} on rank {self.rank}")
+
+    def run(self, name, fn, *a, **k):
+        """fn(*a, **k) as leg `name` on every rank -> (result, fault); fault is None when every rank completed
+        the leg, else the same dict on every rank."""
+        import json
+        import time
+        if self.aborted:
+            return None, {"skipped": f"process group aborted after leg {self.failed_leg!r} failed"}
+        with self._lock:
+            self.seq += 1
+            seq = self.seq
+            self.tripped = None
+            self.active = (seq, name, time.time())
+        res, err = None, None
+        try:
+            if (name, None, self.rank) in self.inject:
+                raise InjectedFailure(f"injected failure at the start of leg {name!r} on rank {self.rank}")
+            res = fn(*a, **k)
+            self.check()
+        except PeerFailed as e:
+            err = ("peer", str(e)[:400])
+        except Exception as e:
+            msg = f"{type(e).__name__}: {e}"[:400]
+            # a collective that errors because a peer failed first (its abort closed the connection) is that
+            # failure's consequence: the peer published its error before aborting
+            first = None
+            try:
+                first = self._get(self._k("fail", seq))
+            except Exception:
+                pass
+            if first is not None and not isinstance(e, InjectedFailure):
+                err = ("peer", f"{first} (here: {msg})"[:400])
+                self.tripped = self.tripped or first
+            else:
+                err = ("self", msg)
+                self.log(f"fence: rank {self.rank} leg {name!r} failed: {msg}")
+                try:
+                    if first is None:
+                        self.store.set(self._k("fail", seq), f"rank {self.rank}: {msg}")
+                except Exception:
+                    pass
+            with self._lock:
+                self.active = None   # the watcher has nothing left to report for this leg
+            self._abort()
+        finally:
+            with self._lock:
+                self.active = None
+        if err is None and self.tripped is not None:   # a peer failed after this rank's last collective
+            err = ("peer", self.tripped)
+        self.store.set(self._k("status", seq, self.rank),
+                       json.dumps({"ok": err is None, "kind": err[0] if err else None, "error": err[1] if err else None}))
+        keys = [self._k("status", seq, r) for r in range(self.world)]
+        deadline = time.time() + self.agree_timeout_s
+        while not self.store.check(keys) and time.time() < deadline:
+            time.sleep(0.02)
+        stats = {}
+        for r, key in enumerate(keys):
+            v = self._get(key)
+            if v is not None:
+                stats[r] = json.loads(v)
+        missing = [r for r in range(self.world) if r not in stats]
+        if not missing and all(s["ok"] for s in stats.values()):
+            return res, None
+        first = self._get(self._k("fail", seq))
+        fault = {"error": first or f"ranks {missing} did not report leg {name!r} within {self.agree_timeout_s:.0f} s",
+                 "failed_ranks": sorted(r for r, s in stats.items() if s["kind"] == "self"),
+                 "abandoned_ranks": sorted(r for r, s in stats.items() if s["kind"] == "peer"),
+                 "unresponsive_ranks": missing}
+        self.failed_leg = name
+        self._abort()   # collectives of the failed leg may be half-issued on some rank
+        if self.reinit is not None and not missing and self.reinits_left > 0:
+            # every rank reported, so every rank is here: a fresh process group for the next legs
+            try:
+                self.reinits += 1
+                self.reinits_left -= 1
+                self.reinit(self.d.PrefixStore(self._k("pg", self.reinits), self.store))
+                self.aborted = False
+                fault["process_group"] = f"re-created ({self.reinits})"
+            except Exception as e:   # reported, never hidden: the later legs are skipped
+                fault["process_group"] = f"re-creation failed: {type(e).__name__}: {e}"[:300]
+        return res, fault
+
+    def finish(self, timeout_s=600.0):
+        """After rank 0 printed its line: every rank leaves together.  An intact process group is destroyed
+        (barrier first); an aborted one is left alone.  Returns when the caller may exit."""
+        import time
+        self._stop = True
+        if self.rank == 0:
+            self.store.set(self._k("done"), "1")
+        else:
+            deadline = time.time() + timeout_s
+            while not self.store.check([self._k("done")]) and time.time() < deadline:
+                time.sleep(0.05)
+        if not self.aborted:
+            self.d.barrier()
+            self.d.destroy_process_group()
+
+
+class LocalFence:
+    """FailureFence at world 1 without a process group: each leg's exception is reported, the next leg runs."""
+
+    def __init__(self, log=None):
+        import os
+        self.inject = parse_inject(os.environ.get("FHESPEAR_BENCH_INJECT"))
+        self.log = log or (lambda m: None)
+        self.active = None
+        self.aborted = False
+
+    def check(self):
+        pass
+
+    def point(self, stage):
+        if self.active is not None and (self.active, stage, 0) in self.inject:
+            raise InjectedFailure(f"injected failure in leg {self.active!r} at {stage!r} on rank 0")
+
+    def run(self, name, fn, *a, **k):
+        self.active = name
+        try:
+            if (name, None, 0) in self.inject:
+                raise InjectedFailure(f"injected failure at the start of leg {name!r} on rank 0")
+            return fn(*a, **k), None
+        except Exception as e:
+            msg = f"{type(e).__name__}: {e}"[:400]
+            self.log(f"fence: leg {name!r} failed: {msg}")
+            return None, {"error": msg, "failed_ranks": [0], "abandoned_ranks": [], "unresponsive_ranks": []}
+        finally:
+            self.active = None
+
+    def finish(self, timeout_s=0.0):
+        pass
 
 
 def device_identity(ph, local: int):

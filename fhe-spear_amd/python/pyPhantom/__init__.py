@@ -186,6 +186,7 @@ _SIGS = {
     "fhs_ciphertext_from_device_async": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_double, C.POINTER(_vp)]),
     "fhs_context_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
     "fhs_staging_stats": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "fhs_debug_fail_next_flushes": (C.c_int, [_vp, C.c_int]),
 }
 # Fork-only symbols the reference probes with try/except AttributeError (bg:449-461, 382-391): if
 # the library lacks one (an older build, or FHESPEAR_DISABLE_SYMBOLS for tests), the Python names
@@ -1120,6 +1121,12 @@ def kernel_timer_read(ctx, reset=False):
     if reset:
         _check(_lib.fhs_kernel_timer(ctx._h, -1, None, None, 1), "kernel_timer")
     return out
+
+
+def debug_fail_next_flushes(ctx, count=1):
+    """Testing hook: the next `count` flushes of queued rotations fail as out of memory (their outputs are
+    marked lost and the queue is dropped: fhs_debug_fail_next_flushes)."""
+    _check(_lib.fhs_debug_fail_next_flushes(ctx._h, int(count)), "debug_fail_next_flushes")
 
 
 def staging_stats(ctx):

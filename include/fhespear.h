@@ -53,6 +53,10 @@ int fhs_device_count(void);
 /* PCI bus id of HIP device `device` (e.g. "0000:05:00.0"), for the multi-rank line's device check.  Replaces
  * no pb symbol (extension). */
 fhs_status fhs_device_pci_bus_id(int device, char* buf, int len);
+/* Testing hook (extension, replaces no pb symbol): the next `count` flushes of queued rotations on `ctx` fail as
+ * out of memory before launching, so the drop-the-queue path (queued outputs marked lost, later uses rejected)
+ * can be exercised without exhausting HBM. */
+fhs_status fhs_debug_fail_next_flushes(fhs_context* ctx, int count);
 
 /* ---- parameters (pb:78-98) ---- */
 /* pb:81 create_coeff_modulus: SEAL CoeffModulus::Create (largest primes = 1 mod 2N per size) */

@@ -75,3 +75,45 @@ def test_exit_with_100gb_cache_returns_zero(require_gpu):
            "--P", "3", "--D", "2048", "--F", "4096", "--blocks", "13", "--bootstrap"]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, f"rc {out.returncode}\n" + out.stdout[-2000:] + out.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_failed_flush_drops_the_queue_and_marks_its_outputs_lost(ph):
+    """The round-5 world-8 rehearsal's rank-0 abort (gpurun_out/r05l): a flush of queued rotations failed out of
+    memory in its workspace, the queue kept its pointers, the caller destroyed the objects (their blocks went back
+    to the device when the cache was trimmed) and a later flush launched the key switch on freed memory -- an
+    illegal address at exit.  Now a failed flush empties the queue: the error surfaces as RuntimeError("... out of
+    memory ..."), the queued outputs are marked lost (every later use raises instead of reading undefined limbs),
+    destroying the inputs launches nothing, and the context keeps working (bit-exact rotations afterwards)."""
+    from oracle.oracle import Oracle
+    N, L0, P = 4096, 6, 3
+    parms = ph.params(ph.scheme_type.ckks)
+    parms.set_poly_modulus_degree(N)
+    parms.set_special_modulus_size(P)
+    parms.set_galois_elts(sorted(set(ph.get_elts_from_steps([1, 2], N))))
+    primes = ph.create_coeff_modulus(N, [59] * (L0 + P))
+    parms.set_coeff_modulus(primes)
+    ctx = ph.context(parms)
+    sk = ph.secret_key(ctx, seed=5)
+    gk = sk.create_galois_keys(ctx)
+    o = Oracle(N, [int(q) for q in primes], P)
+    s = o.gen_secret(5)
+    rng = np.random.default_rng(2)
+    a = np.stack([np.stack([rng.integers(0, int(primes[i]), N, dtype=np.uint64) for i in range(L0)]) for _ in range(2)])
+    ct = ph.ciphertext_from_numpy(ctx, a, 1, 2.0 ** 40)
+    r1, r2 = ph.rotate(ctx, ct, 1, gk), ph.rotate(ctx, ct, 2, gk)     # queued, not yet launched
+    ph.debug_fail_next_flushes(ctx, 1)
+    with pytest.raises(RuntimeError, match="out of memory"):
+        ph.add(ctx, ct, ct)                                              # its entry flushes the queue: fails
+    del ct                                                               # nothing queued references it now
+    ctx.synchronize()
+    for r in (r1, r2):
+        with pytest.raises(ValueError, match="lost"):
+            r.to_numpy()
+        with pytest.raises(ValueError, match="lost"):
+            ph.add(ctx, r, r)
+    del r1, r2
+    ct = ph.ciphertext_from_numpy(ctx, a, 1, 2.0 ** 40)
+    e = ph.get_elt_from_step(1, N)
+    assert np.array_equal(ph.rotate(ctx, ct, 1, gk).to_numpy(), o.rotate_elt(a, o.gen_galois_key(5, s, e), e))
+    ctx.synchronize()

@@ -529,6 +529,110 @@ def test_bsgs_matches_oracle_on_cfg2_ring(ph):
     assert np.array_equal(y.to_numpy(), want)
 
 
+def test_cfg5_ring_matches_oracle(ph):
+    """BASELINE configs[4]'s ring and chain (N = 32768, 36 + 3 primes of 59 bits: tf --N 32768 --L0 36 --P 3, tf:134,
+    tf:209-218) with D = 16 so the C oracle finishes in seconds: the secret, Galois keys,
+    symmetric encryption, the hoisted baby rotations (bg:215-220), the fused BSGS (bg:464-485), the FFN's square
+    (tf:57-61: multiply + relinearize + rescale_to_next) and mod_switch_to_next, each bit-identical to the oracle.
+    Every NTT of this ring runs in its half-limb form with the radix-8 global stages and the lazy encoder NTTs
+    of round 5."""
+    N, L0, P, D, seed = 32768, 36, 3, 16, 53
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=seed)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(seed)
+    assert np.array_equal(sk.export(), s)
+    gk = sk.create_galois_keys(ctx)
+    rlk = sk.gen_relinkey(ctx)
+    keys = {st: o.gen_galois_key(seed, s, ph.get_elt_from_step(st, N)) for st in steps}
+    for st in (1, G):
+        assert np.array_equal(gk.export(ph.get_elt_from_step(st, N)), keys[st]), f"galois key step {st}"
+    rng = np.random.default_rng(29)
+    pt = ph.plaintext_from_numpy(ctx, rand_pt(o, rng, L0), 1, 2.0 ** 59)
+    ct = sk.encrypt_symmetric(ctx, pt)
+    a = o.encrypt_symmetric(seed, 0, s, pt.to_numpy())
+    assert np.array_equal(ct.to_numpy(), a)
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    want_baby = [a] + [o.rotate_elt(a, keys[b], ph.get_elt_from_step(b, N)) for b in range(1, G)]
+    for b in range(G):
+        assert np.array_equal(baby[b].to_numpy(), want_baby[b]), f"baby step {b}"
+    pts = ph.random_plaintexts(ctx, 23, D, 1, 2.0 ** 59)
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    yw = o.bsgs_loop(want_baby, [p.to_numpy() for p in pts], [None] + [keys[g * G] for g in range(1, B)], G, B, D)
+    assert np.array_equal(y.to_numpy(), yw)
+    sq = ph.rescale_to_next(ctx, ph.relinearize(ctx, ph.multiply(ctx, y, y), rlk))
+    sqw = o.rescale(o.relinearize(o.multiply(yw, yw), o.gen_relin_key(seed, s)))
+    assert sq.chain_index() == 3 and np.array_equal(sq.to_numpy(), sqw)
+    assert np.array_equal(ph.mod_switch_to_next(ctx, sq).to_numpy(), sqw[:, :-1])
+
+
+def test_bsgs_g_above_64_matches_oracle(ph):
+    """D = 8192 at N = 16384 (tf --D 8192: G = B = 91, D <= slots): the fused BSGS's Hadamard runs in two
+    baby-step windows (64 + 27 baby steps; the second adds its sums to the first's), bit-identical to the
+    oracle's restatement of the reference loop bg:464-485 (before round 6 this shape was
+    rejected with hipErrorInvalidValue).  The inner products alone (the latency modes' half) are checked
+    against the oracle's sums too."""
+    N, L0, P, D, seed = 16384, 3, 1, 8192, 61
+    G = int(np.ceil(np.sqrt(D)))
+    B = int(np.ceil(D / G))
+    assert (G, B) == (91, 91)
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=seed)
+    gk = sk.create_galois_keys(ctx)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(seed)
+    rng = np.random.default_rng(91)
+    a = rand_ct(o, rng, 2, L0)
+    ct = ph.ciphertext_from_numpy(ctx, a, 1, 2.0 ** 40)
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    want_baby = [a] + [o.rotate_elt(a, o.gen_galois_key(seed, s, ph.get_elt_from_step(b, N)), ph.get_elt_from_step(b, N))
+                       for b in range(1, G)]
+    for b in (1, 63, 64, 90):
+        assert np.array_equal(baby[b].to_numpy(), want_baby[b]), f"baby step {b}"
+    pts = ph.random_plaintexts(ctx, 19, D, 1, 2.0 ** 40)
+    pn = [p.to_numpy() for p in pts]
+    y = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk)
+    gkeys = [None] + [o.gen_galois_key(seed, s, ph.get_elt_from_step(g * G, N)) for g in range(1, B)]
+    assert np.array_equal(y.to_numpy(), o.bsgs_loop(want_baby, pn, gkeys, G, B, D))
+    zero = ph.plaintext_from_numpy(ctx, np.zeros((L0, N), dtype=np.uint64), 1, 2.0 ** 40)
+    inner = ph.bsgs_inner_products(ctx, baby, list(pts) + [zero] * (G * B - D), G, B)
+    for g in (0, 1, B - 1):
+        acc = None
+        for b in range(G):
+            if g * G + b < D:
+                t = o.multiply_plain(want_baby[b], pn[g * G + b])
+                acc = t if acc is None else o.add(acc, t)
+        assert np.array_equal(inner[g].to_numpy(), acc), f"inner product of giant group {g}"
+
+
+def test_exact_p1_all_59_bit_rotations_match_oracle(ph):
+    """Exact (default) key switching with P = 1 on an all-59-bit chain at N = 16384, L0 = 36 (the cfg2seal ring in
+    the default convention): one-prime digits take the radix-4 ModUp conversion (modup_convert1_r4, all_b59) and
+    the centred v = 1 branch -- a batch of hoisted rotations and a relinearisation, bit-identical to the oracle
+    (this path was covered only by the bench digest)."""
+    N, L0, P, seed = 16384, 36, 1, 83
+    steps = [1, 5, -7]
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=seed)
+    assert all(q < 2 ** 59 for q in primes)
+    o = oracle_for(primes, N, P)
+    s = o.gen_secret(seed)
+    gk = sk.create_galois_keys(ctx)
+    rlk = sk.gen_relinkey(ctx)
+    rng = np.random.default_rng(37)
+    for l in (L0, 20):
+        a = rand_ct(o, rng, 2, l)
+        A = ph.ciphertext_from_numpy(ctx, a, L0 + 1 - l, 2.0 ** 40)
+        outs = [ph.rotate(ctx, A, st, gk) for st in steps]
+        for st, out in zip(steps, outs):
+            e = ph.get_elt_from_step(st, N)
+            assert np.array_equal(out.to_numpy(), o.rotate_elt(a, o.gen_galois_key(seed, s, e), e)), f"step {st}, l={l}"
+    c3 = rand_ct(o, rng, 3, L0)
+    C3 = ph.ciphertext_from_numpy(ctx, c3, 1, 2.0 ** 40)
+    assert np.array_equal(ph.relinearize(ctx, C3, rlk).to_numpy(), o.relinearize(c3, o.gen_relin_key(seed, s)))
+
+
 @pytest.mark.parametrize("bits", [59, 60])
 def test_bsgs_full_batches_match_oracle(ph, bits):
     """Shapes the small oracle tests above miss: G = 23 (two full 8-diagonal batches plus a tail per giant

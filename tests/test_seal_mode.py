@@ -100,13 +100,14 @@ def _gpu_ctx(ph, N, bits, P, elts=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,L0", [(1024, 4), (8192, 24), (16384, 26)])
-def test_gpu_seal_mode_bit_exact_vs_oracle(ph, orc, N, L0):
+@pytest.mark.parametrize("N,L0,sp", [(1024, 4, 60), (8192, 24, 60), (16384, 26, 60), (16384, 36, 59)])
+def test_gpu_seal_mode_bit_exact_vs_oracle(ph, orc, N, L0, sp):
     """Rotations (a batch of 5 of one input: each decomposed after its automorphism), relinearize and
     the fused BSGS (its giant steps too) in SEAL mode, limb for limb against the oracle.  (16384, 26): a limb's
     extension (26 one-limb digits x 128 KiB) exceeds 3 MiB, so the hoisted key inner product runs half-major
-    (FHS_KSIP_HALVES), at both levels."""
-    bits = [59] * L0 + [60]
+    (FHS_KSIP_HALVES), at both levels.  sp = 59: every prime 59-bit, the bench's cfg2seal ring, where the ModUp
+    takes its radix-4 one-prime conversion (modup_convert1_r4, all_b59)."""
+    bits = [59] * L0 + [sp]
     D = 32
     G, B = 6, 6
     steps = list(range(1, G)) + [g * G for g in range(1, B)]
@@ -149,14 +150,14 @@ def test_gpu_seal_mode_bit_exact_vs_oracle(ph, orc, N, L0):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,L0", [(1024, 4), (8192, 24)])
-def test_gpu_seal_hoisting_with_a_zero_digit_coefficient(ph, orc, N, L0):
+@pytest.mark.parametrize("N,L0,sp", [(1024, 4, 60), (8192, 24, 60), (16384, 36, 59)])
+def test_gpu_seal_hoisting_with_a_zero_digit_coefficient(ph, orc, N, L0, sp):
     """SEAL lifts the automorphed digit without centring: at a coefficient sigma negates, -y lifts to
     q_j - y, which the hoisted path's correction reproduces only for y != 0.  A ciphertext whose digit has
     coefficient 0 at a position the first rotation negates (and, in a second digit, one it does not)
     must take SEAL's per-rotation path and still match the oracle limb for limb; the same rotations of
-    an unmodified ciphertext take the hoisted path."""
-    bits = [59] * L0 + [60]
+    an unmodified ciphertext take the hoisted path.  sp = 59: the all-59-bit chain (radix-4 ModUp path)."""
+    bits = [59] * L0 + [sp]
     steps = [1, 2, 3, 7]
     elts = sorted(set(ph.get_elts_from_steps(steps, N)))
     ctx = _gpu_ctx(ph, N, bits, 1, elts)

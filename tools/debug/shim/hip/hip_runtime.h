@@ -15,4 +15,5 @@ static inline unsigned __umulhi(unsigned a, unsigned b) { return (unsigned)(((ui
 #define __builtin_amdgcn_readfirstlane(x) (x)
 static inline void __syncthreads() {}
 static inline void __builtin_amdgcn_wave_barrier() {}
+#define __builtin_amdgcn_fence(order, scope) ((void)0)
 static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }

@@ -83,6 +83,9 @@ class Ckks:
 
 HOST_PREP_S = [0.0]   # numpy diagonal extraction / roll / tile (the reference caller's own work)
 HOST_DIAGONALS = [False]   # --host-diagonals: prepare the rows with numpy as tf does (tf:48, 76)
+# chain_over_ranks(record_first=True): the first one-rank BSGS call's input ciphertext, diagonals and output are
+# kept here (device objects: nothing is copied inside the timed blocks) for a limb check after the chain
+RECORD = [None]
 
 
 def matmul(ck, ct, M, D, baby):
@@ -97,7 +100,10 @@ def matmul(ck, ct, M, D, baby):
         pts = ck.encoder.encode_double_vector_batch(ck.ctx, diags, ck.scale, chain_index=ct.chain_index())
     else:                   # the same rows built and encoded on the GPU (limb-identical)
         pts = ck.encoder.encode_matrix_diagonals(ck.ctx, M, G, ck.scale, chain_index=ct.chain_index())
-    return ph.bsgs_multiply_accumulate(ck.ctx, baby, pts, G, B, D, ck.gk)
+    out = ph.bsgs_multiply_accumulate(ck.ctx, baby, pts, G, B, D, ck.gk)
+    if RECORD[0] is not None and "ct_out" not in RECORD[0]:
+        RECORD[0].update(ct_in=ct, pts=pts, ct_out=out)
+    return out
 
 
 def baby_steps(ck, ct, G):
@@ -339,13 +345,17 @@ def ct_digest(ct):
 
 
 def chain_over_ranks(ph, N, L0, P, D, F, blocks, bootstrap, dist, rank, world, device, shard="giant", rb=None,
-                     baby_mode="recompute", seed=42, log=None):
+                     baby_mode="recompute", seed=42, log=None, record_first=False):
     """`blocks` FFN blocks (random weights from `seed`, the same on every rank) on rank 0's chain:
     FfnRanks over the ranks when `dist` is given (any world), else the one-rank ffn_block -- limb-identical.
     tf:239-266: a bootstrap (+ one rescale) before a block whenever fewer than 4 levels remain, its linear
     transforms' giant groups over every rank.  Returns {block_seconds, bootstrap_seconds, chain_index,
-    max_err, ct_sha256 (rank 0), setup_s}; every block and bootstrap is bracketed by a device
-    synchronisation and (over ranks) a barrier."""
+    max_err, corr (per block, decrypted vs the plaintext chain: tf:272-298's pass criterion), ct_sha256 (rank 0),
+    setup_s, bootstrap_before (block indices)}; every block and bootstrap is bracketed by a device
+    synchronisation and (over ranks) a barrier.  `dist.point("block<b>")` / `point("bootstrap")` mark the stage
+    boundaries when the caller's dist has them (bench.py's FailureFence).  record_first (one rank, no dist):
+    the chain's first BSGS call -- block 0, key chunk 0 -- exported after the chain as `first_bsgs` {ct_in,
+    ct_out, pts} limbs (bench.py checks it against the CPU port)."""
     rng = np.random.default_rng(seed)
     t_setup = time.perf_counter()
     ck = Ckks(ph, N, L0, P, D, bootstrap=bootstrap)
@@ -355,13 +365,17 @@ def chain_over_ranks(ph, N, L0, P, D, F, blocks, bootstrap, dist, rank, world, d
     fr = FfnRanks(ck, D, F, dist, rank, world, shard, rb, baby_mode, device) if dist is not None else None
     ck.ctx.synchronize()
     t_setup = time.perf_counter() - t_setup
-    times, boots, cis, errs = [], [], [], []
+    times, boots, cis, errs, corrs, boot_at = [], [], [], [], [], []
+    point = getattr(dist, "point", None) or (lambda stage: None)
+    if record_first and dist is None:
+        RECORD[0] = {}
 
     def sync():
         ck.ctx.synchronize()
         if dist is not None:
             dist.barrier()
     for b in range(blocks):
+        point(f"block{b}")
         Wk = rng.normal(0, 0.02, (D, F))
         Wv = rng.normal(0, 0.02, (F, D))
         if bootstrap:   # tf:239-266: fewer than 4 levels left -> bootstrap (+ one rescale)
@@ -372,6 +386,7 @@ def chain_over_ranks(ph, N, L0, P, D, F, blocks, bootstrap, dist, rank, world, d
                 dist.broadcast(flag, src=0)
                 need = int(flag.item())
             if need:
+                point("bootstrap")
                 sync()
                 t0 = time.perf_counter()
                 if dist is None:
@@ -384,6 +399,7 @@ def chain_over_ranks(ph, N, L0, P, D, F, blocks, bootstrap, dist, rank, world, d
                     ct = ck.ph.rescale_to_next(ck.ctx, out) if rank == 0 else None
                 sync()
                 boots.append(time.perf_counter() - t0)
+                boot_at.append(b)
         sync()
         t0 = time.perf_counter()
         ct = fr.block(ct, Wk, Wv) if fr is not None else ffn_block(ck, ct, Wk, Wv, D, F)
@@ -391,13 +407,23 @@ def chain_over_ranks(ph, N, L0, P, D, F, blocks, bootstrap, dist, rank, world, d
         times.append(time.perf_counter() - t0)
         ref = plain_ffn(ref, Wk, Wv)
         if rank == 0:
-            errs.append(float(np.max(np.abs(ck.decrypt(ct, D) - ref))))
+            dec = ck.decrypt(ct, D)
+            errs.append(float(np.max(np.abs(dec - ref))))
+            corrs.append(float(np.corrcoef(dec, ref)[0, 1]))
             cis.append(ct.chain_index())
             if log:
-                log(f"block {b}: {1e3 * times[-1]:.1f} ms chain_index={cis[-1]} max_err={errs[-1]:.3e}")
-    res = {"block_seconds": times, "bootstrap_seconds": boots, "setup_s": t_setup}
+                log(f"block {b}: {1e3 * times[-1]:.1f} ms chain_index={cis[-1]} max_err={errs[-1]:.3e} "
+                    f"corr={corrs[-1]:.8f}")
+    res = {"block_seconds": times, "bootstrap_seconds": boots, "bootstrap_before": boot_at, "setup_s": t_setup}
     if rank == 0:
-        res.update(chain_index=cis, max_err=errs, ct_sha256=ct_digest(ct))
+        res.update(chain_index=cis, max_err=errs, corr=corrs, ct_sha256=ct_digest(ct))
+    if RECORD[0] is not None:
+        r = RECORD[0]
+        RECORD[0] = None
+        if "ct_out" in r:
+            res["first_bsgs"] = {"ct_in": r["ct_in"].to_numpy(), "ct_out": r["ct_out"].to_numpy(),
+                                 "pts": [p.to_numpy() for p in r["pts"]]}
+        del r
     del fr, ct, ck
     return res
 

@@ -403,6 +403,9 @@ class BlockRunner:
         name -> output ciphertext on rank 0."""
         srv = self.srv
         names = fhespear_dist.RWKV_BLOCK_STAGES[idx]
+        point = getattr(self.dist, "point", None)
+        if point is not None:                # stage boundary (bench.py's FailureFence: check + injection)
+            point(f"stage{idx}")
         cts = {}
         for n in names:                      # distinct input ciphertexts in first-use order
             key = inputs[n][1]
