@@ -363,6 +363,7 @@ struct fhs_context {
     // the zero flag (device word + pinned host word) and the counts of hoisted / fallback flushes
     std::map<std::pair<const uint64_t*, int>, uint64_t*> seal_corr;
     size_t seal_corr_bytes = 0;
+    size_t seal_corr_cap = 0;     // bound on seal_corr_bytes (1/16 of the context's device; FHESPEAR_SEAL_CORR_BYTES)
     fhs::SealHoist seal_hoist{};
     enum { SCR_KS, SCR_BSGS_INNER, SCR_BSGS_WS, SCR_BSGS_SUM, SCR_RESCALE, SCR_ENC_PTRS, SCR_COUNT };
     uint64_t* scr[SCR_COUNT] = {};
@@ -511,6 +512,24 @@ static void evict_cold(fhs_context* c, size_t keep) {
     ctx_sync(c);
     for (void* p : victims) (void)hipFree(p);
 }
+// FHESPEAR_CONTIG_BYTES=n (default 0 = never): allocations of at least n bytes ask for physically contiguous memory
+// (hipDeviceMallocContiguous), falling back to plain hipMalloc when refused.  Round 6 (tools/debug/alloc_spread.py,
+// profiles/r06/alloc_spread/): the Hadamard's time follows where its 9.66 GB diagonal slab lands in HBM -- the same
+// process, clocks and data re-allocated ten times ran 1.79-2.02 ms (hipMalloc) and 1.75-2.01 ms (contiguous), the
+// contiguous placements mostly at the fast end (mean -2 % and -6 % on two boxes); but on the bench's own
+// allocation sequence both landed at 2.00-2.05 ms (4 + 4 interleaved runs, profiles/r06/alloc_spread/ab_bench.txt),
+// so it stays off.
+static hipError_t dev_malloc(void** v, size_t bytes) {
+    static const size_t contig = [] {
+        const char* e = getenv("FHESPEAR_CONTIG_BYTES");
+        return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+    }();
+    if (contig && bytes >= contig) {
+        if (hipExtMallocWithFlags(v, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+        (void)hipGetLastError();
+    }
+    return hipMalloc(v, bytes);
+}
 static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
     bytes = bytes ? bytes : 8;
     c->size_tick[bytes] = ++c->cache_tick;
@@ -523,12 +542,12 @@ static hipError_t dalloc(fhs_context* c, uint64_t** p, size_t bytes) {
         return hipSuccess;
     }
     void* v = nullptr;
-    hipError_t e = hipMalloc(&v, bytes);
+    hipError_t e = dev_malloc(&v, bytes);
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {   // give every cache back, retry once
         (void)hipGetLastError();
         trim_cache(c);
         trim_other_caches(c);
-        e = hipMalloc(&v, bytes);
+        e = dev_malloc(&v, bytes);
     }
     if (e == hipSuccess) {
         *p = (uint64_t*)v;
@@ -613,6 +632,9 @@ static fhs_status new_pts(fhs_context* c, size_t count, int ci, double scale, fh
         delete slab;
         return hip_fail(e, "plaintext allocation");
     }
+    if (getenv("FHESPEAR_TRACE_SLABS"))
+        fprintf(stderr, "[fhespear] slab %p: %zu plaintexts, %zu bytes (block %zu)\n", (void*)slab->base, count,
+                8 * count * per, slab->bytes);
     for (size_t k = 0; k < count; ++k) {
         outs[k] = new fhs_plaintext{c, slab->base + k * per, ci, l, scale, slab};
         ++slab->refs;
@@ -778,12 +800,7 @@ static hipError_t seal_prepare(fhs_context* c, std::vector<KsItem>& items, int l
         if (e != hipSuccess) return e;
         sh.zflag_host = static_cast<unsigned*>(h);
     }
-    static const size_t cap = [] {
-        const char* v = getenv("FHESPEAR_SEAL_CORR_BYTES");
-        if (v) return (size_t)strtoull(v, nullptr, 10);
-        size_t fr = 0, tot = 0;
-        return hipMemGetInfo(&fr, &tot) == hipSuccess ? tot / 16 : (size_t)16 << 30;
-    }();
+    const size_t cap = c->seal_corr_cap;   // per context, from its own device (context_create)
     size_t need = 0;
     for (const KsItem& it : items)
         if (it.elt != 1 && !c->seal_corr.count({it.key, l})) need += seal_corr_bytes(c, l);
@@ -932,6 +949,9 @@ extern "C" fhs_status fhs_context_create(uint64_t N, const uint64_t* primes, int
         (void)hipMemGetInfo(&free_b, &total_b);
         c->cache_cap = total_b / 4;
         if (const char* e = getenv("FHESPEAR_CACHE_BYTES")) c->cache_cap = strtoull(e, nullptr, 10);
+        // SEAL-hoisting corrections: 1/16 of this context's device (seal_prepare)
+        c->seal_corr_cap = total_b ? total_b / 16 : (size_t)16 << 30;
+        if (const char* e = getenv("FHESPEAR_SEAL_CORR_BYTES")) c->seal_corr_cap = strtoull(e, nullptr, 10);
     }
     if (galois_elts && n_elts > 0) {
         c->elts.assign(galois_elts, galois_elts + n_elts);

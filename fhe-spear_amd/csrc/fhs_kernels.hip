@@ -1148,29 +1148,75 @@ constexpr int kBufNT = 2;   // buffer aux: non-temporal (streamed once: the swit
 // seeds, or read from an imported key's explicit a (akey, a separate instantiation: the choice is
 // per item, so the digit loop carries no branch)
 typedef const __attribute__((address_space(4))) u64* cu64p;   // constant address space: scalar loads
+#ifndef FHS_KSIP_V6
+#define FHS_KSIP_V6 0   // 1: own digit first, the other digits branch-free -- measured slower, kept off (profiles/r06/ab_ksip_v6)
+#endif
+template <bool EXPLICIT_A>
+__device__ __forceinline__ void ks_digit(const KsOps& o, u64 x, int j, u64 seed, u64 cx, const RedU& RD, unsigned qb,
+                                         Acc3& a0, Acc3& a1) {
+    const Split30 v = split30(x);
+    acc3_mac(a0, v, split30(__builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(o.key, o.n8, j * o.kn8,
+                                                                                         kBufNT))));
+    if constexpr (EXPLICIT_A)
+        acc3_mac(a1, v, split30(__builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(o.akey, o.n8, j * o.kn8,
+                                                                                             kBufNT))));
+    else
+        acc3_mac(a1, v, split30(seeded_uniform_x(seed + cx, RD.q, qb)));
+}
 template <bool EXPLICIT_A>
 __device__ __forceinline__ void ks_digits(const KsOps& o, const u64* seeds_g, u64 cx, const RedU& RD, unsigned qb,
                                           int dn, u128& c0, u128& c1) {
     // the seeds are wave-uniform and read-only: scalar loads instead of flat vector loads
     const cu64p seeds = (cu64p)seeds_g;
     Acc3 a0 = {0, 0, 0}, a1 = {0, 0, 0};
+#if FHS_KSIP_V6
+    // The digit whose limb t is the input's own (read from the input, not extended) first, then the others as
+    // j = k + (k >= jown): the unrolled body has no per-digit branch between the input and the extension, so the
+    // scheduler can issue a group's seed loads and buffer loads together (round 5: a diamond per digit and a
+    // scalar load waited on at once -- 0.61 SALU per VALU, 46 % of wave cycles ready but not issued).  The sums
+    // are exact integers, so the order of the products does not change them.
+    // wave-uniform by construction (readfirstlane: the own digit's sampler loop must not make them look divergent,
+    // which turns every digit's soffset into a waterfall loop)
+    const int jo = __builtin_amdgcn_readfirstlane(o.jown >= 0 ? o.jown : dn);
+    const int nd = __builtin_amdgcn_readfirstlane(o.jown >= 0 ? dn - 1 : dn);
+    if (o.jown >= 0) {
+        ks_digit<EXPLICIT_A>(o, bload64(o.own, o.sn8, 0), o.jown, seeds[o.jown], cx, RD, qb, a0, a1);
+        acc3_fold(c0, a0);
+        acc3_fold(c1, a1);
+    }
+    int k = 0;
+    for (; k + 4 <= nd; k += 4) {   // groups of 4 digits: the 4 seed loads issued together, then the products
+        int jj[4];
+        u64 sd[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            jj[u] = __builtin_amdgcn_readfirstlane(k + u + (k + u >= jo ? 1 : 0));
+            sd[u] = seeds[jj[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            ks_digit<EXPLICIT_A>(o, bload64(o.ext, o.sn8, jj[u] * o.per_r8), jj[u], sd[u], cx, RD, qb, a0, a1);
+        if (k & 4) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
+            acc3_fold(c0, a0);
+            acc3_fold(c1, a1);
+        }
+    }
+    for (; k < nd; ++k) {   // < 4 left (at most 7 products since the last fold)
+        const int j = __builtin_amdgcn_readfirstlane(k + (k >= jo ? 1 : 0));
+        ks_digit<EXPLICIT_A>(o, bload64(o.ext, o.sn8, j * o.per_r8), j, seeds[j], cx, RD, qb, a0, a1);
+    }
+#else
 #pragma unroll FHS_KSIP_UNROLL
     for (int j = 0; j < dn; ++j) {
         const bool own = j == o.jown;
         const u64 x = own ? bload64(o.own, o.sn8, 0) : bload64(o.ext, o.sn8, j * o.per_r8);
-        const Split30 v = split30(x);
-        acc3_mac(a0, v, split30(__builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(o.key, o.n8, j * o.kn8,
-                                                                                             kBufNT))));
-        if constexpr (EXPLICIT_A)
-            acc3_mac(a1, v, split30(__builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(o.akey, o.n8,
-                                                                                                 j * o.kn8, kBufNT))));
-        else
-            acc3_mac(a1, v, split30(seeded_uniform_x(seeds[j] + cx, RD.q, qb)));
+        ks_digit<EXPLICIT_A>(o, x, j, seeds[j], cx, RD, qb, a0, a1);
         if ((j & 7) == 7) {   // Acc3 holds 8 products; 128-bit sums stay < 2^128 for any dnum <= 8 * 32
             acc3_fold(c0, a0);
             acc3_fold(c1, a1);
         }
     }
+#endif
     acc3_fold(c0, a0);
     acc3_fold(c1, a1);
 }

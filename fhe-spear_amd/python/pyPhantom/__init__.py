@@ -353,7 +353,7 @@ class context:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            _lib.fhs_context_destroy(h)
+            _lib is not None and _lib.fhs_context_destroy(h)
             self._h = None
 
     def synchronize(self):
@@ -411,7 +411,7 @@ class plaintext:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_plaintext_destroy(self._h)
+            _lib is not None and _lib.fhs_plaintext_destroy(self._h)
             self._h = None
 
     def _info(self):
@@ -442,7 +442,7 @@ class ciphertext:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_ciphertext_destroy(self._h)
+            _lib is not None and _lib.fhs_ciphertext_destroy(self._h)
             self._h = None
 
     def _info(self):
@@ -508,7 +508,7 @@ class public_key:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_public_key_destroy(self._h)
+            _lib is not None and _lib.fhs_public_key_destroy(self._h)
             self._h = None
 
     def encrypt_asymmetric(self, ctx, pt):
@@ -522,7 +522,7 @@ class relin_key:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_relin_key_destroy(self._h)
+            _lib is not None and _lib.fhs_relin_key_destroy(self._h)
             self._h = None
 
 
@@ -532,7 +532,7 @@ class galois_key:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_galois_keys_destroy(self._h)
+            _lib is not None and _lib.fhs_galois_keys_destroy(self._h)
             self._h = None
 
     def has(self, elt):
@@ -577,7 +577,7 @@ class secret_key:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_secret_key_destroy(self._h)
+            _lib is not None and _lib.fhs_secret_key_destroy(self._h)
             self._h = None
 
     def gen_publickey(self, ctx):
@@ -1094,7 +1094,7 @@ class Event:
 
     def __del__(self):
         if getattr(self, "_h", None):
-            _lib.fhs_event_destroy(self._h)
+            _lib is not None and _lib.fhs_event_destroy(self._h)
             self._h = None
 
 

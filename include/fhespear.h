@@ -137,7 +137,12 @@ fhs_status fhs_ciphertext_device_ptr(const fhs_ciphertext* ct, void** dptr, uint
 /* values: n complex numbers interleaved (re, im); n <= N/2, zero padded.  pb:141-149 */
 fhs_status fhs_encode(fhs_context* ctx, const double* re_im, size_t n, double scale, int chain_index,
                       fhs_plaintext** out);
-/* batch: count vectors of n complex values each (bg:382 encode_*_vector_batch) */
+/* batch: count vectors of n complex values each (bg:382 encode_*_vector_batch).
+ * Lifetime (every batch creator: encode batches, random_plaintexts, upload_plaintexts, encode_matrix_diagonals):
+ * the plaintexts of one call share one device block (a slab of up to 1.5x the request, reused from the cache),
+ * returned to the cache only when the LAST of them is destroyed -- keeping one diagonal of a batch keeps the whole
+ * batch's HBM, and fhs_context memory_in_use counts the slab as long as any of them lives.  Destroy batches as
+ * a whole, or create plaintexts that must outlive their batch with a single-plaintext call. */
 fhs_status fhs_encode_batch(fhs_context* ctx, const double* re_im, size_t count, size_t n, double scale,
                             int chain_index, fhs_plaintext** out_array);
 /* real-valued fast paths: values are n doubles */

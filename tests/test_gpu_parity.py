@@ -568,18 +568,20 @@ def test_cfg5_ring_matches_oracle(ph):
     assert np.array_equal(ph.mod_switch_to_next(ctx, sq).to_numpy(), sqw[:, :-1])
 
 
-def test_bsgs_g_above_64_matches_oracle(ph):
+@pytest.mark.parametrize("D,bits", [(8192, 59), (4290, 60)])
+def test_bsgs_g_above_64_matches_oracle(ph, D, bits):
     """D = 8192 at N = 16384 (tf --D 8192: G = B = 91, D <= slots): the fused BSGS's Hadamard runs in two
     baby-step windows (64 + 27 baby steps; the second adds its sums to the first's), bit-identical to the
     oracle's restatement of the reference loop bg:464-485 (before round 6 this shape was
     rejected with hipErrorInvalidValue).  The inner products alone (the latency modes' half) are checked
-    against the oracle's sums too."""
-    N, L0, P, D, seed = 16384, 3, 1, 8192, 61
+    against the oracle's sums too.  D = 4290 on 60-bit primes: G = 66 (a 2-step second window), a short last
+    giant group, and the 8-products-per-fold accumulator variant of both windows."""
+    N, L0, P, seed = 16384, 3, 1, 61
     G = int(np.ceil(np.sqrt(D)))
     B = int(np.ceil(D / G))
-    assert (G, B) == (91, 91)
+    assert (G, B) == ((91, 91) if D == 8192 else (66, 65))
     steps = list(range(1, G)) + [g * G for g in range(1, B)]
-    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, seed=seed)
+    ctx, sk, primes = make_ctx(ph, N, L0, P, steps=steps, bits=bits, seed=seed)
     gk = sk.create_galois_keys(ctx)
     o = oracle_for(primes, N, P)
     s = o.gen_secret(seed)
@@ -589,7 +591,7 @@ def test_bsgs_g_above_64_matches_oracle(ph):
     baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
     want_baby = [a] + [o.rotate_elt(a, o.gen_galois_key(seed, s, ph.get_elt_from_step(b, N)), ph.get_elt_from_step(b, N))
                        for b in range(1, G)]
-    for b in (1, 63, 64, 90):
+    for b in (1, 63, 64, G - 1):
         assert np.array_equal(baby[b].to_numpy(), want_baby[b]), f"baby step {b}"
     pts = ph.random_plaintexts(ctx, 19, D, 1, 2.0 ** 40)
     pn = [p.to_numpy() for p in pts]

@@ -26,6 +26,7 @@ shift
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 MV="--no-cpu-baseline --no-block --no-seal --no-cfg5"
+PMV="$MV --sustain-s 0"   # counter passes: the timed steps only (no sustained run under the profiler)
 fail() { echo "step $1 failed"; tail -20 "$2"; exit 1; }
 for step in "$@"; do
     name=${step%%=*}
@@ -65,19 +66,22 @@ for step in "$@"; do
         timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$cfg" -o run --output-format csv \
             -- python3 bench.py --steps 20 --warmup 3 $MV $arg > "$OUT/trace_$cfg.log" 2>&1 || fail trace "$OUT/trace_$cfg.log"
         grep '^{' "$OUT/trace_$cfg.log" | tail -1 > "$OUT/trace_bench_$cfg.json"
-        python3 tools/rocprof_summary.py "$OUT/trace_$cfg" "$OUT/trace_bench_$cfg.json" "$OUT/rocprof_summary_$cfg.json" ;;
+        python3 tools/rocprof_summary.py "$OUT/trace_$cfg" "$OUT/trace_bench_$cfg.json" "$OUT/rocprof_summary_$cfg.json" || exit 1
+        # keep rocprofv3's --stats summary, drop the per-dispatch trace (the sustained run makes it large)
+        find "$OUT/trace_$cfg" -name '*kernel_trace.csv' -delete ;;
     pmc)
         cfg=${arg:-cfg2}
         K="k_modup|k_ks_ip|k_bsgs_inner|k_moddown|k_ks_intt|k_giant_sum|k_centered"
         for c in "fetch FETCH_SIZE" "write WRITE_SIZE" "valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"; do
             d=${c%% *}
             timeout -s KILL 240 rocprofv3 --kernel-include-regex "$K" --pmc ${c#* } -d "$OUT/pmc_$d" -o run \
-                --output-format csv -- python3 bench.py --config "$cfg" --steps 3 --warmup 1 $MV > "$OUT/pmc_$d.log" 2>&1 \
+                --output-format csv -- python3 bench.py --config "$cfg" --steps 3 --warmup 1 $PMV > "$OUT/pmc_$d.log" 2>&1 \
                 || fail "pmc $d" "$OUT/pmc_$d.log"
         done
         python3 tools/pmc_traffic.py "$OUT/pmc_fetch/run_counter_collection.csv" \
             "$OUT/pmc_write/run_counter_collection.csv" 7 "$OUT/pmc_traffic_$cfg.json" || exit 1
-        python3 tools/pmc_valu.py "$OUT/pmc_valu/run_counter_collection.csv" 7 "$OUT/pmc_valu_$cfg.json" || exit 1 ;;
+        python3 tools/pmc_valu.py "$OUT/pmc_valu/run_counter_collection.csv" 7 "$OUT/pmc_valu_$cfg.json" || exit 1
+        rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/pmc_valu" ;;
     stall)
         # where k_modup_h's / k_bsgs_inner's wave cycles go (tools/pmc_stall.py): the counter list, then two SQ
         # passes of 8 counters (+ GRBM) each, one rocprofv3 run per pass
@@ -89,11 +93,12 @@ for step in "$@"; do
                  "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_ACTIVE_INST_SCA SQ_LDS_IDX_ACTIVE SQ_INSTS_BRANCH GRBM_GUI_ACTIVE"; do
             i=$((i + 1))
             timeout -s KILL 240 rocprofv3 --kernel-include-regex "$K" --pmc $c -d "$OUT/stall_$i" -o run \
-                --output-format csv -- python3 bench.py --config "$cfg" --steps 3 --warmup 1 $MV > "$OUT/stall_$i.log" 2>&1 \
+                --output-format csv -- python3 bench.py --config "$cfg" --steps 3 --warmup 1 $PMV > "$OUT/stall_$i.log" 2>&1 \
                 || fail "stall pass $i" "$OUT/stall_$i.log"
         done
         python3 tools/pmc_stall.py "$OUT/pmc_stall_$cfg.json" 7 "$OUT/stall_1/run_counter_collection.csv" \
-            "$OUT/stall_2/run_counter_collection.csv" || exit 1 ;;
+            "$OUT/stall_2/run_counter_collection.csv" || exit 1
+        rm -rf "$OUT/stall_1" "$OUT/stall_2" ;;   # raw counter dumps: gpurun copies back at most 64 MiB
     pstall)
         # the same two SQ passes over a script's kernels (KREGEX: which kernels) -> OUT/pmc_stall_<script>.json
         s=${arg%%:*}

@@ -94,8 +94,14 @@ def main():
     res = summarise(load(trace_dir), int(b["steps"]))
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     from bench import kernel_source_hash
+    sus = b.get("sustained") or None
     res.update({"kernel_source_sha256_16": kernel_source_hash(), "config": b.get("config", {}).get("workload"),
                 "bench_value_under_profiler": b.get("value"), "bench_kernels_events": b.get("kernels"),
+                "state": (f"warm: the last {res['steps_timed']} steps of the bench's {sus.get('seconds')} s sustained "
+                          "run (round 6: the same state as the line's sustained figure)") if sus else
+                         "the bench's K timed steps",
+                "sustained_value_under_profiler": sus.get("value") if sus else None,
+                "sustained_clocks_end": sus.get("clocks_end") if sus else None,
                 "source": "rocprofv3 --kernel-trace (per dispatch), last `steps` BSGS steps of the bench run"})
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v["ms_per_step"] for k, v in res["kernels"].items()}), res["longest_matvec_kernel"])
