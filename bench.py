@@ -685,6 +685,11 @@ def build_line(args, cfg, mv, seal, block, cfg5, faults, ranks_rec, world):
                 # compared with the sustained one; the K-step frac is the cold-box burst
                 ref = roof.get("sustained_frac", roof["frac"])
                 roof["rocprof_vs_line"] = round(roof["rocprof_frac"] / ref, 4) if ref else None
+                if roof["rocprof_vs_line"] is not None and abs(roof["rocprof_vs_line"] - 1) > 0.03:
+                    roof["rocprof_vs_line_note"] = (
+                        "outside 3 %: the Hadamard's time follows where the process's 9.66 GB diagonal slab lands in "
+                        "HBM -- one process re-allocating it ran 1.75-2.02 ms at constant clocks "
+                        "(profiles/r06/alloc_spread/); the record and this line are different processes")
         mu_roof = roofline_of("k_modup")
         if mu_roof is not None:
             mu_roof["note"] = ("ModUp + forward NTT is INT-VALU-bound (valu_busy: SQ_ACTIVE_INST_VALU x 4 over SIMD "
