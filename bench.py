@@ -79,7 +79,7 @@ def bsgs_params(D):
 
 
 def algorithmic_bytes_per_matvec(name, cfg, l):
-    """Unique HBM bytes kernel `name` must move for one matvec (DESIGN.md §5).  Rotations of one
+    """Unique HBM bytes kernel `name` must move for one matvec (DESIGN.md §3).  Rotations of one
     input share one ModUp (hoisting): the G-1 baby rotations have one input, each of the B-1
     giant rotations its own, so a matvec runs B ModUps for its G-1 + B-1 key-switches.  SEAL's
     convention (cfg mode "seal") hoists the baby rotations too (round 5, SealHoist): their key products
@@ -870,7 +870,7 @@ def line_schema_errors(res):
 
 def seal_leg(args, ph, cfg):
     """cfg2's matvec with context.set_key_switch_mode('seal'): primes [59] x (L0 + 1), one special
-    prime, SEAL's switch_key_inplace limbs (DESIGN.md §3 SEAL convention; round 5: the 45 baby rotations
+    prime, SEAL's switch_key_inplace limbs (DESIGN.md §4 SEAL convention; round 5: the 45 baby rotations
     share one decomposition, corrected per Galois key to SEAL's per-rotation lift -- `hoisting` counts the
     flushes taken each way).  Same seeds as the main leg; output limbs checked against the oracle's digest of
     this mode (bench_digests cfg2_seal: the oracle rotates one rotation at a time).

@@ -765,7 +765,7 @@ def grid_shape(world: int, rb: int):
 
 def grid_rb(R: int) -> int:
     """Baby shares of the grid for a projection sharded over R ranks (BlockRunner shard="grid").  Per-rank
-    compute measured alone on one MI355X at cfg2 (profiles/r03/grid_shard_cfg2_projection.log)
+    compute measured alone on one MI355X at cfg2 (HISTORY.md §6, profiles/r03/grid_shard_cfg2_projection.log)
     plus the reduce-scatter's xGMI time at ~64 GB/s per link and direction ((rb - 1)/rb x |column| x 9.4 MB
     per rank, spread over the rb - 1 peers' direct links): at 2-4 ranks the transfer outweighs the baby
     rotations it saves (2x1 4.5 + ~3.3 ms vs 1x2 5.0 ms; 2x2 3.0 + ~1.7 vs 1x4 3.5), at 8 ranks sharding

@@ -12,7 +12,7 @@ Fork-only symbols the reference probes with try/except AttributeError (SURVEY.md
 implemented: bsgs_multiply_accumulate (bg:459), encode_*_vector_batch (bg:382, 423),
 offload_plaintexts / upload_plaintexts / bsgs_from_cpu (bg:336-358, 449), ciphertext.chain_index /
 scale / coeff_modulus_size, and ckks_bootstrapper (bootstrap.py; the fork's is un-vendored, so its
-limbs are unpinned -- DESIGN.md §4).
+limbs are unpinned -- DESIGN.md §5).
 """
 from __future__ import annotations
 
@@ -368,7 +368,7 @@ class context:
         return self.L0 + 1 - chain_index
 
     def set_key_switch_mode(self, mode):
-        """Key-switch convention (extension; DESIGN.md §3): 'exact' (default: exact centred ModUp,
+        """Key-switch convention (extension; DESIGN.md §4): 'exact' (default: exact centred ModUp,
         ModDown without rounding -- rotations of one input share a ModUp) or 'seal' (special_modulus_size
         1 only: SEAL's switch_key_inplace -- per-limb lift without centring, automorphism before the
         decomposition, ModDown rounded; batched rotations of one input still share one decomposition,

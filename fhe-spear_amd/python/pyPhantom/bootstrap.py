@@ -7,7 +7,7 @@ Reference surface (the fork's C++ bootstrapper is un-vendored -- SURVEY.md §2.4
   scripts/bootstrap_generation.py:149-154  ct mod-switched down to 2 limbs, then bt.bootstrap(ctx, ct)
   test_fully_enc_bsgs.py:243-262           output "at scale ~ (2^bits)^2, must rescale" once
   paper/main.tex:698, 1138                 CoeffToSlot / EvalMod / SlotToCoeff, level budget [2, 2]
-Its limbs are therefore not pinnable (parity unpinned, DESIGN.md §4); the algorithm below is the
+Its limbs are therefore not pinnable (parity unpinned, DESIGN.md §5); the algorithm below is the
 public CKKS bootstrapping recipe (Cheon-Han-Kim-Kim-Song 2018; the FFT-factored linear transforms
 of Chen-Chillotti-Song 2019 evaluated with BSGS; EvalMod as a low-frequency exp(i theta) series
 raised to a power of two by repeated squaring, in the spirit of Han-Ki 2020's double angle) laid

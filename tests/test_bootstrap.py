@@ -1,7 +1,7 @@
 """CKKS bootstrapping (bg:72-74, 112-116, 149-154; tf:243-262).
 
 The fork's bootstrapper is un-vendored, so limb parity against the reference is unpinned
-(DESIGN.md §4).  What is pinned here:
+(DESIGN.md §5).  What is pinned here:
   CPU  -- the special-FFT factorisation (CoeffToSlot / SlotToCoeff diagonal forms) against the
           dense decode matrix and an FFT; the BSGS layout of each merged group; the scale-exact
           Chebyshev split; the whole pipeline as a float model; and the pipeline run on the C

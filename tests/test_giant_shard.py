@@ -28,7 +28,7 @@ def test_giant_groups_rejects_more_ranks_than_groups():
 
 
 def test_stage_groups_eight_rank_block_layout():
-    """Latency-mode layout of the RWKV block's stages at 8 GPUs: r/k/v 3+3+2,
+    """Latency-mode layout of the RWKV block's stages at 8 GPUs (HISTORY.md §6): r/k/v 3+3+2,
     o 8, each FFN pair 4+4; fewer ranks than projections -> None (dealt instead)."""
     assert fd.stage_groups(3, 8) == [[0, 1, 2], [3, 4, 5], [6, 7]]
     assert fd.stage_groups(1, 8) == [list(range(8))]
