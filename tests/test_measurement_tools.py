@@ -148,6 +148,7 @@ def test_pmc_stall_shares(tmp_path):
 @pytest.mark.parametrize("record", ["r05/rehearse_n4_gloo_one_gpu.json", "r05/rehearse_n8_gloo_one_gpu_matvec_cfg5.json",
                                     "r05/rehearse_n8_gloo_one_gpu_matvec_block.json",
                                     "r05/rehearse_n2_gloo_one_gpu.json", "r06/rehearse_n2_gloo_one_gpu.json",
+                                    "r06/rehearse_n4_gloo_one_gpu.json",
                                     "r06/rehearse_n8_gloo_one_gpu_full_line.json"])
 def test_multi_rank_line_schema_on_the_rehearsal_records(record):
     """the fields the driver's first 8-GPU run must carry -- world size, a device record
@@ -158,7 +159,7 @@ def test_multi_rank_line_schema_on_the_rehearsal_records(record):
     records, the ranks' memory together exceeding one GPU's 288 GB with all legs at once)."""
     res = json.loads((REPO / "profiles" / record).read_text())
     assert bench.line_schema_errors(res) == []
-    if "cfg5" in record or record.startswith("r06/rehearse_n2"):
+    if "cfg5" in record or record.startswith(("r06/rehearse_n2", "r06/rehearse_n4")):
         assert res["cfg5_chain"]["parity"]["matches_one_rank"] is True
     if record.startswith("r06/"):
         # round 6: the whole default line in one run; at world 8 with 8 ranks on one GPU the cfg5 leg runs out of
