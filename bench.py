@@ -418,8 +418,17 @@ def main():
     if not args.no_cfg5 and args.config == "cfg2":
         cfg5 = leg("cfg5", run_cfg5, args, ph, tdist, rank, world, local)
     if rank == 0:
-        res = build_line(args, cfg, mv, seal, block, cfg5, faults, ranks_rec, world)
-        print(json.dumps(res), flush=True)
+        try:
+            res = build_line(args, cfg, mv, seal, block, cfg5, faults, ranks_rec, world)
+        except Exception as e:   # the line is still printed (and the other ranks still released below)
+            import traceback
+            traceback.print_exc()
+            med = (mv or {}).get("median_ms")
+            res = {"metric": "BSGS matvecs/sec at d=2048,N=16384,L0=36; sec/RWKV-block at 1/2/4/8 GPU",
+                   "value": round(1000.0 * world / med, 3) if med and world == 1 else None, "unit": "matvec/s",
+                   "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                   "error": f"line builder: {type(e).__name__}: {e}"[:400], "leg_faults": faults}
+        print(json.dumps(res, default=str), flush=True)
     fence.finish()
 
 
