@@ -179,7 +179,7 @@ class FailureFence:
 
     PREFIX = "fhespear_fence/"
 
-    def __init__(self, dist, rank, world, store=None, poll_s=0.1, agree_timeout_s=120.0, leg_timeout_s=None,
+    def __init__(self, dist, rank, world, store=None, poll_s=0.1, agree_timeout_s=300.0, leg_timeout_s=None,
                  inject=None, log=None, reinit=None, max_reinits=3):
         import os
         import threading
@@ -281,7 +281,7 @@ class FailureFence:
                 first = self._get(self._k("fail", seq))
             except Exception:
                 pass
-            if first is not None and not isinstance(e, InjectedFailure):
+            if first is not None and not first.startswith(f"rank {self.rank}:") and not isinstance(e, InjectedFailure):
                 err = ("peer", f"{first} (here: {msg})"[:400])
                 self.tripped = self.tripped or first
             else:
