@@ -66,6 +66,14 @@ class TimedDist:
     def _timed(self, kind, tensor, fn, *a, **k):
         if self.fence is not None:
             self.fence.check()
+            self.fence.waiting = True   # a leg timeout that fires now is a peer's stall, not this rank's
+            try:
+                return self._timed_call(kind, tensor, fn, *a, **k)
+            finally:
+                self.fence.waiting = False
+        return self._timed_call(kind, tensor, fn, *a, **k)
+
+    def _timed_call(self, kind, tensor, fn, *a, **k):
         if not self.on:
             return fn(*a, **k)
         import time
@@ -174,7 +182,8 @@ class FailureFence:
         a fresh one under a new store prefix and the next leg runs; without it, or when a rank did not report,
         the later legs are skipped (`run` returns {"skipped": ...}); `finish()` lets rank 0 print its line
         before the others exit, and destroys the process group when it is still intact.
-    A leg still running after `leg_timeout_s` counts as failed on that rank (a hung collective).
+    A leg still running after `leg_timeout_s` counts as failed on that rank -- after twice that while the rank waits
+    inside a collective (TimedDist sets `waiting`), so the rank that stalls elsewhere is the one named.
     World 1 without a process group: LocalFence (the same interface, legs independent)."""
 
     PREFIX = "fhespear_fence/"
@@ -194,6 +203,7 @@ class FailureFence:
         self.active = None        # (seq, name, start time) of the running leg
         self.tripped = None       # a peer's failure message for the running leg
         self.aborted = False      # process group aborted: no collective may follow
+        self.waiting = False      # inside a collective (TimedDist)
         self.failed_leg = None
         self.reinit, self.reinits_left, self.reinits = reinit, max_reinits, 0
         self._lock = threading.Lock()
@@ -229,8 +239,10 @@ class FailureFence:
                 msg = self._get(self._k("fail", seq))
             except Exception:
                 continue
-            if msg is None and time.time() - t0 > self.leg_timeout_s:
-                msg = f"rank {self.rank}: leg {name!r} still running after {self.leg_timeout_s:.0f} s"
+            limit = self.leg_timeout_s * (2 if self.waiting else 1)
+            if msg is None and time.time() - t0 > limit:
+                msg = (f"rank {self.rank}: leg {name!r} still running after {limit:.0f} s"
+                       + (" (waiting in a collective)" if self.waiting else ""))
                 try:
                     self.store.set(self._k("fail", seq), msg)
                 except Exception:
@@ -270,8 +282,8 @@ class FailureFence:
                 raise InjectedFailure(f"injected failure at the start of leg {name!r} on rank {self.rank}")
             res = fn(*a, **k)
             self.check()
-        except PeerFailed as e:
-            err = ("peer", str(e)[:400])
+        except PeerFailed as e:   # this rank's own watcher may have timed the leg out: that is this rank's failure
+            err = ("self" if str(e).startswith(f"rank {self.rank}:") else "peer", str(e)[:400])
         except Exception as e:
             msg = f"{type(e).__name__}: {e}"[:400]
             # a collective that errors because a peer failed first (its abort closed the connection) is that
@@ -299,7 +311,7 @@ class FailureFence:
             with self._lock:
                 self.active = None
         if err is None and self.tripped is not None:   # a peer failed after this rank's last collective
-            err = ("peer", self.tripped)
+            err = ("self" if self.tripped.startswith(f"rank {self.rank}:") else "peer", self.tripped)
         self.store.set(self._k("status", seq, self.rank),
                        json.dumps({"ok": err is None, "kind": err[0] if err else None, "error": err[1] if err else None}))
         keys = [self._k("status", seq, r) for r in range(self.world)]

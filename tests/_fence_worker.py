@@ -25,12 +25,25 @@ import torch.distributed as dist  # noqa: E402
 import fhespear_dist as fd  # noqa: E402
 
 WORK_S = float(os.environ.get("FENCE_WORK_S", "0.02"))
+# FENCE_HANG="leg/stage@rank:seconds": that rank stalls there (outside any collective) -- a hung rank, which its own
+# watcher times out after FHESPEAR_LEG_TIMEOUT seconds
+_HANG = os.environ.get("FENCE_HANG", "")
+
+
+def point(td, stage, rank):
+    if _HANG:
+        where, secs = _HANG.rsplit(":", 1)
+        leg_stage, r = where.rsplit("@", 1)
+        act = td.fence.active
+        if act is not None and int(r) == rank and leg_stage == f"{act[1]}/{stage}":
+            time.sleep(float(secs))
+    td.point(stage)
 
 
 def matvec_leg(td, rank, world):
     buf = torch.full((1024,), float(rank))
     for s in range(6):
-        td.point(f"step{s}")
+        point(td, f"step{s}", rank)
         time.sleep(WORK_S)
         got = fd.gather_to_root(td, buf, world, rank)
         if rank == 0:
@@ -40,7 +53,7 @@ def matvec_leg(td, rank, world):
 
 def block_leg(td, rank, world):
     for i in range(4):
-        td.point(f"stage{i}")
+        point(td, f"stage{i}", rank)
         x = torch.full((4096,), float(i) if rank == 0 else -1.0)
         td.broadcast(x, src=0)
         assert float(x[0]) == float(i)
@@ -58,11 +71,11 @@ def block_leg(td, rank, world):
 def cfg5_leg(td, rank, world):
     acc = torch.zeros(2048)
     for b in range(5):
-        td.point(f"block{b}")
+        point(td, f"block{b}", rank)
         flag = torch.tensor([b % 2])
         td.broadcast(flag, src=0)
         if int(flag[0]):
-            td.point("bootstrap")
+            point(td, "bootstrap", rank)
         time.sleep(WORK_S)
         part = torch.full((2048,), float(rank + 1))
         td.reduce(part, dst=0)

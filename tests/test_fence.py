@@ -19,7 +19,8 @@ REPO = Path(__file__).resolve().parents[1]
 WORKER = REPO / "tests" / "_fence_worker.py"
 LEGS = ("matvec", "block", "cfg5")
 
-# (world, injection, re-create the process group after a failure)
+# (world, injection, re-create the process group after a failure); "hang:" = FENCE_HANG (a rank stalls outside any
+# collective; FHESPEAR_LEG_TIMEOUT = 3 s makes its own watcher fail the leg)
 CASES = [
     (2, "matvec/step2@1", True),
     (2, "block@0", True),
@@ -29,6 +30,7 @@ CASES = [
     (4, "cfg5/bootstrap@3", True),
     (4, "block/stage1@3", False),   # no re-creation: the later legs are skipped, the line still printed
     (4, "", True),                  # no failure: every leg completes, the group is destroyed cleanly
+    (3, "hang:block/stage2@2:12", True),
 ]
 
 
@@ -42,8 +44,9 @@ def _port():
 def runs():
     procs = []
     for world, inj, reinit in CASES:
-        env = dict(os.environ, FHESPEAR_BENCH_INJECT=inj, FENCE_REINIT="1" if reinit else "0", OMP_NUM_THREADS="1",
-                   MASTER_ADDR="127.0.0.1")
+        env = dict(os.environ, FHESPEAR_BENCH_INJECT="" if inj.startswith("hang:") else inj,
+                   FENCE_HANG=inj[5:] if inj.startswith("hang:") else "", FHESPEAR_LEG_TIMEOUT="3",
+                   FENCE_REINIT="1" if reinit else "0", OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr=127.0.0.1", f"--master-port={_port()}", str(WORKER)]
         procs.append((time.time(), subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
@@ -74,13 +77,19 @@ def test_one_rank_failure_ends_the_leg_on_every_rank(runs, k):
     if not r["inj"]:
         assert all(legs[n]["fault"] is None for n in LEGS)
         return
-    where, rank = r["inj"].rsplit("@", 1)
+    hang = r["inj"].startswith("hang:")
+    where, rank = (r["inj"][5:].rsplit(":", 1)[0] if hang else r["inj"]).rsplit("@", 1)
     bad = where.split("/")[0]
     f = legs[bad]["fault"]
     assert f is not None and f["failed_ranks"] == [int(rank)], f
     assert sorted(f["abandoned_ranks"]) == [x for x in range(r["world"]) if x != int(rank)], f
-    assert f["unresponsive_ranks"] == [] and "injected failure" in f["error"]
-    assert legs[bad]["seconds"] < 10.0, legs[bad]          # peers left the leg within seconds (gloo timeout: 120 s)
+    assert f["unresponsive_ranks"] == []
+    if hang:   # the stalled rank's own watcher failed the leg after 3 s; its peers left then, not after the stall
+        assert "still running after 3 s" in f["error"], f
+        assert legs[bad]["seconds"] < 40.0, legs[bad]
+    else:
+        assert "injected failure" in f["error"]
+        assert legs[bad]["seconds"] < 10.0, legs[bad]      # peers left the leg within seconds (gloo timeout: 120 s)
     i = LEGS.index(bad)
     for n in LEGS[:i]:
         assert legs[n]["fault"] is None, legs[n]
