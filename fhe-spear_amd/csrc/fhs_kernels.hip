@@ -1895,11 +1895,7 @@ __device__ __forceinline__ void ld_diag(const u64* limb, int voff, int soff, u64
 // Baby-step window (G > 64: the slice of every baby step no longer fits LDS): this launch covers baby steps
 // [b0, b0 + Gw) -- `baby` and `pts` arrive offset by b0 (pts keeps its row stride G), D is the caller's D - b0 --
 // and ACC adds its sums to the previous windows' reduced inner products (one extra read of `inner` per window).
-// VAR (round 6 same-placement A/B variants, tools/debug/inner_ab.py; 0 = the kernel):
-//   1: a group's last bmax mod 8 diagonals loaded by the last full batch's refill into the slots it frees;
-//   2: each slot refilled right after its own product (not per half batch);
-//   3: wave priority raised while the refills are issued (s_setprio).
-template <int VEC, int WAVES, int FOLD, bool ACC, int VAR = 0>
+template <int VEC, int WAVES, int FOLD, bool ACC>
 __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
                                                     const u64* const* __restrict__ pts, int G, int Gw, int g0, int g1,
                                                     int D, int l, u64* __restrict__ inner) {
@@ -1942,7 +1938,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
             a0[v] = a1[v] = Acc3{0, 0, 0};
         }
         const u64* const* pg = pts + (size_t)g * G;
-        const int nb = bmax / 8, rem = bmax - 8 * nb;
+        const int nb = bmax / 8;
         // the wave's next group with a full batch (its first batch is what the last batch here refills)
         int gn = g + WAVES;
         while (gn < g1 && full_batches(gn) == 0) gn += WAVES;
@@ -1958,27 +1954,6 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
                 for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
             }
             const u64* const* nxt = ROLL && bi + 1 < nb ? pg + b + 8 : nullptr;
-            const bool tail_refill = VAR == 1 && ROLL && bi + 1 == nb && rem > 0;
-            if constexpr (VAR == 2 && ROLL) {   // slot by slot: product, then that slot's refill
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) {
-                        const Split30 y = split30(p[u][v]);
-                        acc3_mac(a0[v], unpack30(sb[((b + u) * 2 + 0) * W + lane * VEC + v]), y);
-                        acc3_mac(a1[v], unpack30(sb[((b + u) * 2 + 1) * W + lane * VEC + v]), y);
-                    }
-                    if (u == 7 && (b & 15) == 8) {
-#pragma unroll
-                        for (int v = 0; v < VEC; ++v) {
-                            acc3_fold(c0[v], a0[v]);
-                            acc3_fold(c1[v], a1[v]);
-                        }
-                    }
-                    if (nxt) ld_diag<VEC>(nxt[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
-                }
-                continue;
-            }
 #pragma unroll
             for (int h = 0; h < 8; h += 4) {   // half a batch at a time: products, then that half's refill
 #pragma unroll
@@ -1997,29 +1972,10 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
                     }
                 }
                 if (nxt) {
-                    if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
                     for (int u = h; u < h + 4; ++u) ld_diag<VEC>(nxt[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
-                    if constexpr (VAR == 3) __builtin_amdgcn_s_setprio(0);
-                } else if (tail_refill) {
-#pragma unroll
-                    for (int u = h; u < h + 4; ++u)
-                        if (u < rem) ld_diag<VEC>(pg[b + 8 + u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
                 }
             }
-        }
-        if (VAR == 1 && FOLD == 16 && nb > 0 && rem > 0) {   // the partial batch the last refill loaded (< 16 products unfolded)
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (u < rem) {
-#pragma unroll
-                    for (int v = 0; v < VEC; ++v) {
-                        const Split30 y = split30(p[u][v]);
-                        acc3_mac(a0[v], unpack30(sb[((b + u) * 2 + 0) * W + lane * VEC + v]), y);
-                        acc3_mac(a1[v], unpack30(sb[((b + u) * 2 + 1) * W + lane * VEC + v]), y);
-                    }
-                }
-            b = bmax;
         }
         for (; b < bmax; ++b) {   // < 8 left: at most FOLD - 1 products since the last fold
             u64 q1[VEC];
@@ -2169,10 +2125,7 @@ static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, con
         for (const void* k : {reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8, false>),
                               reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false>),
                               reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8, true>),
-                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true>),
-                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false, 1>),
-                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false, 2>),
-                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false, 3>)}) {
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true>)}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(kInnerWindow * 2 * W * 8));
             if (e != hipSuccess) return e;
@@ -2184,18 +2137,7 @@ static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, con
         const int Gw = std::min(kInnerWindow, G - b0), Dw = D - b0;
         const size_t lds = (size_t)Gw * 2 * W * 8;
         const dim3 grid(T.N / W, l), block(64 * WAVES);
-        const char* var_env = getenv("FHESPEAR_INNER_VAR");   // A/B knob (tools/debug/inner_ab.py), one window only
-        const int var = var_env && !b0 && G <= kInnerWindow ? atoi(var_env) : 0;
-        if (T.max_qbits <= 59 && var == 1)
-            hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, false, 1>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
-                               Dw, l, inner);
-        else if (T.max_qbits <= 59 && var == 2)
-            hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, false, 2>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
-                               Dw, l, inner);
-        else if (T.max_qbits <= 59 && var == 3)
-            hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, false, 3>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
-                               Dw, l, inner);
-        else if (T.max_qbits <= 59) {
+        if (T.max_qbits <= 59) {
             if (b0)
                 hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, true>), grid, block, lds, st, T, baby + b0, pts + b0, G, Gw,
                                    g0, g1, Dw, l, inner);
