@@ -7,6 +7,10 @@ STEPS fused BSGS calls (kernel-timer events); the output limbs must be identical
 
     python tools/debug/inner_ab.py ENV VALUE [PLACEMENTS] [REPS] [STEPS]   (ENV=0 against ENV=VALUE, e.g.
     FHESPEAR_INNER_VAR 2)
+
+The round-6 variants it measured (profiles/r06/ab_inner_same_placement/) were compiled in behind
+FHESPEAR_INNER_VAR at commit 810c6ec and removed after the A/B; a new variant needs its own run-time knob read at
+launch, as there.
 """
 import hashlib
 import os
