@@ -395,6 +395,12 @@ struct fhs_plaintext {
     int ci, l;
     double scale;
     PtSlab* slab = nullptr;   // non-null: d points into a batch's shared block
+    // compact shadow of a periodic plaintext (encode_rows_dev): word e >> tlog of each limb (N >> tlog words)
+    // equals dense word e; read by the fused BSGS's Hadamard only (2^-tlog of the diagonal bytes).  Plaintexts
+    // are immutable, so the two never diverge; every other op reads d.
+    uint64_t* dc = nullptr;
+    int tlog = 0;
+    PtSlab* cslab = nullptr;
 };
 struct fhs_secret_key {
     fhs_context* ctx;
@@ -1709,6 +1715,10 @@ extern "C" fhs_status fhs_plaintext_destroy(fhs_plaintext* pt) {
         } else {
             dfree(c, pt->d, pt_bytes(pt));
         }
+        if (pt->cslab && --pt->cslab->refs == 0) {
+            dfree(c, pt->cslab->base, pt->cslab->bytes);
+            delete pt->cslab;
+        }
     }
     delete pt;
     ctx_release(c);
@@ -1851,26 +1861,80 @@ static void fft_inplace(std::vector<std::complex<double>>& a, const std::vector<
 
 // values: count vectors of n complex (re,im) (or real when is_real); produces rounded coefficients
 
+// The encoder's periodic-row detection (fhs_kernels.hip k_enc_period): *tl = a scratch of one byte per row, or null
+// when no row can take the sparse form (fewer values than slots, a ring below 512, FHESPEAR_ENCODE_DENSE=1)
+static hipError_t enc_periods(fhs_context* c, const double* dvals, size_t cnt, size_t n, size_t stride, bool is_real,
+                              uint64_t** tl, size_t* tbytes) {
+    *tl = nullptr;
+    *tbytes = 0;
+    static const bool dense = getenv("FHESPEAR_ENCODE_DENSE") != nullptr;
+    const int smax = fhs::encode_sparse_max_log(c->logN);
+    if (dense || smax < 1 || n != c->N / 2 || cnt == 0) return hipSuccess;
+    const size_t tb = (cnt + 7) & ~(size_t)7;
+    hipError_t e = dalloc(c, tl, tb);
+    if (e != hipSuccess) {
+        *tl = nullptr;
+        return e;
+    }
+    *tbytes = tb;
+    return fhs::launch_enc_period(dvals, (int)cnt, n, stride, is_real, smax, reinterpret_cast<unsigned char*>(*tl),
+                                  c->st);
+}
 // Encode `cnt` value rows already in HBM (row v at dvals + v * stride doubles) into new plaintexts.
+// A batch of >= 32 rows (diagonal batches, not a client's few vectors) whose every row is periodic (tlog >= 1, read
+// back after k_enc_period: one wait per batch) also gets the
+// compact shadow at the batch's smallest tlog (fhs_plaintext::dc), which the fused BSGS's Hadamard reads instead
+// of the dense limbs; without the device memory for it the batch is simply dense.  FHESPEAR_ENCODE_NO_SHADOW=1 skips
+// it.
 static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cnt, size_t n, size_t stride,
                                   bool is_real, double scale, int ci, fhs_plaintext** outs) {
     const int l = c->L0 + 1 - ci;
-    std::vector<uint64_t*> ptrs(cnt);
+    std::vector<uint64_t*> ptrs(2 * cnt, nullptr);
     fhs_status s0 = new_pts(c, cnt, ci, scale, outs);
     if (s0 != FHS_OK) return s0;
     for (size_t v = 0; v < cnt; ++v) ptrs[v] = outs[v]->d;
     uint64_t* dptrs = nullptr;
-    hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 8 * cnt, &dptrs);
-    if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 8 * cnt);
+    hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 16 * cnt, &dptrs);
     // fused reduction + NTT through a scratch of rounded coefficients (FHESPEAR_ENCODE_UNFUSED=1: the
     // encoder reduces into every limb and the NTT runs in place -- same limbs, A/B and test knob)
     static const bool unfused = getenv("FHESPEAR_ENCODE_UNFUSED") != nullptr;
+    static const bool no_shadow = getenv("FHESPEAR_ENCODE_NO_SHADOW") != nullptr;
     uint64_t* coef = nullptr;
     const size_t cbytes = 8 * cnt * c->N;
     if (e == hipSuccess && !unfused) e = dalloc(c, &coef, cbytes);
+    uint64_t* tl = nullptr;
+    size_t tbytes = 0;
+    if (e == hipSuccess) e = enc_periods(c, dvals, cnt, n, stride, is_real, &tl, &tbytes);
+    int ss = 0;
+    if (e == hipSuccess && tl && coef && !no_shadow && c->T.max_qbits <= 59 && cnt >= 32) {
+        std::vector<unsigned char> th(cnt);
+        e = hipMemcpyAsync(th.data(), tl, cnt, hipMemcpyDeviceToHost, c->st);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+        if (e == hipSuccess) ss = *std::min_element(th.begin(), th.end());
+        if (ss > 0) {
+            const size_t per = (size_t)l * (c->N >> ss);
+            auto* cs = new PtSlab{nullptr, 8 * cnt * per, 0};
+            if (dalloc_fit(c, &cs->base, &cs->bytes) == hipSuccess) {
+                for (size_t v = 0; v < cnt; ++v) {
+                    outs[v]->dc = cs->base + v * per;
+                    outs[v]->tlog = ss;
+                    outs[v]->cslab = cs;
+                    ++cs->refs;
+                    ptrs[cnt + v] = outs[v]->dc;
+                }
+            } else {
+                (void)hipGetLastError();   // no room for the shadow: a dense batch
+                delete cs;
+                ss = 0;
+            }
+        }
+    }
+    if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 16 * cnt);
     if (e == hipSuccess)
         e = fhs::launch_encode(c->T, dvals, (int)cnt, n, stride, is_real, scale, reinterpret_cast<fhs::u64* const*>(dptrs),
-                               l, c->st, reinterpret_cast<double*>(coef));
+                               l, c->st, reinterpret_cast<double*>(coef), reinterpret_cast<const unsigned char*>(tl),
+                               ss ? reinterpret_cast<fhs::u64* const*>(dptrs + cnt) : nullptr, ss);
+    if (tl) dfree(c, tl, tbytes);
     if (coef) dfree(c, coef, cbytes);
     return e == hipSuccess ? FHS_OK : hip_fail(e, "encode");
 }
@@ -2681,9 +2745,14 @@ extern "C" fhs_status fhs_encode_encrypt_symmetric_batch(fhs_context* c, fhs_sec
     HIPCHK(dalloc(c, &dvals, vb), "encode_encrypt");
     hipError_t e = dalloc(c, &coef, cb);
     if (e == hipSuccess && stride) e = stage_h2d(c, dvals, values, 8 * count * stride);
+    uint64_t* tl = nullptr;   // periodic rows: the sparse encoding, as encode_*_batch gives them
+    size_t tbytes = 0;
+    if (e == hipSuccess)
+        e = enc_periods(c, reinterpret_cast<const double*>(dvals), count, n, stride, is_real != 0, &tl, &tbytes);
     if (e == hipSuccess)
         e = fhs::launch_encode_coef(c->T, reinterpret_cast<const double*>(dvals), (int)count, n, stride, is_real != 0,
-                                    scale, reinterpret_cast<double*>(coef), c->st);
+                                    scale, reinterpret_cast<double*>(coef), c->st, reinterpret_cast<const unsigned char*>(tl));
+    if (tl) dfree(c, tl, tbytes);
     if (e == hipSuccess) {
         std::vector<double> scales(count, scale);
         st = encrypt_sym_core(c, sk, (int)count, l, ci, scales.data(), nullptr, reinterpret_cast<const double*>(coef),
@@ -2963,9 +3032,10 @@ extern "C" fhs_status fhs_rotate_many(fhs_context* c, const fhs_ciphertext* cons
 // ============================================================================ fused BSGS
 // giant_elts: null = 5^(g G) (the matvec, bg:478-483); else B Galois elements, giant_elts[0] = 1.
 // rescale = false leaves the sum at the product scale (last SlotToCoeff group of the bootstrap).
+// ptl > 0: pt_ptrs are the diagonals' compact shadows (pts_ptl)
 static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, int G, const uint64_t* const* pt_ptrs,
                             int D, int B, int ci, double pt_scale, const fhs_galois_keys* gk, fhs_ciphertext** out,
-                            const uint64_t* giant_elts = nullptr, bool rescale = true) {
+                            const uint64_t* giant_elts = nullptr, bool rescale = true, int ptl = 0) {
     if (G < 1 || D < 1 || !baby) return fail(FHS_ERR_INVALID, "bsgs: bad G/D");
     const int Beff = std::min(B, (D + G - 1) / G);
     if (Beff < 1) return fail(FHS_ERR_INVALID, "bsgs: no giant groups");
@@ -3007,7 +3077,7 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     HIPCHK(scratch(c, fhs_context::SCR_BSGS_SUM, 16 * S, &sum), "bsgs sum");
     ht.mark("workspaces");
     HIPCHK(fhs::launch_bsgs(c->T, dbaby, dpts, G, Beff, D, l, keys.data(), akeys.data(), giant_elts, inner, sum, ws, wsb,
-                            c->items_dev, c->stager, c->st, tm),
+                            c->items_dev, c->stager, c->st, tm, ptl),
            "bsgs");
     ht.mark("launch bsgs");
     fhs_ciphertext* r;
@@ -3028,6 +3098,15 @@ static fhs_status bsgs_core(fhs_context* c, const fhs_ciphertext* const* baby, i
     return FHS_OK;
 }
 
+// The Hadamard reads the diagonals' compact shadows when every one has one at the same tlog (encode_rows_dev; the
+// same products, 2^-tlog of the bytes), else the dense limbs.  FHESPEAR_BSGS_DENSE=1 always reads the dense limbs.
+static int pts_ptl(const fhs_context* c, const fhs_plaintext* const* pts, int D) {
+    static const bool dense = getenv("FHESPEAR_BSGS_DENSE") != nullptr;
+    if (dense || D < 1 || c->T.max_qbits > 59 || !pts[0]->dc) return 0;
+    for (int k = 1; k < D; ++k)
+        if (!pts[k]->dc || pts[k]->tlog != pts[0]->tlog) return 0;
+    return pts[0]->tlog;
+}
 extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_ciphertext* const* baby, int G,
                                                    const fhs_plaintext* const* pts, int D, int B,
                                                    const fhs_galois_keys* gk, fhs_ciphertext** out) {
@@ -3037,9 +3116,10 @@ extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_cip
     for (int k = 0; k < D; ++k) {
         if (!pts[k] || pts[k]->ci != baby[0]->ci) return fail(FHS_ERR_LEVEL, "bsgs: diagonal at a different chain index");
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs: diagonal scales differ");
-        p[k] = pts[k]->d;
     }
-    return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out);
+    const int ptl = pts_ptl(c, pts, D);
+    for (int k = 0; k < D; ++k) p[k] = ptl ? pts[k]->dc : pts[k]->d;
+    return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out, nullptr, true, ptl);
 }
 
 // The Hadamard half of the fused BSGS alone: outs[g] = sum_{b < G} baby[b] (.) pts[g G + b], g < B, not
@@ -3061,11 +3141,12 @@ static fhs_status inner_products_core(fhs_context* c, const fhs_ciphertext* cons
     for (int k = 0; k < D; ++k) {
         if (!pts[k] || pts[k]->ci != ci) return fail(FHS_ERR_LEVEL, "bsgs_inner_products: plaintext at a different chain index");
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_inner_products: plaintext scales differ");
-        ptrs[G + k] = pts[k]->d;
     }
+    const int ptl = pts_ptl(c, pts, D);
+    for (int k = 0; k < D; ++k) ptrs[G + k] = ptl ? pts[k]->dc : pts[k]->d;
     HIPCHK(stage_h2d(c, c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D)), "bsgs_inner_products");
     const uint64_t* const* dbaby = reinterpret_cast<const uint64_t* const*>(c->ptrs_dev);
-    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dbaby + G, G, 0, B, D, l, dst, c->st), "bsgs_inner_products");
+    HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dbaby + G, G, 0, B, D, l, dst, c->st, ptl), "bsgs_inner_products");
     return FHS_OK;
 }
 extern "C" fhs_status fhs_bsgs_inner_products(fhs_context* c, const fhs_ciphertext* const* baby, int G,
@@ -3184,11 +3265,12 @@ extern "C" fhs_status fhs_linear_transform(fhs_context* c, const fhs_ciphertext*
     for (int k = 0; k < D; ++k) {
         if (!pts[k] || pts[k]->ci != baby[0]->ci) return fail(FHS_ERR_LEVEL, "linear_transform: plaintext at a different chain index");
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "linear_transform: plaintext scales differ");
-        p[k] = pts[k]->d;
     }
+    const int ptl = pts_ptl(c, pts, D);
+    for (int k = 0; k < D; ++k) p[k] = ptl ? pts[k]->dc : pts[k]->d;
     for (int g = 0; g < B; ++g)
         if ((giant_elts[g] & 1) == 0 || giant_elts[g] >= 2 * c->N) return fail(FHS_ERR_INVALID, "linear_transform: bad Galois element");
-    return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out, giant_elts, rescale != 0);
+    return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out, giant_elts, rescale != 0, ptl);
 }
 
 // ============================================================================ bootstrapping primitives

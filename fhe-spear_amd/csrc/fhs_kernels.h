@@ -143,16 +143,26 @@ size_t bsgs_workspace_bytes(const DevTables& T, int R, int l);
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
                        u64* out, u64* workspace, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
-                       const KTimer* tm);
+                       const KTimer* tm, int ptl = 0);
 // inner[g] = sum_{b < G, gG + b < D} baby[b] (.) pts[gG + b] for g in [g0, g1) (k_bsgs_inner), inner laid out
-// [g][2][l][N]
+// [g][2][l][N].  ptl > 0: pts_dev are compact diagonals (word e >> ptl of each limb of l N >> ptl words holds dense
+// word e: the periodic plaintexts' shadow, fhs_host.hip encode_rows_dev), 59-bit chains only.
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int g0,
-                             int g1, int D, int l, u64* inner, hipStream_t st);
+                             int g1, int D, int l, u64* inner, hipStream_t st, int ptl = 0);
 // CKKS encode on the GPU: `count` vectors of n values (real, or interleaved re/im), stride doubles
 // apart in device memory, to plaintexts outs[0..count) at l limbs, NTT form.
+// tlog (device, count bytes, or null): each row's periodicity from launch_enc_period -- rows with tlog > 0 are
+// encoded through the sparse form (fhs_kernels.hip k_enc_period).
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
                          double scale, u64* const* outs_dev, int l, hipStream_t st,
-                         double* coef_scratch = nullptr);
+                         double* coef_scratch = nullptr, const unsigned char* tlog = nullptr,
+                         u64* const* couts_dev = nullptr, int ss = 0);
+// couts_dev (with coef_scratch and tlog, every row's tlog >= ss >= 1): each plaintext's compact shadow too, l limbs of
+// N >> ss words, word e >> ss = dense word e
+// per row (n = N/2 values) the largest s <= smax with the row periodic of period (N/2) >> s, into tlog[row]
+hipError_t launch_enc_period(const double* vals, int count, size_t n, size_t stride, bool is_real, int smax,
+                             unsigned char* tlog, hipStream_t st);
+int encode_sparse_max_log(int logN);   // the smax the encoder supports at this ring (0: none)
 // SAMPLE_UNIFORM / TERNARY / CBD draw from the ChaCha20 PRF stream (K, sid); SAMPLE_SEEDED expands
 // the public seed `sid` (switching-key a_j); SAMPLE_TESTDATA is the non-secret SplitMix64 uniform of
 // random_plaintexts (K unused)
@@ -174,7 +184,7 @@ hipError_t launch_encrypt_sym_batch(const DevTables& T, const ::PrfKey& K, u64 s
 // coef (count x N rounded message coefficients, launch_encode_coef) instead of pts_dev (null): encode and
 // encrypt fused -- the message enters the error's NTT, the same limbs as encoding then encrypting.
 hipError_t launch_encode_coef(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
-                              double scale, double* coef, hipStream_t st);
+                              double scale, double* coef, hipStream_t st, const unsigned char* tlog = nullptr);
 hipError_t launch_encrypt_combine(const DevTables& T, int mode, u64* c0, u64* c1, const u64* s_or_pk0, const u64* pk1,
                                   const u64* u_ntt, const u64* e0, const u64* e1, const u64* pt, int l, hipStream_t st);
 hipError_t launch_decrypt(const DevTables& T, const u64* ct, int ncomp, const u64* s, u64* out, int l, hipStream_t st);

@@ -1878,10 +1878,15 @@ hipError_t launch_keyswitch(const DevTables& T, const KsItem* items_host, int R,
 // diagonal words of plaintext `p` (limb base p + i N) at this lane's coefficients: a non-temporal buffer
 // load (the limb offset and the slice offset n0 are wave-uniform: descriptor base and soffset), so no
 // 64-bit address arithmetic and no flat load (which would also wait on the LDS counter)
-template <int VEC>
+// TL > 0: a compact diagonal (the periodic plaintexts' shadow, fhs_host.hip encode_rows_dev): word e >> TL of the
+// limb holds dense word e, so a lane's VEC = 2 coefficients share one 8-byte word (voff, soff already shifted)
+template <int VEC, int TL = 0>
 __device__ __forceinline__ void ld_diag(const u64* limb, int voff, int soff, u64* out) {
     const __amdgpu_buffer_rsrc_t r = brsrc(limb, 0x7ffffff0);
-    if constexpr (VEC == 2) {
+    if constexpr (TL > 0) {
+        static_assert(VEC == 2, "compact diagonals: two coefficients per lane");
+        out[0] = out[1] = __builtin_bit_cast(u64, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, kBufNT));
+    } else if constexpr (VEC == 2) {
         const auto t = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kBufNT);
         out[0] = ((u64)t[1] << 32) | t[0];
         out[1] = ((u64)t[3] << 32) | t[2];
@@ -1895,7 +1900,8 @@ __device__ __forceinline__ void ld_diag(const u64* limb, int voff, int soff, u64
 // Baby-step window (G > 64: the slice of every baby step no longer fits LDS): this launch covers baby steps
 // [b0, b0 + Gw) -- `baby` and `pts` arrive offset by b0 (pts keeps its row stride G), D is the caller's D - b0 --
 // and ACC adds its sums to the previous windows' reduced inner products (one extra read of `inner` per window).
-template <int VEC, int WAVES, int FOLD, bool ACC>
+// TL > 0: compact diagonals (ld_diag) -- the same products, 2^-TL of the diagonal bytes
+template <int VEC, int WAVES, int FOLD, bool ACC, int TL = 0>
 __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u64* const* __restrict__ baby,
                                                     const u64* const* __restrict__ pts, int G, int Gw, int g0, int g1,
                                                     int D, int l, u64* __restrict__ inner) {
@@ -1906,6 +1912,8 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: the diagonal pointers come by scalar loads
     const size_t S = (size_t)l * N;
     const size_t off = (size_t)i * N + n0 + lane * VEC;
+    const size_t dlimb = (size_t)i * (N >> TL);                   // limb i of a (compact) diagonal
+    const int dvoff = ((lane * VEC) >> TL) * 8, dsoff = (n0 >> TL) * 8;
     // Rolling refill: within a giant group a wave keeps 8 diagonal loads in flight at every moment --
     // slot u is reloaded with the next batch's diagonal u as soon as its product is formed, so the loads
     // do not drain while the wave computes (they drain once per group, at its tail and stores).  The first
@@ -1919,7 +1927,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
     if (gf < g1) {
         const u64* const* pg0 = pts + (size_t)gf * G;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg0[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
+        for (int u = 0; u < 8; ++u) ld_diag<VEC, TL>(pg0[u] + dlimb, dvoff, dsoff, p[u]);
     }
     for (int idx = tid; idx < Gw * 2 * W; idx += 64 * WAVES) {
         const int b = idx / (2 * W), comp = (idx / W) & 1, c = idx % W;
@@ -1951,7 +1959,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
             constexpr bool ROLL = FOLD == 16;
             if (!ROLL && bi > 0) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) ld_diag<VEC>(pg[b + u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
+                for (int u = 0; u < 8; ++u) ld_diag<VEC, TL>(pg[b + u] + dlimb, dvoff, dsoff, p[u]);
             }
             const u64* const* nxt = ROLL && bi + 1 < nb ? pg + b + 8 : nullptr;
 #pragma unroll
@@ -1973,13 +1981,13 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
                 }
                 if (nxt) {
 #pragma unroll
-                    for (int u = h; u < h + 4; ++u) ld_diag<VEC>(nxt[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
+                    for (int u = h; u < h + 4; ++u) ld_diag<VEC, TL>(nxt[u] + dlimb, dvoff, dsoff, p[u]);
                 }
             }
         }
         for (; b < bmax; ++b) {   // < 8 left: at most FOLD - 1 products since the last fold
             u64 q1[VEC];
-            ld_diag<VEC>(pg[b] + (size_t)i * N, lane * VEC * 8, n0 * 8, q1);
+            ld_diag<VEC, TL>(pg[b] + dlimb, dvoff, dsoff, q1);
 #pragma unroll
             for (int v = 0; v < VEC; ++v) {
                 const Split30 y = split30(q1[v]);
@@ -2006,7 +2014,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_bsgs_inner(DevTables T, const u6
         if (gn < g1) {
             const u64* const* pgn = pts + (size_t)gn * G;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) ld_diag<VEC>(pgn[u] + (size_t)i * N, lane * VEC * 8, n0 * 8, p[u]);
+            for (int u = 0; u < 8; ++u) ld_diag<VEC, TL>(pgn[u] + dlimb, dvoff, dsoff, p[u]);
         }
     }
 }
@@ -2116,28 +2124,56 @@ size_t bsgs_workspace_bytes(const DevTables& T, int R, int l) {
 }
 
 constexpr int kInnerWindow = 64;   // baby steps per k_bsgs_inner launch: [64][2][128] words = 128 KiB of LDS
+// compact diagonals (tlog 1..3; 59-bit chains: the FOLD = 16 kernels)
+template <int VEC, int WAVES, int TL>
+static void launch_inner_compact(dim3 grid, dim3 block, size_t lds, hipStream_t st, const DevTables& T,
+                                 const u64* const* baby, const u64* const* pts, int G, int Gw, int g0, int g1, int Dw,
+                                 int l, u64* inner, bool acc) {
+    if (acc)
+        hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, true, TL>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
+                           Dw, l, inner);
+    else
+        hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, false, TL>), grid, block, lds, st, T, baby, pts, G, Gw, g0, g1,
+                           Dw, l, inner);
+}
 template <int VEC, int WAVES>
 static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, const u64* const* pts, int G, int g0,
-                                 int g1, int D, int l, u64* inner, hipStream_t st) {
+                                 int g1, int D, int l, u64* inner, hipStream_t st, int ptl) {
     constexpr int W = 64 * VEC;
     static bool attr = false;
     if (!attr) {   // dynamic LDS above 64 KiB must be opted into
         for (const void* k : {reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8, false>),
                               reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false>),
                               reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 8, true>),
-                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true>)}) {
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false, 1>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true, 1>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false, 2>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true, 2>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, false, 3>),
+                              reinterpret_cast<const void*>(&k_bsgs_inner<VEC, WAVES, 16, true, 3>)}) {
             hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)(kInnerWindow * 2 * W * 8));
             if (e != hipSuccess) return e;
         }
         attr = true;
     }
+    if (ptl < 0 || ptl > 3 || (ptl > 0 && (T.max_qbits > 59 || VEC != 2))) return hipErrorInvalidValue;
     // G <= 64: one launch over every baby step; else windows of 64, each adding to the previous ones' sums
     for (int b0 = 0; b0 < G; b0 += kInnerWindow) {
         const int Gw = std::min(kInnerWindow, G - b0), Dw = D - b0;
         const size_t lds = (size_t)Gw * 2 * W * 8;
         const dim3 grid(T.N / W, l), block(64 * WAVES);
-        if (T.max_qbits <= 59) {
+        if (ptl == 1) {
+            launch_inner_compact<VEC, WAVES, 1>(grid, block, lds, st, T, baby + b0, pts + b0, G, Gw, g0, g1, Dw, l, inner,
+                                                b0 > 0);
+        } else if (ptl == 2) {
+            launch_inner_compact<VEC, WAVES, 2>(grid, block, lds, st, T, baby + b0, pts + b0, G, Gw, g0, g1, Dw, l, inner,
+                                                b0 > 0);
+        } else if (ptl == 3) {
+            launch_inner_compact<VEC, WAVES, 3>(grid, block, lds, st, T, baby + b0, pts + b0, G, Gw, g0, g1, Dw, l, inner,
+                                                b0 > 0);
+        } else if (T.max_qbits <= 59) {
             if (b0)
                 hipLaunchKernelGGL((k_bsgs_inner<VEC, WAVES, 16, true>), grid, block, lds, st, T, baby + b0, pts + b0, G, Gw,
                                    g0, g1, Dw, l, inner);
@@ -2159,9 +2195,9 @@ static hipError_t launch_inner_t(const DevTables& T, const u64* const* baby, con
 }
 
 hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int g0,
-                             int g1, int D, int l, u64* inner, hipStream_t st) {
+                             int g1, int D, int l, u64* inner, hipStream_t st, int ptl) {
     if (T.N % 128 || G < 1) return hipErrorInvalidValue;
-    return launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, g0, g1, D, l, inner, st);
+    return launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, g0, g1, D, l, inner, st, ptl);
 }
 
 // Hadamard (every giant group's inner product; skipped when pts_dev is null and `inner` already holds
@@ -2172,7 +2208,7 @@ hipError_t launch_bsgs_inner(const DevTables& T, const u64* const* baby_dev, con
 hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64* const* pts_dev, int G, int B, int D,
                        int l, const u64* const* keys_host, const u64* const* akeys_host, const u64* giant_elts, u64* inner,
                        u64* out, u64* ws, size_t ws_bytes, void* items_dev, const Stager& sg, hipStream_t st,
-                       const KTimer* tm) {
+                       const KTimer* tm, int ptl) {
     const int R = B - 1;
     const size_t N = T.N, S = (size_t)l * N;
     if (T.N % 128 || G < 1 || R > 512) return hipErrorInvalidValue;
@@ -2207,7 +2243,7 @@ hipError_t launch_bsgs(const DevTables& T, const u64* const* baby_dev, const u64
     hipError_t he = hipSuccess;
     if (pts_dev) {   // null: the B inner products are already in `inner` (giant steps only)
         FHS_TMARK(tm, KID_BSGS_INNER, 1, st);
-        he = launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, 0, B, D, l, inner, st);
+        he = launch_inner_t<FHS_INNER_VEC, FHS_INNER_WAVES>(T, baby_dev, pts_dev, G, 0, B, D, l, inner, st, ptl);
         FHS_TMARK(tm, KID_BSGS_INNER, 0, st);
         if (he != hipSuccess) return he;
     }
@@ -2609,10 +2645,78 @@ __device__ __forceinline__ void enc_finish(const DevTables& T, double2 v, int k,
         out[(size_t)i * N + H + k] = dbl_mod(T, hi, i);
     }
 }
+// ---- periodic rows.  The reference's callers encode tiled vectors (np.tile of a d-vector: the BSGS diagonals,
+// bg:361-378 / tf:48, and encrypt_replicated's input, bg:53-58).  A slot vector with z_{j+d} = z_j, d = (N/2) / t, is
+// the encoding of m(X) = p(X^t): its coefficients vanish off the multiples of t, and p is the encoding of the first d
+// slots in the ring of dimension M = N / t (X -> X^t carries that ring's slot group onto this one's: 5^j mod 2M has
+// period d).  The encoder then runs the d-point FFT of one period instead of the N/2-point FFT of the whole vector
+// (slot j of the first period goes to bin enc_pos[j] >> log t, twist t * enc_twist[t k]), and every limb's forward
+// NTT is the M-point NTT of p with the first M twiddles of the limb's own N-point table (psi^rev_N(i) = (psi^t)^rev_M(i)
+// for i < M), each output repeated t times (bit-reversed order: slot j of the N-point NTT holds slot j >> log t of
+// the M-point one).  The NTT side is exact -- the N-point NTT of the spread coefficients gives the same canonical
+// residues (FHESPEAR_ENCODE_UNFUSED runs it: tests/test_gpu_parity.py) -- and the coefficients off the multiples of t
+// are exact zeros instead of the dense FFT's float64 rounding noise, so the limbs differ from a dense encode of the
+// same vector by that noise, well inside the encoder's precision.  t <= 8, M >= 256; FHESPEAR_ENCODE_DENSE=1 turns
+// it off.  k_enc_period: per row the largest s <= smax with z_{j + (N/2 >> s)} = z_j for every j (bit patterns).
+constexpr int kEncSparseMaxLog = 3, kEncSparseMinLogM = 8;
+__global__ void __launch_bounds__(256) k_enc_period(const double* vals, size_t n, size_t stride, int is_real, int smax,
+                                                    unsigned char* tlog) {
+    __shared__ unsigned bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(vals + (size_t)blockIdx.x * stride);
+    const size_t words = is_real ? n : 2 * n;
+    unsigned b = 0;
+    for (size_t j = threadIdx.x; j < words; j += blockDim.x) {
+        const unsigned long long x = w[j];
+        for (int s = 1; s <= smax; ++s) {
+            const size_t p = words >> s;
+            if (j >= p && x != w[j - p]) b |= 1u << s;
+        }
+    }
+    if (b) atomicOr(&bad, b);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        while (s < smax && !(bad & (2u << s))) ++s;
+        tlog[blockIdx.x] = (unsigned char)s;
+    }
+}
+// coefficient k < d of a periodic row's first period (bin k of its d-point FFT): compact (the M-ring coefficients
+// p_k, p_{d+k} at k, d + k: k_ntt_fwd_from_dbl_sp reads them), or spread over the N-ring (m_{tk}, m_{N/2+tk}, zeros
+// between) into the coefficient scratch or straight into every limb
+template <int LOGN>
+__device__ __forceinline__ void enc_finish_sparse(const DevTables& T, double2 v, int k, int sp, double scale, u64* out,
+                                                  int l, double* dout, bool compact) {
+    constexpr int N = 1 << LOGN, H = N / 2;
+    const int t = 1 << sp;
+    const double2 z0 = reinterpret_cast<const double2*>(T.enc_twist)[k << sp];
+    const double2 z = {z0.x * t, z0.y * t};   // (2/M) zeta_M^-k = t (2/N) zeta^-tk, a power-of-two scaling: exact
+    const double lo = round((v.x * z.x - v.y * z.y) * scale);
+    const double hi = round((v.x * z.y + v.y * z.x) * scale);
+    if (dout && compact) {
+        dout[k] = lo;
+        dout[(H >> sp) + k] = hi;
+        return;
+    }
+    const int e0 = k << sp, e1 = H + (k << sp);
+    if (dout) {
+        dout[e0] = lo;
+        dout[e1] = hi;
+        for (int r = 1; r < t; ++r) dout[e0 + r] = dout[e1 + r] = 0.0;
+        return;
+    }
+    for (int i = 0; i < l; ++i) {
+        u64* o = out + (size_t)i * N;
+        o[e0] = dbl_mod(T, lo, i);
+        o[e1] = dbl_mod(T, hi, i);
+        for (int r = 1; r < t; ++r) o[e0 + r] = o[e1 + r] = 0;
+    }
+}
 template <int LOGN>
 __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024)
     k_encode(DevTables T, const double* vals, size_t n, size_t stride, int is_real, double scale, u64* const* outs,
-             int l, double* coef_out) {
+             int l, double* coef_out, const unsigned char* tlog, int compact) {
     constexpr int N = 1 << LOGN, H = N / 2, LOGH = LOGN - 1;
     constexpr int TH = (N / 16) < 1024 ? (N / 16) : 1024;
     constexpr bool SPLIT = LOGN > 14;   // N = 32768: the H-point FFT as two H/2-point halves + a final stage
@@ -2622,6 +2726,16 @@ __global__ void __launch_bounds__(((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16)
     const double2* W = reinterpret_cast<const double2*>(T.enc_w);
     u64* out = outs ? outs[blockIdx.x] : nullptr;   // null: coefficients to coef_out only
     double* dout = coef_out ? coef_out + (size_t)blockIdx.x * N : nullptr;
+    const int sp = tlog ? tlog[blockIdx.x] : 0;
+    if (sp) {   // a periodic row (k_enc_period, n = N/2): the (N/2 >> sp)-point FFT of its first period
+        const int HM = H >> sp;
+        for (int j = tid; j < HM; j += TH)
+            a[T.enc_pos[j] >> sp] = is_real ? double2{src[j], 0.0} : double2{src[2 * j], src[2 * j + 1]};
+        __syncthreads();
+        enc_fft_stages<LOGN>(a, tid, TH, HM, LOGH - sp, W, LOGH);
+        for (int k = tid; k < HM; k += TH) enc_finish_sparse<LOGN>(T, a[k], k, sp, scale, out, l, dout, compact != 0);
+        return;
+    }
     if constexpr (!SPLIT) {
         for (int j = tid; j < H; j += TH) {
             double2 z = {0.0, 0.0};
@@ -2766,9 +2880,11 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_ptrs(DevTables 
 // written once instead of written, read and rewritten
 template <int LOGN>
 __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_from_dbl(DevTables T, const double* coef,
-                                                                         u64* const* ptrs, int limbs) {
+                                                                         u64* const* ptrs, int limbs,
+                                                                         const unsigned char* tlog) {
     constexpr int N = 1 << LOGN;
     __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN>()];
+    if (tlog && tlog[blockIdx.y]) return;   // a periodic row: k_ntt_fwd_from_dbl_sp
     const int b = blockIdx.x;
     const RedU R = redu(PK(T, b));
     const double* cf = coef + (size_t)blockIdx.y * N;
@@ -2777,29 +2893,92 @@ __global__ void __launch_bounds__(ntt_threads<LOGN>()) k_ntt_fwd_from_dbl(DevTab
     fwd_limb<LOGN, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, enc_lazy(R, M),
                                [&](int e) { return dbl_mod(M, cf[e]); }, [&](int e, u64 v) { p[e] = v; });
 }
+// the same for the rows with tlog = S (see k_enc_period): the 2^(LOGN-S)-point NTT of the compact coefficients,
+// each value stored 2^S times (16-byte stores of two copies)
+// couts (ss <= S): the compact shadow as well, 2^(S - ss) copies per value in limbs of N >> ss words
+template <int LOGN, int S>
+__global__ void __launch_bounds__(ntt_threads<LOGN - S>()) k_ntt_fwd_from_dbl_sp(DevTables T, const double* coef,
+                                                                                u64* const* ptrs, int limbs,
+                                                                                const unsigned char* tlog,
+                                                                                u64* const* couts, int ss) {
+    constexpr int N = 1 << LOGN, LOGM = LOGN - S;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGM>()];
+    if (tlog[blockIdx.y] != S) return;
+    const int b = blockIdx.x;
+    const RedU R = redu(PK(T, b));
+    const double* cf = coef + (size_t)blockIdx.y * N;
+    u64* p = ptrs[blockIdx.y] + (size_t)b * N;
+    u64* pc = couts ? couts[blockIdx.y] + (size_t)b * (N >> ss) : nullptr;
+    const int cs = S - ss;   // log2 of the copies per value in the shadow (wave-uniform)
+    const DblMod M = dbl_mod_of(T, b);
+    fwd_limb<LOGM, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, enc_lazy(R, M),
+                               [&](int e) { return dbl_mod(M, cf[e]); },
+                               [&](int e, u64 v) {
+                                   ulonglong2* d = reinterpret_cast<ulonglong2*>(p + ((size_t)e << S));
+#pragma unroll
+                                   for (int r = 0; r < (1 << S) / 2; ++r) d[r] = ulonglong2{v, v};
+                                   if (pc) {
+                                       u64* c = pc + ((size_t)e << cs);
+                                       if (cs == 0) {
+                                           c[0] = v;
+                                       } else {
+                                           for (int r = 0; r < (1 << cs) / 2; ++r)
+                                               reinterpret_cast<ulonglong2*>(c)[r] = ulonglong2{v, v};
+                                       }
+                                   }
+                               });
+}
+template <int LOGN>
+static void launch_ntt_fwd_sparse(const DevTables& T, const double* coef, u64* const* outs, int l, int count,
+                                  const unsigned char* tlog, u64* const* couts, int ss, hipStream_t st) {
+    static_assert(kEncSparseMaxLog == 3, "one launch per sparse factor below");
+    if constexpr (LOGN - 1 >= kEncSparseMinLogM)
+        if (ss <= 1)
+            hipLaunchKernelGGL((k_ntt_fwd_from_dbl_sp<LOGN, 1>), dim3(l, count), dim3(ntt_threads<LOGN - 1>()), 0, st,
+                               T, coef, outs, l, tlog, couts, ss);
+    if constexpr (LOGN - 2 >= kEncSparseMinLogM)
+        if (ss <= 2)
+            hipLaunchKernelGGL((k_ntt_fwd_from_dbl_sp<LOGN, 2>), dim3(l, count), dim3(ntt_threads<LOGN - 2>()), 0, st,
+                               T, coef, outs, l, tlog, couts, ss);
+    if constexpr (LOGN - 3 >= kEncSparseMinLogM)
+        hipLaunchKernelGGL((k_ntt_fwd_from_dbl_sp<LOGN, 3>), dim3(l, count), dim3(ntt_threads<LOGN - 3>()), 0, st, T,
+                           coef, outs, l, tlog, couts, ss);
+}
+int encode_sparse_max_log(int logN) { return std::max(0, std::min(kEncSparseMaxLog, logN - kEncSparseMinLogM)); }
+hipError_t launch_enc_period(const double* vals, int count, size_t n, size_t stride, bool is_real, int smax,
+                             unsigned char* tlog, hipStream_t st) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_enc_period, dim3(count), dim3(256), 0, st, vals, n, stride, is_real ? 1 : 0, smax, tlog);
+    return hipGetLastError();
+}
 
 hipError_t launch_encode_coef(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
-                              double scale, double* coef, hipStream_t st) {
+                              double scale, double* coef, hipStream_t st, const unsigned char* tlog) {
     if (count <= 0) return hipSuccess;
     FHS_DISPATCH_LOGN(T.logN, {
         constexpr int TH = ((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024;
         hipLaunchKernelGGL((k_encode<LOGN>), dim3(count), dim3(TH), 0, st, T, vals, n, stride, is_real ? 1 : 0, scale,
-                           static_cast<u64* const*>(nullptr), 0, coef);
+                           static_cast<u64* const*>(nullptr), 0, coef, tlog, 0);
     });
     return hipGetLastError();
 }
 hipError_t launch_encode(const DevTables& T, const double* vals, int count, size_t n, size_t stride, bool is_real,
-                         double scale, u64* const* outs_dev, int l, hipStream_t st, double* coef_scratch) {
+                         double scale, u64* const* outs_dev, int l, hipStream_t st, double* coef_scratch,
+                         const unsigned char* tlog, u64* const* couts_dev, int ss) {
     if (count <= 0) return hipSuccess;
+    if (couts_dev && (!coef_scratch || !tlog || ss < 1 || ss > kEncSparseMaxLog)) return hipErrorInvalidValue;
+    if (!couts_dev) ss = 0;
     FHS_DISPATCH_LOGN(T.logN, {
         constexpr int TH = ((1 << LOGN) / 16) < 1024 ? ((1 << LOGN) / 16) : 1024;
         hipLaunchKernelGGL((k_encode<LOGN>), dim3(count), dim3(TH), 0, st, T, vals, n, stride, is_real ? 1 : 0, scale,
-                           outs_dev, l, coef_scratch);
-        if (coef_scratch)
+                           outs_dev, l, coef_scratch, tlog, coef_scratch ? 1 : 0);
+        if (coef_scratch) {
             hipLaunchKernelGGL((k_ntt_fwd_from_dbl<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T,
-                               static_cast<const double*>(coef_scratch), outs_dev, l);
-        else
+                               static_cast<const double*>(coef_scratch), outs_dev, l, tlog);
+            if (tlog) launch_ntt_fwd_sparse<LOGN>(T, coef_scratch, outs_dev, l, count, tlog, couts_dev, ss, st);
+        } else {   // unfused: the spread coefficients in every limb, the N-point NTT in place
             hipLaunchKernelGGL((k_ntt_fwd_ptrs<LOGN>), dim3(l, count), dim3(ntt_threads<LOGN>()), 0, st, T, outs_dev, l);
+        }
     });
     return hipGetLastError();
 }

@@ -417,7 +417,11 @@ for N, L0 in ((4096, 8), (32768, 3)):
     r = enc.encode_double_vector_batch(ctx, rng.normal(0, 3, (3, N // 2)), 2.0 ** 59, chain_index=1)
     z = rng.normal(0, 3, (2, N // 2)) + 1j * rng.normal(0, 3, (2, N // 2))
     c = enc.encode_complex_vector_batch(ctx, z, 2.0 ** 70, chain_index=2)
-    out += [p.to_numpy().ravel() for p in r + c]
+    # periodic rows (the sparse form, t = 2, 4, 8 in one batch, and complex t = 4)
+    per = [np.tile(rng.normal(0, 3, N // 2 // t), t) for t in (2, 4, 8, 16)]
+    rp = enc.encode_double_vector_batch(ctx, np.stack(per), 2.0 ** 59, chain_index=1)
+    cp = enc.encode_complex_vector_batch(ctx, np.tile(z[:, :N // 8], (1, 4)), 2.0 ** 70, chain_index=2)
+    out += [p.to_numpy().ravel() for p in r + c + rp + cp]
 np.save(sys.argv[1], np.concatenate(out))
 '''
 
@@ -425,7 +429,9 @@ np.save(sys.argv[1], np.concatenate(out))
 def test_encode_fused_ntt_equals_unfused(require_gpu, tmp_path):
     """The encoder's fused exact-reduction + NTT (k_ntt_fwd_from_dbl) gives the same limbs as
     reducing into every limb and transforming in place (FHESPEAR_ENCODE_UNFUSED=1), at N = 4096 and
-    at N = 32768 (split FFT, half-limb NTT), real and complex, scales 2^59 and 2^70."""
+    at N = 32768 (split FFT, half-limb NTT), real and complex, scales 2^59 and 2^70 -- and for periodic rows
+    the (N/t)-point NTTs of the sparse form (k_ntt_fwd_from_dbl_sp, t = 2, 4, 8) give the limbs of the N-point NTT
+    of the spread coefficients (the unfused path)."""
     import os
     import subprocess
     import sys as _sys
@@ -444,6 +450,72 @@ def test_encode_fused_ntt_equals_unfused(require_gpu, tmp_path):
         assert r.returncode == 0, r.stderr[-3000:]
         outs.append(np.load(f))
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("N,t", [(4096, 2), (4096, 16), (16384, 4), (32768, 8)])
+def test_encode_periodic_rows_take_the_sparse_form(ph, N, t):
+    """Tiled rows (np.tile of an (N/2t)-vector: the reference's diagonals, bg:361-378, and replicated inputs,
+    bg:53-58) are encoded as p(X^t'), t' = min(t, 8) (fhs_kernels.hip k_enc_period): in coefficient form (the
+    oracle's INTT of every limb) the coefficients off the multiples of t' are exact zeros, in NTT form every value
+    repeats t' times, and the slots decode to the input as closely as the dense encoder's do.  A row that breaks the
+    period in one value keeps the dense form."""
+    ctx, _, primes = make_ctx(ph, N, 3, 1, seed=31)
+    enc = ph.ckks_encoder(ctx)
+    o = oracle_for(primes, N, 1)
+    rng = np.random.default_rng(N + t)
+    d, tt = N // 2 // t, min(t, 8)
+    x = rng.normal(0, 1, d)
+    z = rng.normal(0, 1, d) + 1j * rng.normal(0, 1, d)
+    off = np.arange(N) % tt != 0
+    for want, pt in ((np.tile(x, t), enc.encode_double_vector(ctx, np.tile(x, t), 2.0 ** 40)),
+                     (np.tile(z, t), enc.encode_complex_vector(ctx, np.tile(z, t), 2.0 ** 40))):
+        limbs = pt.to_numpy()
+        assert (limbs.reshape(limbs.shape[0], N // tt, tt) == limbs[:, ::tt, None]).all()
+        for i in range(limbs.shape[0]):
+            assert not o.intt(limbs[i], i)[off].any(), f"limb {i}: nonzero coefficient off the multiples of {tt}"
+        if np.iscomplexobj(want):
+            dec = np.array(enc.decode_complex_vector(ctx, pt))
+        else:
+            dec = np.array(enc.decode_double_vector(ctx, pt))
+        assert np.max(np.abs(dec - want)) < 1e-6
+    y = np.tile(x, t)
+    y[-1] += 1.0
+    limbs = enc.encode_double_vector(ctx, y, 2.0 ** 40).to_numpy()
+    assert o.intt(limbs[0], 0)[off].any()
+    assert np.max(np.abs(np.array(enc.decode_double_vector(ctx, enc.encode_double_vector(ctx, y, 2.0 ** 40))) - y)) < 1e-6
+
+
+@pytest.mark.parametrize("N,D,L0", [(4096, 1024, 4), (16384, 2048, 3), (32768, 2048, 3), (32768, 8192, 2)])
+def test_bsgs_compact_diagonals_equal_dense(ph, N, D, L0):
+    """Tiled diagonals (encode_matrix_diagonals, bg:361-378) carry a compact shadow (word e >> t of each limb
+    holds dense word e, t = log2 of the tiling, at most 3) that the fused BSGS's Hadamard reads instead of the
+    dense limbs (k_bsgs_inner<..., TL>): the matvec, the inner products alone and the linear transform give the
+    limbs of the same call on dense copies of the same plaintexts (plaintext_from_numpy: no shadow).  D = 8192
+    (G = 91) takes the baby-step windows (G > 64) on compact diagonals."""
+    G = int(np.ceil(np.sqrt(D)))
+    B = -(-D // G)
+    steps = list(range(1, G)) + [g * G for g in range(1, B)]
+    ctx, sk, _ = make_ctx(ph, N, L0, 1, steps=steps, seed=41)
+    gk = sk.create_galois_keys(ctx)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(N + D)
+    x = rng.normal(0, 0.1, D)
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, np.tile(x, N // 2 // D), 2.0 ** 50))
+    baby = [ct] + [ph.rotate(ctx, ct, b, gk) for b in range(1, G)]
+    W = rng.normal(0, 0.02, (D, D))
+    pts = enc.encode_matrix_diagonals(ctx, W, G, 2.0 ** 50, chain_index=ct.chain_index())
+    dense = [ph.plaintext_from_numpy(ctx, p.to_numpy(), p.chain_index(), p.scale()) for p in pts]
+    got = ph.bsgs_multiply_accumulate(ctx, baby, pts, G, B, D, gk).to_numpy()
+    want = ph.bsgs_multiply_accumulate(ctx, baby, dense, G, B, D, gk).to_numpy()
+    assert np.array_equal(got, want)
+    if D == 2048 and N == 16384:
+        dec = np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, ph.bsgs_multiply_accumulate(
+            ctx, baby, pts, G, B, D, gk))))[:D]
+        assert np.max(np.abs(dec - W @ x)) < 1e-4
+        Bi = 3
+        gi = [c.to_numpy() for c in ph.bsgs_inner_products(ctx, baby, pts[:Bi * G], G, Bi)]
+        wi = [c.to_numpy() for c in ph.bsgs_inner_products(ctx, baby, dense[:Bi * G], G, Bi)]
+        assert all(np.array_equal(a, b) for a, b in zip(gi, wi))
 
 
 def _bg_rows(W, D, G, slots):
@@ -862,7 +934,10 @@ def test_fused_client_calls_equal_separate_calls(ph):
     rng = np.random.default_rng(53)
     real = rng.normal(0, 1, (3, N // 2))
     cplx = rng.normal(0, 1, (2, 100)) + 1j * rng.normal(0, 1, (2, 100))
-    for rows, ci in ((real, 1), (cplx, 1), (real[:1], 3), (cplx, 2)):
+    # periodic rows (encode_*_batch's sparse form): the fused call must detect them the same way
+    tiled = np.concatenate([np.tile(rng.normal(0, 1, (2, N // 16)), (1, 8)), real[:1]])
+    tiledc = np.tile(rng.normal(0, 1, (2, N // 4)) + 1j * rng.normal(0, 1, (2, N // 4)), (1, 2))
+    for rows, ci in ((real, 1), (cplx, 1), (real[:1], 3), (cplx, 2), (tiled, 1), (tiledc, 2)):
         batch = enc.encode_complex_vector_batch if np.iscomplexobj(rows) else enc.encode_double_vector_batch
         want = a.encrypt_symmetric_batch(ctx, batch(ctx, rows, 2.0 ** 40, ci))
         got = b.encode_encrypt_batch(ctx, rows, 2.0 ** 40, ci)
