@@ -650,6 +650,29 @@ static fhs_status new_pts(fhs_context* c, size_t count, int ci, double scale, fh
 }
 static size_t ct_bytes(const fhs_ciphertext* ct) { return 8ull * ct->ncomp * ct->l * ct->ctx->N; }
 static size_t pt_bytes(const fhs_plaintext* pt) { return 8ull * pt->l * pt->ctx->N; }
+// The dense limbs of a plaintext.  A compact-only one (a periodic diagonal batch, encode_rows_dev) gets them on first
+// use -- expanded from its shadow on the stream (k_expand_compact) and kept for the rest of its life, so the fused
+// BSGS, which reads the shadow, never pays for them.  Plaintexts are immutable: the two copies never diverge.
+static hipError_t pt_dense(fhs_context* c, const fhs_plaintext* cpt, const uint64_t** out) {
+    auto* pt = const_cast<fhs_plaintext*>(cpt);
+    if (!pt->d) {
+        if (!pt->dc) return hipErrorInvalidValue;
+        uint64_t* d = nullptr;
+        hipError_t e = dalloc(c, &d, pt_bytes(pt));
+        if (e != hipSuccess) return e;
+        e = fhs::launch_expand_compact(pt->dc, d, pt->l, c->N, pt->tlog, c->st);
+        if (e != hipSuccess) {
+            dfree(c, d, pt_bytes(pt));
+            return e;
+        }
+        pt->d = d;
+    }
+    *out = pt->d;
+    return hipSuccess;
+}
+#define PT_DENSE(var, pt, where)        \
+    const uint64_t* var = nullptr;      \
+    HIPCHK(pt_dense(c, (pt), &var), where)
 
 // ---------------------------------------------------------------- timing events
 // A pool of timing events per device: hipEventCreate can take milliseconds now and then (it may
@@ -1784,7 +1807,8 @@ extern "C" fhs_status fhs_ciphertext_export(fhs_context* c, const fhs_ciphertext
 extern "C" fhs_status fhs_plaintext_export(fhs_context* c, const fhs_plaintext* pt, uint64_t* host) {
     ENTER(c);
     if (!pt || !host) return fail(FHS_ERR_INVALID, "null argument");
-    return export_dev(c, pt->d, pt_bytes(pt), host);
+    PT_DENSE(pd, pt, "plaintext_export");
+    return export_dev(c, pd, pt_bytes(pt), host);
 }
 extern "C" fhs_status fhs_ciphertext_import(fhs_context* c, const uint64_t* host, int ncomp, int ci, double scale,
                                             fhs_ciphertext** out) {
@@ -1882,28 +1906,41 @@ static hipError_t enc_periods(fhs_context* c, const double* dvals, size_t cnt, s
 }
 // Encode `cnt` value rows already in HBM (row v at dvals + v * stride doubles) into new plaintexts.
 // A batch of >= 32 rows (diagonal batches, not a client's few vectors) whose every row is periodic (tlog >= 1, read
-// back after k_enc_period: one wait per batch) also gets the
-// compact shadow at the batch's smallest tlog (fhs_plaintext::dc), which the fused BSGS's Hadamard reads instead
-// of the dense limbs; without the device memory for it the batch is simply dense.  FHESPEAR_ENCODE_NO_SHADOW=1 skips
-// it.
+// back after k_enc_period: one wait per batch) is stored compact only, at the batch's smallest tlog
+// (fhs_plaintext::dc): the fused BSGS's Hadamard reads it as it is, every other op through pt_dense.  Otherwise (or
+// without room for the compact block, or FHESPEAR_ENCODE_NO_SHADOW=1) the batch is dense.
+static fhs_status new_pts_compact(fhs_context* c, size_t count, int ci, double scale, int tlog, fhs_plaintext** outs) {
+    const int l = c->L0 + 1 - ci;
+    const size_t per = (size_t)l * (c->N >> tlog);
+    auto* cs = new PtSlab{nullptr, 8 * count * per, 0};
+    hipError_t e = dalloc_fit(c, &cs->base, &cs->bytes);
+    if (e != hipSuccess) {
+        delete cs;
+        return hip_fail(e, "plaintext allocation");
+    }
+    for (size_t k = 0; k < count; ++k) {
+        outs[k] = new fhs_plaintext{c, nullptr, ci, l, scale};
+        outs[k]->dc = cs->base + k * per;
+        outs[k]->tlog = tlog;
+        outs[k]->cslab = cs;
+        ++cs->refs;
+        ctx_retain(c);
+    }
+    return FHS_OK;
+}
 static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cnt, size_t n, size_t stride,
                                   bool is_real, double scale, int ci, fhs_plaintext** outs) {
     const int l = c->L0 + 1 - ci;
-    std::vector<uint64_t*> ptrs(2 * cnt, nullptr);
-    fhs_status s0 = new_pts(c, cnt, ci, scale, outs);
-    if (s0 != FHS_OK) return s0;
-    for (size_t v = 0; v < cnt; ++v) ptrs[v] = outs[v]->d;
-    uint64_t* dptrs = nullptr;
-    hipError_t e = scratch(c, fhs_context::SCR_ENC_PTRS, 16 * cnt, &dptrs);
+    if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
     // fused reduction + NTT through a scratch of rounded coefficients (FHESPEAR_ENCODE_UNFUSED=1: the
     // encoder reduces into every limb and the NTT runs in place -- same limbs, A/B and test knob)
     static const bool unfused = getenv("FHESPEAR_ENCODE_UNFUSED") != nullptr;
     static const bool no_shadow = getenv("FHESPEAR_ENCODE_NO_SHADOW") != nullptr;
-    uint64_t* coef = nullptr;
+    uint64_t *coef = nullptr, *tl = nullptr, *dptrs = nullptr;
     const size_t cbytes = 8 * cnt * c->N;
-    if (e == hipSuccess && !unfused) e = dalloc(c, &coef, cbytes);
-    uint64_t* tl = nullptr;
     size_t tbytes = 0;
+    hipError_t e = hipSuccess;
+    if (!unfused) e = dalloc(c, &coef, cbytes);
     if (e == hipSuccess) e = enc_periods(c, dvals, cnt, n, stride, is_real, &tl, &tbytes);
     int ss = 0;
     if (e == hipSuccess && tl && coef && !no_shadow && c->T.max_qbits <= 59 && cnt >= 32) {
@@ -1911,31 +1948,29 @@ static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cn
         e = hipMemcpyAsync(th.data(), tl, cnt, hipMemcpyDeviceToHost, c->st);
         if (e == hipSuccess) e = hipStreamSynchronize(c->st);
         if (e == hipSuccess) ss = *std::min_element(th.begin(), th.end());
-        if (ss > 0) {
-            const size_t per = (size_t)l * (c->N >> ss);
-            auto* cs = new PtSlab{nullptr, 8 * cnt * per, 0};
-            if (dalloc_fit(c, &cs->base, &cs->bytes) == hipSuccess) {
-                for (size_t v = 0; v < cnt; ++v) {
-                    outs[v]->dc = cs->base + v * per;
-                    outs[v]->tlog = ss;
-                    outs[v]->cslab = cs;
-                    ++cs->refs;
-                    ptrs[cnt + v] = outs[v]->dc;
-                }
-            } else {
-                (void)hipGetLastError();   // no room for the shadow: a dense batch
-                delete cs;
-                ss = 0;
-            }
-        }
     }
-    if (e == hipSuccess) e = stage_h2d(c, dptrs, ptrs.data(), 16 * cnt);
-    if (e == hipSuccess)
+    fhs_status s0 = FHS_OK;
+    if (e == hipSuccess && ss > 0 && new_pts_compact(c, cnt, ci, scale, ss, outs) != FHS_OK) {
+        (void)hipGetLastError();   // no room for the compact block: a dense batch
+        ss = 0;
+    }
+    if (e == hipSuccess && ss == 0) s0 = new_pts(c, cnt, ci, scale, outs);
+    std::vector<uint64_t*> ptrs(2 * cnt, nullptr);
+    if (e == hipSuccess && s0 == FHS_OK) {
+        for (size_t v = 0; v < cnt; ++v) {
+            ptrs[v] = outs[v]->d;   // null for a compact batch
+            ptrs[cnt + v] = outs[v]->dc;
+        }
+        e = scratch(c, fhs_context::SCR_ENC_PTRS, 16 * cnt, &dptrs);
+    }
+    if (e == hipSuccess && s0 == FHS_OK) e = stage_h2d(c, dptrs, ptrs.data(), 16 * cnt);
+    if (e == hipSuccess && s0 == FHS_OK)
         e = fhs::launch_encode(c->T, dvals, (int)cnt, n, stride, is_real, scale, reinterpret_cast<fhs::u64* const*>(dptrs),
                                l, c->st, reinterpret_cast<double*>(coef), reinterpret_cast<const unsigned char*>(tl),
                                ss ? reinterpret_cast<fhs::u64* const*>(dptrs + cnt) : nullptr, ss);
     if (tl) dfree(c, tl, tbytes);
     if (coef) dfree(c, coef, cbytes);
+    if (s0 != FHS_OK) return s0;
     return e == hipSuccess ? FHS_OK : hip_fail(e, "encode");
 }
 static fhs_status encode_checks(fhs_context* c, size_t n, double scale, int ci) {
@@ -2366,7 +2401,9 @@ static fhs_status decode_coeffs_dev(fhs_context* c, const fhs_plaintext* pt, int
     if (e != hipSuccess) { dfree(c, dbl, 8 * N); dfree(c, tmp, bytes); return hip_fail(e, "decode"); }
     unsigned* flag = reinterpret_cast<unsigned*>(aux + vt.size());
     unsigned hflag = 0;
-    e = hipMemcpyAsync(tmp, pt->d, bytes, hipMemcpyDeviceToDevice, c->st);
+    const uint64_t* pd = nullptr;
+    e = pt_dense(c, pt, &pd);
+    if (e == hipSuccess) e = hipMemcpyAsync(tmp, pd, bytes, hipMemcpyDeviceToDevice, c->st);
     if (e == hipSuccess && nx > 0) e = stage_h2d(c, aux, vt.data(), 8 * vt.size());
     if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4, c->st);
     if (e == hipSuccess) e = fhs::launch_ntt_inv(c->T, tmp, lv, lv, 1, 0, c->st);
@@ -2387,8 +2424,9 @@ static fhs_status decode_coeffs_dev(fhs_context* c, const fhs_plaintext* pt, int
 static fhs_status decode_coeffs(fhs_context* c, const fhs_plaintext* pt, int k, std::vector<uint64_t>& host) {
     const size_t N = c->N, bytes = 8ull * k * N;
     uint64_t* tmp = nullptr;
+    PT_DENSE(pd, pt, "decode");
     HIPCHK(dalloc(c, &tmp, bytes), "decode");
-    HIPCHK(hipMemcpyAsync(tmp, pt->d, bytes, hipMemcpyDeviceToDevice, c->st), "decode");
+    HIPCHK(hipMemcpyAsync(tmp, pd, bytes, hipMemcpyDeviceToDevice, c->st), "decode");
     HIPCHK(fhs::launch_ntt_inv(c->T, tmp, k, k, 1, 0, c->st), "decode");
     host.resize((size_t)k * N);
     HIPCHK(hipMemcpyAsync(host.data(), tmp, bytes, hipMemcpyDeviceToHost, c->st), "decode");
@@ -2546,8 +2584,11 @@ static fhs_status decode_many(fhs_context* c, const fhs_plaintext* const* pts, i
         for (int i = 0; e == hipSuccess && i < count; ++i) {
             if (!fast[i]) continue;
             const int l = lv(i);
-            e = cts ? fhs::launch_decrypt(c->T, cts[i]->d, cts[i]->ncomp, sk->s, tmp + to, l, c->st)
-                    : hipMemcpyAsync(tmp + to, pts[i]->d, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
+            const uint64_t* pd = nullptr;
+            if (!cts) e = pt_dense(c, pts[i], &pd);
+            if (e == hipSuccess)
+                e = cts ? fhs::launch_decrypt(c->T, cts[i]->d, cts[i]->ncomp, sk->s, tmp + to, l, c->st)
+                        : hipMemcpyAsync(tmp + to, pd, 8ull * l * N, hipMemcpyDeviceToDevice, c->st);
             if (e == hipSuccess && !one_l) e = fhs::launch_ntt_inv(c->T, tmp + to, l, l, 1, 0, c->st);
             to += (size_t)l * N;
         }
@@ -2652,7 +2693,8 @@ extern "C" fhs_status fhs_encrypt_symmetric(fhs_context* c, fhs_secret_key* sk, 
     HIPCHK(dalloc(c, &eb, 8 * S), "encrypt");
     HIPCHK(fhs::launch_sample(c->T, fhs::SAMPLE_UNIFORM, sk->key, stream_id(ST_ENC_SYM, ctr, 0), ct->d + S, l, c->st), "encrypt");
     HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, sk->key, stream_id(ST_ENC_SYM, ctr, 1), eb, l), "encrypt");
-    HIPCHK(fhs::launch_encrypt_combine(c->T, 0, ct->d, ct->d + S, sk->s, nullptr, nullptr, eb, nullptr, pt->d, l, c->st),
+    PT_DENSE(pd, pt, "encrypt");
+    HIPCHK(fhs::launch_encrypt_combine(c->T, 0, ct->d, ct->d + S, sk->s, nullptr, nullptr, eb, nullptr, pd, l, c->st),
            "encrypt");
     dfree(c, eb, 8 * S);
     *out = ct;
@@ -2677,7 +2719,11 @@ static fhs_status encrypt_sym_core(fhs_context* c, fhs_secret_key* sk, int count
     std::vector<uint64_t*> ptrs(2 * (size_t)count, nullptr);
     for (int i = 0; i < count; ++i) {
         ptrs[i] = outs[i]->d;
-        if (pts) ptrs[count + i] = pts[i]->d;
+        if (pts) {
+            const uint64_t* pd = nullptr;
+            HIPCHK(pt_dense(c, pts[i], &pd), "encrypt");
+            ptrs[count + i] = const_cast<uint64_t*>(pd);
+        }
     }
     uint64_t *eb = nullptr, *dptrs = nullptr, *small = nullptr;
     const size_t small_b = ((size_t)c->N * count + 7) & ~(size_t)7;
@@ -2780,7 +2826,8 @@ extern "C" fhs_status fhs_encrypt_asymmetric(fhs_context* c, fhs_public_key* pk,
     HIPCHK(sample_small_ntt(c, fhs::SAMPLE_TERNARY, pk->rng, stream_id(ST_ENC_ASYM, ctr, 0), u, l), "encrypt");
     HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, pk->rng, stream_id(ST_ENC_ASYM, ctr, 1), e0, l), "encrypt");
     HIPCHK(sample_small_ntt(c, fhs::SAMPLE_CBD, pk->rng, stream_id(ST_ENC_ASYM, ctr, 2), e1, l), "encrypt");
-    HIPCHK(fhs::launch_encrypt_combine(c->T, 1, ct->d, ct->d + S, pk->pk, pk->pk + SL, u, e0, e1, pt->d, l, c->st),
+    PT_DENSE(pd, pt, "encrypt");
+    HIPCHK(fhs::launch_encrypt_combine(c->T, 1, ct->d, ct->d + S, pk->pk, pk->pk + SL, u, e0, e1, pd, l, c->st),
            "encrypt");
     dfree(c, tmp, 24 * S);
     *out = ct;
@@ -2852,7 +2899,8 @@ static fhs_status plainop(fhs_context* c, int op, const fhs_ciphertext* a, const
     fhs_status s = new_ct(c, a->ncomp, a->ci, sc, &r);
     if (s != FHS_OK) return s;
     const size_t cs = (size_t)a->l * c->N;
-    HIPCHK(fhs::launch_eltwise(c->T, op, a->d, p->d, r->d, a->ncomp, a->l, cs, 0, c->st), "plain op");
+    PT_DENSE(pd, p, "plain op");
+    HIPCHK(fhs::launch_eltwise(c->T, op, a->d, pd, r->d, a->ncomp, a->l, cs, 0, c->st), "plain op");
     *out = r;
     return FHS_OK;
 }
@@ -2961,7 +3009,8 @@ static fhs_status drop_pt(fhs_context* c, const fhs_plaintext* a, int ci, fhs_pl
     fhs_plaintext* r;
     fhs_status s = new_pt(c, ci, a->scale, &r);
     if (s != FHS_OK) return s;
-    HIPCHK(hipMemcpyAsync(r->d, a->d, pt_bytes(r), hipMemcpyDeviceToDevice, c->st), "mod_switch");
+    PT_DENSE(pd, a, "mod_switch");
+    HIPCHK(hipMemcpyAsync(r->d, pd, pt_bytes(r), hipMemcpyDeviceToDevice, c->st), "mod_switch");
     *out = r;
     return FHS_OK;
 }
@@ -3118,7 +3167,10 @@ extern "C" fhs_status fhs_bsgs_multiply_accumulate(fhs_context* c, const fhs_cip
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs: diagonal scales differ");
     }
     const int ptl = pts_ptl(c, pts, D);
-    for (int k = 0; k < D; ++k) p[k] = ptl ? pts[k]->dc : pts[k]->d;
+    for (int k = 0; k < D; ++k) {
+        p[k] = pts[k]->dc;
+        if (!ptl) HIPCHK(pt_dense(c, pts[k], &p[k]), "bsgs");
+    }
     return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out, nullptr, true, ptl);
 }
 
@@ -3143,7 +3195,10 @@ static fhs_status inner_products_core(fhs_context* c, const fhs_ciphertext* cons
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "bsgs_inner_products: plaintext scales differ");
     }
     const int ptl = pts_ptl(c, pts, D);
-    for (int k = 0; k < D; ++k) ptrs[G + k] = ptl ? pts[k]->dc : pts[k]->d;
+    for (int k = 0; k < D; ++k) {
+        ptrs[G + k] = pts[k]->dc;
+        if (!ptl) HIPCHK(pt_dense(c, pts[k], &ptrs[G + k]), "bsgs_inner_products");
+    }
     HIPCHK(stage_h2d(c, c->ptrs_dev, ptrs.data(), sizeof(void*) * (G + D)), "bsgs_inner_products");
     const uint64_t* const* dbaby = reinterpret_cast<const uint64_t* const*>(c->ptrs_dev);
     HIPCHK(fhs::launch_bsgs_inner(c->T, dbaby, dbaby + G, G, 0, B, D, l, dst, c->st, ptl), "bsgs_inner_products");
@@ -3267,7 +3322,10 @@ extern "C" fhs_status fhs_linear_transform(fhs_context* c, const fhs_ciphertext*
         if (!scales_close(pts[k]->scale, pts[0]->scale)) return fail(FHS_ERR_SCALE, "linear_transform: plaintext scales differ");
     }
     const int ptl = pts_ptl(c, pts, D);
-    for (int k = 0; k < D; ++k) p[k] = ptl ? pts[k]->dc : pts[k]->d;
+    for (int k = 0; k < D; ++k) {
+        p[k] = pts[k]->dc;
+        if (!ptl) HIPCHK(pt_dense(c, pts[k], &p[k]), "linear_transform");
+    }
     for (int g = 0; g < B; ++g)
         if ((giant_elts[g] & 1) == 0 || giant_elts[g] >= 2 * c->N) return fail(FHS_ERR_INVALID, "linear_transform: bad Galois element");
     return bsgs_core(c, baby, G, p.data(), D, B, baby[0]->ci, pts[0]->scale, gk, out, giant_elts, rescale != 0, ptl);
@@ -3555,7 +3613,8 @@ extern "C" fhs_status fhs_offload_plaintexts(fhs_context* c, const fhs_plaintext
     const size_t b = pt_bytes(pts[0]);
     for (int k = 0; k < count; ++k) {
         if (pts[k]->l != pts[0]->l) return fail(FHS_ERR_LEVEL, "offload: plaintexts at different levels");
-        HIPCHK(hipMemcpyAsync((char*)host + (size_t)k * b, pts[k]->d, b, hipMemcpyDeviceToHost, c->st), "offload");
+        PT_DENSE(pd, pts[k], "offload");
+        HIPCHK(hipMemcpyAsync((char*)host + (size_t)k * b, pd, b, hipMemcpyDeviceToHost, c->st), "offload");
     }
     HIPCHK(hipStreamSynchronize(c->st), "offload");
     return FHS_OK;

@@ -163,6 +163,8 @@ hipError_t launch_encode(const DevTables& T, const double* vals, int count, size
 hipError_t launch_enc_period(const double* vals, int count, size_t n, size_t stride, bool is_real, int smax,
                              unsigned char* tlog, hipStream_t st);
 int encode_sparse_max_log(int logN);   // the smax the encoder supports at this ring (0: none)
+// dense limbs (l x N) of a compact plaintext (l x N >> tl, word e >> tl = dense word e)
+hipError_t launch_expand_compact(const u64* dc, u64* d, int l, int N, int tl, hipStream_t st);
 // SAMPLE_UNIFORM / TERNARY / CBD draw from the ChaCha20 PRF stream (K, sid); SAMPLE_SEEDED expands
 // the public seed `sid` (switching-key a_j); SAMPLE_TESTDATA is the non-secret SplitMix64 uniform of
 // random_plaintexts (K unused)

@@ -2907,16 +2907,18 @@ __global__ void __launch_bounds__(ntt_threads<LOGN - S>()) k_ntt_fwd_from_dbl_sp
     const int b = blockIdx.x;
     const RedU R = redu(PK(T, b));
     const double* cf = coef + (size_t)blockIdx.y * N;
-    u64* p = ptrs[blockIdx.y] + (size_t)b * N;
+    u64* p = ptrs[blockIdx.y] ? ptrs[blockIdx.y] + (size_t)b * N : nullptr;   // null: a compact-only plaintext
     u64* pc = couts ? couts[blockIdx.y] + (size_t)b * (N >> ss) : nullptr;
     const int cs = S - ss;   // log2 of the copies per value in the shadow (wave-uniform)
     const DblMod M = dbl_mod_of(T, b);
     fwd_limb<LOGM, FHS_NTT_RL>(lds, threadIdx.x, T.tw_fwd + (size_t)b * N * 2, enc_lazy(R, M),
                                [&](int e) { return dbl_mod(M, cf[e]); },
                                [&](int e, u64 v) {
-                                   ulonglong2* d = reinterpret_cast<ulonglong2*>(p + ((size_t)e << S));
+                                   if (p) {
+                                       ulonglong2* d = reinterpret_cast<ulonglong2*>(p + ((size_t)e << S));
 #pragma unroll
-                                   for (int r = 0; r < (1 << S) / 2; ++r) d[r] = ulonglong2{v, v};
+                                       for (int r = 0; r < (1 << S) / 2; ++r) d[r] = ulonglong2{v, v};
+                                   }
                                    if (pc) {
                                        u64* c = pc + ((size_t)e << cs);
                                        if (cs == 0) {
@@ -2943,6 +2945,21 @@ static void launch_ntt_fwd_sparse(const DevTables& T, const double* coef, u64* c
     if constexpr (LOGN - 3 >= kEncSparseMinLogM)
         hipLaunchKernelGGL((k_ntt_fwd_from_dbl_sp<LOGN, 3>), dim3(l, count), dim3(ntt_threads<LOGN - 3>()), 0, st, T,
                            coef, outs, l, tlog, couts, ss);
+}
+// dense limbs of a compact plaintext (fhs_host.hip pt_dense): d[i N + e] = dc[i (N >> tl) + (e >> tl)]
+__global__ void k_expand_compact(const u64* __restrict__ dc, u64* __restrict__ d, int l, int N, int tl) {
+    const size_t total = (size_t)l * N;
+    const int Nc = N >> tl;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+        const size_t i = idx / N;
+        const int e = (int)(idx - i * N);
+        d[idx] = dc[i * Nc + (e >> tl)];
+    }
+}
+hipError_t launch_expand_compact(const u64* dc, u64* d, int l, int N, int tl, hipStream_t st) {
+    if (tl < 1 || tl > kEncSparseMaxLog || l < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_expand_compact, dim3(eltwise_grid((size_t)l * N)), dim3(256), 0, st, dc, d, l, N, tl);
+    return hipGetLastError();
 }
 int encode_sparse_max_log(int logN) { return std::max(0, std::min(kEncSparseMaxLog, logN - kEncSparseMinLogM)); }
 hipError_t launch_enc_period(const double* vals, int count, size_t n, size_t stride, bool is_real, int smax,

@@ -518,6 +518,37 @@ def test_bsgs_compact_diagonals_equal_dense(ph, N, D, L0):
         assert all(np.array_equal(a, b) for a, b in zip(gi, wi))
 
 
+def test_compact_plaintexts_behave_as_dense(ph):
+    """A batch of >= 32 periodic rows is stored compact only (fhs_host.hip new_pts_compact): every op other than the
+    fused BSGS's Hadamard expands it on first use (pt_dense), so multiply_plain / add_plain, decode, encryption,
+    plain mod_switch, export and offload_plaintexts see the limbs of the same rows encoded one at a time (dense)."""
+    N, L0 = 4096, 4
+    ctx, sk, _ = make_ctx(ph, N, L0, 1, seed=61)
+    enc = ph.ckks_encoder(ctx)
+    rng = np.random.default_rng(62)
+    rows = np.tile(rng.normal(0, 1, (40, N // 8)), (1, 4))
+    ct = sk.encrypt_symmetric(ctx, enc.encode_double_vector(ctx, rng.normal(0, 1, N // 2), 2.0 ** 40, 2))
+
+    def fresh():
+        return enc.encode_double_vector_batch(ctx, rows, 2.0 ** 40, chain_index=2)
+    single = [enc.encode_double_vector(ctx, rows[k], 2.0 ** 40, 2) for k in (0, 7, 39)]
+    for op in (ph.multiply_plain, ph.add_plain):   # the first use of each compact plaintext is the op itself
+        b = fresh()
+        for k, s in zip((0, 7, 39), single):
+            assert np.array_equal(op(ctx, ct, b[k]).to_numpy(), op(ctx, ct, s).to_numpy())
+    b = fresh()
+    assert np.array_equal(np.array(enc.decode_double_vector(ctx, b[7])), np.array(enc.decode_double_vector(ctx, single[1])))
+    b = fresh()
+    assert np.array_equal(ph.mod_switch_to_next(ctx, b[39]).to_numpy(), ph.mod_switch_to_next(ctx, single[2]).to_numpy())
+    b = fresh()
+    dec = np.array(enc.decode_double_vector(ctx, sk.decrypt(ctx, sk.encrypt_symmetric(ctx, b[0]))))
+    assert np.max(np.abs(dec - rows[0])) < 1e-6
+    b = fresh()
+    data = ph.offload_plaintexts(b)
+    assert np.array_equal(np.asarray(data[0])[7], single[1].to_numpy())
+    assert all(np.array_equal(b[k].to_numpy(), s.to_numpy()) for k, s in zip((0, 7, 39), single))
+
+
 def _bg_rows(W, D, G, slots):
     """numpy restatement of bg:198-203 (_extract_diagonals) + bg:361-378 (roll, tile, remainder)"""
     j = np.arange(D)
