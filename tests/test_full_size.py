@@ -29,7 +29,9 @@ def test_cfg3_rwkv_block_full_size(require_gpu):
     block = rb.BlockWeights(rng, 1, D, F, H)
     srv = rb.Server(ph, 16384, 36, 3, D)
     run = rb.BlockRunner(srv, block, True)
-    assert srv.ctx.memory_in_use() > 8 * D * 36 * 16384 * 8     # all 8 projections resident
+    # all 8 projections resident: 2048 diagonals each, tiled 4 times in the 8192 slots, so stored compact (N/4
+    # words per limb, fhs_host.hip new_pts_compact) -- 19.3 GB instead of the dense 77.3 GB
+    assert 8 * D * 36 * (16384 // 4) * 8 < srv.ctx.memory_in_use() < 8 * D * 36 * 16384 * 8
     x = rng.standard_normal(D)
     st = (x, np.zeros(D), np.zeros(D), np.zeros((H, 64, 64)), rng.standard_normal(D))
     out = rb.client_aided_block(run, *st)
