@@ -478,6 +478,9 @@ def test_encode_periodic_rows_take_the_sparse_form(ph, N, t):
         else:
             dec = np.array(enc.decode_double_vector(ctx, pt))
         assert np.max(np.abs(dec - want)) < 1e-6
+        # the oracle's decoder (CRT + its own FFT) reads the same slots from these limbs
+        dec_o = o.decode(limbs, 2.0 ** 40)
+        assert np.max(np.abs((dec_o if np.iscomplexobj(want) else dec_o.real) - want)) < 1e-6
     y = np.tile(x, t)
     y[-1] += 1.0
     limbs = enc.encode_double_vector(ctx, y, 2.0 ** 40).to_numpy()
