@@ -631,7 +631,10 @@ static fhs_status new_pts(fhs_context* c, size_t count, int ci, double scale, fh
     for (size_t k = 0; k < count; ++k) outs[k] = nullptr;
     if (count == 0) return FHS_OK;
     if (count == 1) return new_pt(c, ci, scale, outs);
-    const size_t per = (size_t)l * c->N;
+    // FHESPEAR_PT_PAD_WORDS (experiment, default 0): words of padding between a slab's plaintexts (read per call)
+    const char* padv = getenv("FHESPEAR_PT_PAD_WORDS");
+    const size_t pad = padv ? (strtoull(padv, nullptr, 10) + 1) & ~(size_t)1 : 0;
+    const size_t per = (size_t)l * c->N + pad;
     auto* slab = new PtSlab{nullptr, 8 * count * per, 0};
     hipError_t e = dalloc_fit(c, &slab->base, &slab->bytes);
     if (e != hipSuccess) {
