@@ -1931,8 +1931,10 @@ static fhs_status new_pts_compact(fhs_context* c, size_t count, int ci, double s
     }
     return FHS_OK;
 }
+// ss_hint >= 0: the caller knows every row is periodic at tlog >= ss_hint (encode_diag_rows' tiled rows), so the
+// compact factor needs no read-back of the periods (no host wait); -1: read them back.
 static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cnt, size_t n, size_t stride,
-                                  bool is_real, double scale, int ci, fhs_plaintext** outs) {
+                                  bool is_real, double scale, int ci, fhs_plaintext** outs, int ss_hint = -1) {
     const int l = c->L0 + 1 - ci;
     if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
     // fused reduction + NTT through a scratch of rounded coefficients (FHESPEAR_ENCODE_UNFUSED=1: the
@@ -1946,7 +1948,9 @@ static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cn
     if (!unfused) e = dalloc(c, &coef, cbytes);
     if (e == hipSuccess) e = enc_periods(c, dvals, cnt, n, stride, is_real, &tl, &tbytes);
     int ss = 0;
-    if (e == hipSuccess && tl && coef && !no_shadow && c->T.max_qbits <= 59 && cnt >= 32) {
+    if (e == hipSuccess && tl && coef && !no_shadow && c->T.max_qbits <= 59 && cnt >= 32 && ss_hint >= 0) {
+        ss = ss_hint;
+    } else if (e == hipSuccess && tl && coef && !no_shadow && c->T.max_qbits <= 59 && cnt >= 32) {
         std::vector<unsigned char> th(cnt);
         e = hipMemcpyAsync(th.data(), tl, cnt, hipMemcpyDeviceToHost, c->st);
         if (e == hipSuccess) e = hipStreamSynchronize(c->st);
@@ -2045,6 +2049,11 @@ static fhs_status encode_diag_rows(fhs_context* c, const double* M1, const doubl
     if (e == hipSuccess) e = hipStreamSynchronize(c->st);   // caller's buffers may be reused on return
     const double* m1 = reinterpret_cast<const double*>(dm);
     const double* m2 = is_real ? nullptr : reinterpret_cast<const double*>((char*)dm + mb);
+    // the gathered rows repeat with period D (slot j reads column j mod D): periodic at t = n / D when that is a power
+    // of two, so the compact factor is known without reading the detected periods back
+    int ss_hint = 0;
+    if (n % (size_t)D == 0 && ((n / D) & (n / D - 1)) == 0)
+        ss_hint = std::min(__builtin_ctzll((unsigned long long)(n / D)), fhs::encode_sparse_max_log(c->logN));
     const size_t chunk = 2048;
     for (size_t base = 0; e == hipSuccess && st == FHS_OK && base < (size_t)nrows; base += chunk) {
         const size_t cnt = std::min(chunk, (size_t)nrows - base);
@@ -2058,7 +2067,8 @@ static fhs_status encode_diag_rows(fhs_context* c, const double* M1, const doubl
             k += r;
         }
         if (e == hipSuccess)
-            st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci, out + base);
+            st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci, out + base,
+                                 ss_hint);
         dfree(c, dvals, 8 * cnt * stride);
     }
     dfree(c, dm, mb * (is_real ? 1 : 2));
