@@ -1932,9 +1932,11 @@ static fhs_status new_pts_compact(fhs_context* c, size_t count, int ci, double s
     return FHS_OK;
 }
 // ss_hint >= 0: the caller knows every row is periodic at tlog >= ss_hint (encode_diag_rows' tiled rows), so the
-// compact factor needs no read-back of the periods (no host wait); -1: read them back.
+// compact factor needs no read-back of the periods (no host wait); -1: read them back.  rows_known: every row's
+// tlog IS ss_hint >= 1 and only its first (N/2) >> ss_hint values are in HBM (stride apart): no detection either.
 static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cnt, size_t n, size_t stride,
-                                  bool is_real, double scale, int ci, fhs_plaintext** outs, int ss_hint = -1) {
+                                  bool is_real, double scale, int ci, fhs_plaintext** outs, int ss_hint = -1,
+                                  bool rows_known = false) {
     const int l = c->L0 + 1 - ci;
     if (l < 1) return fail(FHS_ERR_LEVEL, "chain index out of range");
     // fused reduction + NTT through a scratch of rounded coefficients (FHESPEAR_ENCODE_UNFUSED=1: the
@@ -1946,7 +1948,13 @@ static fhs_status encode_rows_dev(fhs_context* c, const double* dvals, size_t cn
     size_t tbytes = 0;
     hipError_t e = hipSuccess;
     if (!unfused) e = dalloc(c, &coef, cbytes);
-    if (e == hipSuccess) e = enc_periods(c, dvals, cnt, n, stride, is_real, &tl, &tbytes);
+    if (e == hipSuccess && rows_known) {
+        tbytes = (cnt + 7) & ~(size_t)7;
+        e = dalloc(c, &tl, tbytes);
+        if (e == hipSuccess) e = hipMemsetAsync(tl, ss_hint, cnt, c->st);
+    } else if (e == hipSuccess) {
+        e = enc_periods(c, dvals, cnt, n, stride, is_real, &tl, &tbytes);
+    }
     int ss = 0;
     if (e == hipSuccess && tl && coef && !no_shadow && c->T.max_qbits <= 59 && cnt >= 32 && ss_hint >= 0) {
         ss = ss_hint;
@@ -2039,7 +2047,7 @@ static fhs_status encode_diag_rows(fhs_context* c, const double* M1, const doubl
     if (st != FHS_OK) return st;
     const bool is_real = M2 == nullptr;
     BatchOut bo(out, (size_t)nrows);
-    const size_t mb = 8ull * D * D, stride = is_real ? n : 2 * n;
+    const size_t mb = 8ull * D * D;
     uint64_t *dm = nullptr, *dvals = nullptr;
     HIPCHK(dalloc(c, &dm, mb * (is_real ? 1 : 2)), "encode_diagonals matrix");
     // D rows of D doubles, `ld` apart on the host, packed on the device (no host-side copy of a view)
@@ -2054,22 +2062,30 @@ static fhs_status encode_diag_rows(fhs_context* c, const double* M1, const doubl
     int ss_hint = 0;
     if (n % (size_t)D == 0 && ((n / D) & (n / D - 1)) == 0)
         ss_hint = std::min(__builtin_ctzll((unsigned long long)(n / D)), fhs::encode_sparse_max_log(c->logN));
+    // The sparse encoder reads only each row's first (N/2) >> ss_hint values, so with ss_hint >= 1 only those are
+    // gathered (a whole number of periods) and the periods are not detected: every row takes tlog = ss_hint -- the
+    // largest power-of-two period the detector would find in a row of period D (one with a smaller period, e.g. a
+    // constant diagonal, keeps the same factor; its encoding is the same polynomial up to the FFT's rounding).
+    // FHESPEAR_ENCODE_DENSE=1 / FHESPEAR_ENCODE_UNFUSED=1 keep the full rows and the detector.
+    static const bool full_rows = getenv("FHESPEAR_ENCODE_DENSE") || getenv("FHESPEAR_ENCODE_UNFUSED");
+    const bool known = ss_hint >= 1 && !full_rows;
+    const size_t ng = known ? n >> ss_hint : n, gstride = is_real ? ng : 2 * ng;
     const size_t chunk = 2048;
     for (size_t base = 0; e == hipSuccess && st == FHS_OK && base < (size_t)nrows; base += chunk) {
         const size_t cnt = std::min(chunk, (size_t)nrows - base);
-        e = dalloc(c, &dvals, 8 * cnt * stride);
+        e = dalloc(c, &dvals, 8 * cnt * gstride);
         if (e != hipSuccess) break;
         for (size_t k = 0; e == hipSuccess && k < cnt;) {   // one gather per run of consecutive rows
             size_t r = 1;
             while (k + r < cnt && rows[base + k + r] == rows[base + k] + (int)r) ++r;
-            e = fhs::launch_diag_gather(m1, m2, D, G, (int)n, rows[base + k], (int)r, trans ? 1 : 0,
-                                        reinterpret_cast<double*>(dvals) + k * stride, c->st);
+            e = fhs::launch_diag_gather(m1, m2, D, G, (int)ng, rows[base + k], (int)r, trans ? 1 : 0,
+                                        reinterpret_cast<double*>(dvals) + k * gstride, c->st);
             k += r;
         }
         if (e == hipSuccess)
-            st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, stride, is_real, scale, ci, out + base,
-                                 ss_hint);
-        dfree(c, dvals, 8 * cnt * stride);
+            st = encode_rows_dev(c, reinterpret_cast<const double*>(dvals), cnt, n, gstride, is_real, scale, ci,
+                                 out + base, ss_hint, known);
+        dfree(c, dvals, 8 * cnt * gstride);
     }
     dfree(c, dm, mb * (is_real ? 1 : 2));
     if (e != hipSuccess) return hip_fail(e, "encode_diagonals");
