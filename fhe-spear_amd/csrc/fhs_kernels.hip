@@ -551,10 +551,106 @@ __global__ void __launch_bounds__((ntt_threads<LOGN, H>())) k_rescale_ntt(DevTab
                                [&](int e) { return submod(reduce64(src[e], P), hq, q); },
                                [&](int e, u64 t) { o[e] = shoup(submod(a[e], t, q), inv, inv_s, q); });
 }
+// N = 32768: a rescale is two latency-bound launches (2 and 2 (l - 1) workgroups, each transforming a whole limb as
+// two halves in turn).  Here every half gets its own workgroup -- twice the workgroups, half the serial work each:
+// (a) k_rescale_intt_hs: the last limb's INTT up to its final two stages, per half (inv_limb's iteration h), the
+//     thread's 16 rows to `pre` ([comp][half][row][thread]: the scratch's 2 N words);
+// (b) k_rescale_ntt_hs, per (target limb, comp, half): for the thread's column the INTT's last two stages
+//     (inv_quad_last2, as inv_limb), k_rescale_intt's + floor(q_last/2) and k_rescale_ntt's conversion, the forward
+//     NTT's first three stages (fwd_oct_first3, as fwd_limb: its row groups c, c+4, c+8, c+12 are the INTT quads c and
+//     c+4), then only this half's LDS passes and stores.  The same operations on the same values: identical limbs.
+template <int LOGN>
+__global__ void __launch_bounds__((ntt_threads<LOGN, true>())) k_rescale_intt_hs(DevTables T, const u64* in, u64* pre,
+                                                                             int l) {
+    constexpr int N = 1 << LOGN, TH = N / 32;
+    static_assert(!(FHS_NTT_WAVELOCAL && (LOGN - 2) % 3 == 0), "plain half loads (inv_limb's non-wave-local head)");
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN, true>()];
+    const int h = blockIdx.x, comp = blockIdx.y, pi = l - 1, tid = threadIdx.x;
+    const PrimeK& P = PK(T, pi);
+    const u64* src = in + ((size_t)comp * l + pi) * N + (size_t)h * (N / 2);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = src[tid + c * TH];
+    __syncthreads();
+    ntt_inv_half_lds<LOGN - 1, 3, 16, 1, false>(lds, tid, T.tw_inv + (size_t)pi * N * 2, P.q, 1 + h);
+    u64* o = pre + ((size_t)comp * 2 + h) * 16 * TH + tid;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) o[(size_t)c * TH] = lds[row_pad<TH>(tid, c)];
+}
+template <int LOGN>
+__global__ void __launch_bounds__((ntt_threads<LOGN, true>())) k_rescale_ntt_hs(DevTables T, const u64* in, const u64* pre,
+                                                                            u64* out, int l) {
+    static_assert(FHS_FWD_FIRST3 && fwd_first3<LOGN>(), "the column's forward first stages in radix-8 groups");
+    constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
+    __shared__ __attribute__((aligned(16))) u64 lds[ntt_lds_words<LOGN, true>()];
+    const int i = blockIdx.x, comp = blockIdx.y, g = blockIdx.z, tid = threadIdx.x;
+    const PrimeK& P = PK(T, i);
+    const RedU RU = redu(P);
+    const u64* rs = T.rescale + ((size_t)l * T.L0 + i) * 4;   // inv, inv_s, half mod q_i
+    const u64 inv = rs[0], inv_s = rs[1], hq = rs[2], q = RU.q;
+    const PrimeK& PL = PK(T, l - 1);
+    const u64 qL = PL.q, halfL = qL >> 1;
+    const u64* twL = T.tw_inv + (size_t)(l - 1) * N * 2;
+    const u64* tw = T.tw_fwd + (size_t)i * N * 2;
+    const u64* pr = pre + (size_t)comp * 2 * 16 * TH + tid;
+    auto conv = [&](u64 y) { return submod(reduce64(addmod(csub(y, qL), halfL, qL), P), hq, q); };
+    u64 hi[16];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        u64 x[8];   // x[m] = half 0 row c + 4m, x[4 + m] = half 1 row c + 4m (fwd_limb's F3 loads)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {   // INTT quad r = c + 4j: rows r, r + 8 of both halves
+            const int r = c + 4 * j;
+            u64 y[4] = {pr[(size_t)r * TH], pr[(size_t)(r + 8) * TH], pr[(size_t)(16 + r) * TH], pr[(size_t)(24 + r) * TH]};
+            inv_quad_last2(y, twL, qL, PL.ninv, PL.ninv_s, PL.w1ninv, PL.w1ninv_s);
+            x[j] = conv(y[0]);
+            x[j + 2] = conv(y[1]);
+            x[4 + j] = conv(y[2]);
+            x[6 + j] = conv(y[3]);
+        }
+        fwd_oct_first3<TH>(x, tw, q, RU.lazy, lds, tid, c, hi);
+    }
+    if (g) {   // the upper half's rows from registers (each thread overwrites only its own rows)
+#pragma unroll
+        for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
+    }
+    __syncthreads();
+    const u64* a = in + ((size_t)comp * l + i) * N;
+    u64* o = out + ((size_t)comp * (l - 1) + i) * N;
+    constexpr bool WLX = FHS_NTT_WAVELOCAL && fwd_exit_wave_local<LOGN - 1, 3, 2>();
+    ntt_fwd_lds<LOGN - 1, 3, 16, 2, WLX>(lds, tid, tw, q, RU.lazy, 1 + g);
+    if constexpr (WLX) {
+        const int wb = wl_base<LOGN - 1, 16, 8>(tid), wp = lds_pad(wb);
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int off = wl_off<LOGN - 1, 16, 8>(c);
+            const int e = g * NH + wb + off;
+            o[e] = shoup(submod(a[e], fwd_canon(lds[wp + off + off / 16], RU), q), inv, inv_s, q);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            const int e = g * NH + tid + c * TH;
+            o[e] = shoup(submod(a[e], fwd_canon(lds[row_pad<TH>(tid, c)], RU), q), inv, inv_s, q);
+        }
+    }
+}
+#ifndef FHS_RESCALE_SPLIT
+#define FHS_RESCALE_SPLIT 1   // 0: the one-workgroup-per-limb rescale at N = 32768 too (A/B and test knob)
+#endif
 hipError_t launch_rescale(const DevTables& T, const u64* in, u64* out, u64* scratch, int ncomp, int l,
                           hipStream_t st, const KTimer* tm) {
     FHS_TMARK(tm, KID_RESCALE, 1, st);
+    static const bool split_off = getenv("FHESPEAR_RESCALE_UNSPLIT") != nullptr;
     FHS_DISPATCH_LOGN(T.logN, {
+        if constexpr (LOGN == 15 && FHS_RESCALE_SPLIT) {
+            if (!split_off && ncomp <= 2) {
+                hipLaunchKernelGGL((k_rescale_intt_hs<LOGN>), dim3(2, ncomp), dim3(ntt_threads<LOGN, true>()), 0, st, T,
+                                   in, scratch, l);
+                hipLaunchKernelGGL((k_rescale_ntt_hs<LOGN>), dim3(l - 1, ncomp, 2), dim3(ntt_threads<LOGN, true>()), 0, st,
+                                   T, in, scratch, out, l);
+                break;
+            }
+        }
         FHS_NTT_LAUNCH(k_rescale_intt, ncomp, dim3(ncomp), st, T, in, scratch, l);
         FHS_NTT_LAUNCH(k_rescale_ntt, (l - 1) * ncomp, dim3(l - 1, ncomp), st, T, in, scratch, out, l);
     });
