@@ -634,6 +634,9 @@ __global__ void __launch_bounds__((ntt_threads<LOGN, true>())) k_rescale_ntt_hs(
         }
     }
 }
+#ifndef FHS_SPLIT_MAX_WG
+#define FHS_SPLIT_MAX_WG 256   // below this many workgroups a launch is latency-bound: one workgroup per half-limb
+#endif
 #ifndef FHS_RESCALE_SPLIT
 #define FHS_RESCALE_SPLIT 1   // 0: the one-workgroup-per-limb rescale at N = 32768 too (A/B and test knob)
 #endif
@@ -1544,16 +1547,19 @@ __device__ __forceinline__ void moddown_convert3x(const u64* y, const u64* xt, c
 
 // k_moddown with half the limb in LDS (see k_modup_h): conversion of both coefficients of each
 // (e, e + N/2) pair, global NTT stage 0 in registers, then each half transformed in LDS and finished
-// ((acc - conv) P^-1 + sigma(c0)).  Same values as k_moddown.
-template <int LOGN, bool MX, bool B59 = false>
+// ((acc - conv) P^-1 + sigma(c0)).  Same values as k_moddown.  SPLIT (launches with few workgroups: a single key
+// switch's ModDown, latency-bound): two workgroups per (limb, component, item), each converting the whole column
+// and transforming and finishing one half -- twice the workgroups, half the serial work each (as k_rescale_ntt_hs).
+template <int LOGN, bool MX, bool B59 = false, bool SPLIT = false>
 __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, const KsItem* items, const u64* acc,
                                                                    const u64* ycoef, int l, int R) {
     constexpr int N = 1 << LOGN, NH = N / 2, TH = N / 32;
     __shared__ __attribute__((aligned(16))) u64 lds[(1 << (LOGN - 1)) + (1 << (LOGN - 1)) / 16];
     const int tid = threadIdx.x;
     const int P_ = T.P, E = l + P_;
-    int i, mm;
-    if (!plain_tm(l, 2 * R, i, mm)) return;
+    const int bx = SPLIT ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, hg = SPLIT ? (int)(blockIdx.x & 1) : 0;
+    const int i = bx % l, mm = bx / l;
+    if (mm >= 2 * R) return;
     const int comp = mm & 1, r = mm >> 1;
     const PrimeK& P = PK(T, i);
     const RedU RU = redu(P);
@@ -1607,8 +1613,8 @@ __global__ void __launch_bounds__((1 << LOGN) / 32, 4) k_moddown_h(DevTables T, 
     u64* o = (comp == 0 ? it.out0 : it.out1) + (size_t)i * N;
     const u64* ac = acc + (((size_t)r * 2 + comp) * E + i) * N;
 #pragma unroll 1
-    for (int h = 0; h < 2; ++h) {
-        if (h) {
+    for (int h = hg; h < (SPLIT ? hg + 1 : 2); ++h) {
+        if (h) {   // (SPLIT, upper half: each thread overwrites only its own rows; the barrier is harmless)
             __syncthreads();
 #pragma unroll
             for (int c = 0; c < 16; ++c) lds[row_pad<TH>(tid, c)] = hi[c];
@@ -1803,10 +1809,16 @@ template <int LOGN>
 static hipError_t launch_moddown(const DevTables& T, const KsItem* it, u64* acc, u64* ycoef, int l, int R, hipStream_t st,
                                  const KTimer* tm) {
     FHS_TMARK(tm, KID_MODDOWN, 1, st);
+    // a single key switch's ModDown at N = 32768 (few workgroups): one workgroup per half (SPLIT)
+    static const bool split_off = getenv("FHESPEAR_MODDOWN_UNSPLIT") != nullptr;
+    const bool split = LOGN == 15 && !split_off && l * 2 * R < FHS_SPLIT_MAX_WG;
     if ((FHS_MODDOWN_HALF && LOGN >= 9) || ntt_half<LOGN>()) {
         if (T.md_xform) {   // the special digit to its X form, then the two-product conversion
             hipLaunchKernelGGL(k_special_x, dim3((T.N + 255) / 256, 2 * R), dim3(256), 0, st, T, ycoef, 2 * R);
-            if (T.conv_b59)
+            if (T.conv_b59 && split)
+                hipLaunchKernelGGL((k_moddown_h<LOGN, true, true, true>), dim3(2 * l * 2 * R), dim3((1 << LOGN) / 32), 0,
+                                   st, T, it, acc, ycoef, l, R);
+            else if (T.conv_b59)
                 hipLaunchKernelGGL((k_moddown_h<LOGN, true, true>), dim3(l * 2 * R), dim3((1 << LOGN) / 32), 0, st, T,
                                    it, acc, ycoef, l, R);
             else
